@@ -1,0 +1,206 @@
+/*
+ * macm.h — C-ABI of the MI355X-native batched gym-macm stepper (libmacm_hip.so).
+ *
+ * What this replaces (reference = siyarvurucu/gym-macm, file:line):
+ *   - the per-env Box2D world owned by FrameworkBase
+ *       gym_macm/cm_framework.py:155-167  (b2World(gravity=(0,0), doSleep=True))
+ *       gym_macm/backends/no_render.py:4-19 (NoRender, the headless framework)
+ *   - the body construction loop of Flock.__init__      gym_macm/envs/mvmnt.py:35-79
+ *   - the whole env.step hot path                        gym_macm/envs/mvmnt.py:81-140
+ *       action -> angle/force (:97-129), FrameworkBase.Step -> b2World.Step(1/60,8,3)
+ *       + ClearForces (cm_framework.py:172-225), get_rewards (:160-179),
+ *       time/done (:134-136), get_obs (:181-222)
+ *
+ * The reference's "API" at this boundary is pybox2d (SWIG) called per agent from
+ * Python. Here one call advances E independent envs of N agents each, with all
+ * per-agent arrays on the device (SoA), so control crosses host->device once per
+ * step. No torch / C++ types cross this ABI: plain pointers, sizes, POD structs.
+ *
+ * Conventions
+ *   - Every function returns int status: MACM_OK (0) or a negative MACM_E_* code;
+ *     macm_last_error() returns a thread-local message for the last failure.
+ *     Nothing aborts or throws across the ABI.
+ *   - "device pointer" = memory the HIP runtime can dereference in a kernel
+ *     (hipMalloc / torch CUDA tensor data_ptr()). Output buffers are borrowed for
+ *     the duration of the call only; the world owns its state.
+ *   - stream = hipStream_t passed as void* (NULL = default stream). Calls are
+ *     asynchronous on that stream; completion is the caller's synchronisation.
+ *   - A world is bound to one device. Calls on one world are not thread-safe.
+ */
+#ifndef MACM_H
+#define MACM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MACM_ABI_VERSION 1
+
+enum {
+  MACM_OK = 0,
+  MACM_E_INVALID = -1,     /* bad argument / config                          */
+  MACM_E_OOM = -2,         /* device allocation failed                       */
+  MACM_E_HIP = -3,         /* HIP runtime error                              */
+  MACM_E_UNSUPPORTED = -4, /* config valid for the reference, not built here */
+  MACM_E_OVERFLOW = -5     /* a per-env capacity (contacts/islands) overflowed */
+};
+
+enum { MACM_ACTION_DISCRETE = 0, MACM_ACTION_CONTINUOUS = 1 };
+enum { MACM_REWARD_BINARY = 0, MACM_REWARD_LINEAR = 1 };
+enum { MACM_COORD_POLAR = 0, MACM_COORD_CARTESIAN = 1 };
+
+/* Status bits accumulated per env on the device (macm_world_status). */
+enum {
+  MACM_ST_CONTACT_OVERFLOW = 1, /* Ov(F_t) list exceeded max_contacts            */
+  MACM_ST_TOUCH_OVERFLOW = 2,   /* touching contacts exceeded the solver capacity */
+  MACM_ST_DEGREE_OVERFLOW = 4   /* a body touched more bodies than the adjacency cap */
+};
+
+/*
+ * macm_config — flockSettings (gym_macm/settings.py:110-146) + fwSettings
+ * (settings.py:25-59) flattened. Field names follow the reference's attribute
+ * names. macm_config_default() fills the reference defaults.
+ */
+typedef struct macm_config {
+  int32_t n_agents;            /* sum(n_agents)                     mvmnt.py:61      */
+  int32_t n_targets;           /* len(np.unique(targets))           mvmnt.py:42      */
+  int32_t action_mode;         /* "discrete"/"continuous"           settings.py:136  */
+  int32_t reward_mode;         /* "binary"/"linear"                 settings.py:137  */
+  int32_t coord;               /* "polar"/"cartesian"               settings.py:141  */
+  int32_t velocity_iterations; /* 8                                 settings.py:31   */
+  int32_t position_iterations; /* 3                                 settings.py:32   */
+  int32_t warm_starting;       /* enableWarmStarting = True         settings.py:34   */
+  int32_t obs_f64;             /* 0: obs written as float32, 1: float64              */
+  int32_t _pad0;
+  double hz;                   /* 60.0                              settings.py:30   */
+  double start_spread;         /* 20                                settings.py:119  */
+  double start_point[2];       /* [0, 0]                            settings.py:120  */
+  double agent_rotation_speed; /* 0.8 * 2pi                         settings.py:121  */
+  double agent_force;          /* 20                                settings.py:122  */
+  double time_limit;           /* 60                                settings.py:123  */
+  double reward_radius;        /* 7 if binary else 1                settings.py:146  */
+  double target_mindist;       /* 25                                settings.py:139  */
+  double target_maxdist;       /* 60                                settings.py:140  */
+  float radius;                /* circle r = 0.5                    settings.py:127-131 */
+  float density;               /* 1                                                  */
+  float friction;              /* 0.3                                                */
+  float linear_damping;        /* 5                                 settings.py:133  */
+} macm_config;
+
+/*
+ * Device-side outputs of one step (all device pointers; NULL = not wanted,
+ * except reward which is required). Shapes: E = n_envs, N = n_agents,
+ * OD = 4 (polar: nbr r, nbr t, target r, target t) or 6 (cartesian: nbr r,
+ * cos t, sin t, target r, cos t, sin t). Matches Flock.get_obs node order
+ * (mvmnt.py:197-220): node 0 = closest agent (type 0, id = nbr_id), node 1 =
+ * the agent's target (type 1, id = N).
+ */
+typedef struct macm_outputs {
+  void* obs;        /* [E, N, OD] float32 or float64 (config.obs_f64)          */
+  int32_t* nbr_id;  /* [E, N] index of the closest other agent                 */
+  float* reward;    /* [E, N] -1 in any contact, else binary 0/1 or linear     */
+  uint8_t* collided;/* [E, N] 1 if the agent is in world.contacts              */
+  uint8_t* done;    /* [E] time_passed > time_limit                            */
+} macm_outputs;
+
+/*
+ * World state, SoA. Used by get/set_state (parity injection, checkpoints).
+ * Pointers may be host or device memory (copied with hipMemcpyDefault).
+ *   pos, vel      [E, N, 2] float32   body position (sweep c) / linear velocity
+ *   angle         [E, N]    float32   sweep angle
+ *   fat           [E, N, 4] float32   broad-phase fat AABB (lo.x, lo.y, hi.x, hi.y)
+ *   sleep         [E, N]    float32   sleepTime
+ *   targets       [E, T, 2] float32
+ *   contact_count [E]       int32     length of the ordered contact list
+ *   contact_ab    [E, C]    uint32    a | b << 16, a < b, Box2D world-list order
+ *   contact_imp   [E, C, 2] float32   (normalImpulse, tangentImpulse) warm start
+ *   step_count    [E]       int32     steps taken (0 => dtRatio 0 on next step)
+ *   time_passed   [E]       float64
+ * C = macm_world_info().max_contacts.
+ */
+typedef struct macm_state {
+  void* pos;
+  void* vel;
+  void* angle;
+  void* fat;
+  void* sleep;
+  void* targets;
+  void* contact_count;
+  void* contact_ab;
+  void* contact_imp;
+  void* step_count;
+  void* time_passed;
+} macm_state;
+
+typedef struct macm_world_info {
+  int32_t n_envs, n_agents, n_targets, obs_dim;
+  int32_t max_contacts;   /* per-env ordered contact list capacity */
+  int32_t max_touching;   /* per-env solver capacity               */
+  int32_t device;
+  int32_t _pad;
+} macm_world_info;
+
+typedef struct macm_world macm_world;
+
+/* Library identity. */
+const char* macm_version(void);
+int macm_abi_version(void);
+const char* macm_last_error(void);
+
+/* Reference defaults (settings.py:25-59, 110-146). */
+int macm_config_default(macm_config* cfg);
+
+/*
+ * Create E envs of one Flock configuration on `device`.
+ *   targets_idx: host int32[N], agent -> target index (mvmnt.py:43), or NULL = all 0.
+ *   max_contacts: per-env ordered contact list capacity, 0 = N(N-1)/2 (never overflows).
+ * Replaces: Flock.__init__ world + body creation (mvmnt.py:35-79,
+ * cm_framework.py:155-167). State is undefined until macm_world_reset.
+ */
+int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_t n_envs,
+                      int32_t device, int32_t max_contacts, macm_world** out);
+int macm_world_destroy(macm_world* w);
+int macm_world_info_get(const macm_world* w, macm_world_info* info);
+
+/*
+ * Initialise every env exactly as Flock.__init__ would after
+ * random.seed(seed + env_offset + e) (CPython MT19937; mvmnt.py:47-79 draw order:
+ * targets (angle, dist) then agents (x, y, angle)). Resets time, contacts, status.
+ * Writes the initial observation (Flock.obs, mvmnt.py:79) into `out` if non-NULL.
+ */
+int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const macm_outputs* out,
+                     void* stream);
+
+/*
+ * One env.step for all E envs.
+ *   actions: device pointer. Discrete: uint8/int8 [E, N, 3] in {0,1,2}
+ *   (MultiDiscrete([3,3,3]), mvmnt.py:143-145). Continuous: float32 [E, N, 2] in [-1,1].
+ * Replaces Flock.step (mvmnt.py:81-140) incl. b2World.Step(1/hz, 8, 3) + ClearForces.
+ */
+int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream);
+
+/* Observation of the current state without stepping (Flock.get_obs, mvmnt.py:181-222). */
+int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream);
+
+/* Copy state out / in (synchronous w.r.t. `stream`). */
+int macm_world_get_state(macm_world* w, const macm_state* dst, void* stream);
+int macm_world_set_state(macm_world* w, const macm_state* src, void* stream);
+
+/* OR over envs of the per-env status bits (synchronises `stream`). */
+int macm_world_status(macm_world* w, int32_t* status_or, void* stream);
+
+/*
+ * Per-world counters, accumulated on device by every step (synchronises `stream`):
+ *   out[0] agent-steps, out[1] collided agent-steps, out[2] positive-reward
+ *   agent-steps, out[3] env-steps with done set. Used for the RCCL all-reduce
+ *   in multi-GPU runs. reset_counters zeroes them.
+ */
+int macm_world_counters(macm_world* w, int64_t out[4], void* stream);
+int macm_world_reset_counters(macm_world* w, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MACM_H */
