@@ -1,0 +1,197 @@
+"""bench.py — agent·steps/sec of the cm-flock-v0 step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One "step" = one env.step of every env on this rank: one HIP launch of
+flock_step_w64 over E envs x N agents (physics + rewards + observations), with
+the actions pre-generated on the device (uniform {0,1,2}^3 uint8, the
+MultiDiscrete([3,3,3]) action space) and outputs written to device tensors.
+Weak scaling: every rank runs its own E envs (global env ids rank*E .. rank*E+E-1),
+no collective on the data path; one all-reduce of counters after the timed region.
+
+Rank 0 prints ONE JSON line. `roofline` prices the step kernel against HBM with the
+algorithmic bytes of SURVEY.md §8(d) (B_alg = 107 B per agent-step); `cpu_baseline`
+times the CPU oracle (oracle/, a C restatement of the reference's path) on this
+host's cores over a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gym-macm_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+B_ALG = 107  # bytes per agent-step: state r+w 2x40, action 3, obs 20, reward 4
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n_agents, seed, budget_s=15.0):
+    """Time the CPU oracle on this host (OpenMP over envs) on a bounded sample."""
+    from oracle import OracleFlock
+    from gym_macm.settings import flockSettings, to_config
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    E = max(4 * threads, 64)
+    cfg = to_config(flockSettings(), n_agents, 1, obs_f64=True)
+    orc = OracleFlock(cfg, None, E, seed)
+    rng = np.random.default_rng(seed + 1)
+    bufs = dict(obs=np.zeros((E, n_agents, 4), np.float64), nbr_id=np.zeros((E, n_agents), np.int32),
+                reward=np.zeros((E, n_agents), np.float64))
+    pre = [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(8)]
+    t0 = time.perf_counter()
+    for a in pre[:3]:
+        orc.step_raw(a, bufs, threads)
+    per_step = (time.perf_counter() - t0) / 3
+    steps = int(max(10, min(3000, budget_s / max(per_step, 1e-6))))
+    acts = [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(16)]
+    t0 = time.perf_counter()
+    for s in range(steps):
+        orc.step_raw(acts[s % 16], bufs, threads)
+    dt = time.perf_counter() - t0
+    return dict(value=E * n_agents * steps / dt, unit="agent·steps/s", cores=threads, kind="port",
+                sample=f"oracle/ C restatement, {E} envs x {n_agents} agents x {steps} steps (after 3 "
+                       f"warm-up steps) from reset, uniform random discrete actions, OpenMP {threads} threads, "
+                       f"{dt:.1f} s")
+
+
+def load_traffic(path):
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        j = json.load(f)
+    return j
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=0x6D61636D)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_flock_step.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from gym_macm.vec import FlockVec
+
+    E, N, K, W = args.envs, args.agents, args.steps, args.warmup
+    vec = FlockVec(E, n_agents=[N], seed=args.seed, env_offset=rank * E, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + 1 + rank)
+    acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    step = vec.world.step_raw
+    base = acts.data_ptr()
+    stride = E * N * 3
+    log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}")
+    for w in range(W):
+        step(base + w * stride, sh)
+    torch.cuda.synchronize(dev)
+    vec.world.reset_counters()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(K):
+        step(base + (W + k) * stride, sh)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kernel_ms = ev0.elapsed_time(ev1) / K  # per launch, on the launch stream
+    status = vec.status()
+    cnt = torch.tensor(vec.counters(), dtype=torch.int64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        st = torch.tensor([status], dtype=torch.int32, device=dev)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        status = int(st.item())
+    elapsed = float(el.item())
+    cnt = cnt.cpu().numpy()
+    total_agent_steps = world * E * N * K
+    assert int(cnt[0]) == total_agent_steps, (cnt, total_agent_steps)
+    if status != 0:
+        raise RuntimeError(f"device status bits {status}: a capacity overflowed, results invalid")
+    value = total_agent_steps / elapsed
+
+    if rank == 0:
+        achieved_gbs = B_ALG * E * N / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        tj = load_traffic(args.traffic_json)
+        if tj and tj.get("envs") == E and tj.get("agents") == N:
+            traffic = tj.get("hbm_bytes_per_launch")
+        with open(os.path.join(REPO, "BASELINE.json")) as f:
+            metric = json.load(f)["metric"]
+        out = {
+            "metric": metric,
+            "value": value,
+            "unit": "agent·steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"cm-flock-v0 n_agents=[{N}] x {E} envs per GPU, uniform random discrete actions "
+                            f"(MultiDiscrete[3,3,3]) pre-generated on device, from reset (seed {args.seed:#x})",
+                "envs_per_gpu": E, "n_agents": N, "total_envs": E * world,
+                "parallelism": f"env-sharded x{world} (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "flock_step_w64<float>", "kernel_ms": kernel_ms,
+                "bytes_alg_per_launch": B_ALG * E * N,
+            },
+            "counters": {"agent_steps": int(cnt[0]), "collided_agent_steps": int(cnt[1]),
+                         "positive_reward_agent_steps": int(cnt[2]), "done_env_steps": int(cnt[3])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline (oracle) ...")
+            out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,68 @@
+// flock_common.hpp — shared device/host definitions for the batched Flock stepper.
+//
+// Arithmetic contract: every float expression that mirrors Box2D keeps Box2D's
+// operand order and is compiled with -ffp-contract=off, so each op rounds exactly
+// as Box2D's SSE2 (no-FMA) build does. Double expressions mirror the reference's
+// numpy/Python double math (gym_macm/envs/mvmnt.py) in the same order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/macm.h"
+
+namespace macm {
+
+// Box2D 2.3 b2Settings.h constants used on the path.
+constexpr float kEps = 1.1920928955078125e-07f;  // FLT_EPSILON
+constexpr float kLinearSlop = 0.005f;
+constexpr float kAabbExtension = 0.1f;
+constexpr float kAabbMultiplier = 2.0f;
+constexpr float kMaxTranslation = 2.0f;
+constexpr float kBaumgarte = 0.2f;
+constexpr float kMaxLinearCorrection = 0.2f;
+constexpr float kTimeToSleep = 0.5f;
+constexpr float kLinearSleepTol = 0.01f;
+constexpr float kPi32 = 3.14159265359f;  // b2_pi
+
+// Per-launch parameters derived on the host from macm_config exactly as the
+// reference derives them (Python double arithmetic / SWIG float conversion).
+struct StepParams {
+  int32_t n_envs, n_agents, n_targets, max_contacts;
+  int32_t vel_iters, pos_iters, warm_starting;
+  int32_t action_mode, reward_mode, coord;
+  float dt;          // fl32(1.0 / hz)                       cm_framework.py:182-185 -> world.Step
+  float inv_dt;      // 1.0f / dt                            b2World::Step
+  float inv_mass;    // 1 / (density * b2_pi * r * r)        b2CircleShape::ComputeMass
+  float damp;        // 1 / (1 + dt * linearDamping)         b2Island::Solve
+  float radius;      // circle radius
+  float friction;    // b2MixFriction = sqrtf(f * f)
+  float force_f32;   // (float)agent_force (continuous mode: numpy float32 * int)
+  float _padf;
+  double rot_step;   // rotation_speed, multiplied as ((a2-1) * rot) * (1/hz)   mvmnt.py:103-104
+  double inv_hz;     // 1 / hz (Python float division)                       mvmnt.py:104,134
+  double force;      // agent_force (double)                                 mvmnt.py:113-116
+  double diag_c;     // 1 / np.sqrt(2)                                       mvmnt.py:112
+  double reward_radius;
+  double time_limit;
+};
+
+struct WorldBuffers {
+  float2* pos;         // [E, N]
+  float2* vel;         // [E, N]
+  float* angle;        // [E, N]
+  float4* fat;         // [E, N]   (lo.x, lo.y, hi.x, hi.y)
+  float* sleep;        // [E, N]
+  float2* targets;     // [E, T]
+  int32_t* tidx;       // [N]
+  int32_t* ccount[2];  // [E]      double-buffered ordered contact list
+  uint32_t* cab[2];    // [E, C]   a | b << 16
+  float2* cimp[2];     // [E, C]   (normalImpulse, tangentImpulse)
+  int32_t* step_count; // [E]
+  double* time_passed; // [E]
+  uint8_t* done;       // [E]
+  int32_t* status;     // [E]      MACM_ST_* bits
+  unsigned long long* counters;  // [4]
+};
+
+}  // namespace macm

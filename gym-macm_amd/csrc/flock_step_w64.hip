@@ -1,0 +1,743 @@
+// flock_step_w64.hip — batched Flock env.step for N <= 64 agents per env on gfx950.
+//
+// One 64-lane wavefront advances one env; lane i owns agent i. Per-env state is
+// staged in LDS for the duration of the step (≈11 KB) and written back once.
+// The step restates, in one launch:
+//   action -> angle/force                gym_macm/envs/mvmnt.py:97-129
+//   b2World::Step(1/hz, 8, 3)            gym_macm/cm_framework.py:222-223 [EXT-B2D]
+//     Collide (contact persistence, circle manifolds, warm-start carry)
+//     island DFS in Box2D order, integrate velocities + damping,
+//     sequential-impulse velocity solve (warm start + 8 iterations),
+//     integrate positions, position solve (<= 3 iterations, early exit),
+//     sleep, SynchronizeFixtures (fat-AABB hysteresis), FindNewContacts
+//   ClearForces                           cm_framework.py:224
+//   get_rewards                           mvmnt.py:160-179
+//   time / done                           mvmnt.py:134-136
+//   get_obs                               mvmnt.py:181-222
+//
+// Box2D-order representation. Box2D keeps contacts in a world list and per-body
+// edge lists, both prepend-on-create; its island DFS walks bodies in reverse
+// creation order and each body's edges most-recent-first, and the Gauss-Seidel
+// sweep follows that order. Here each env carries ONE ordered array of the
+// contacts that survive the next Collide (the pairs whose current fat AABBs
+// overlap): each step prepends the newly created pairs in descending (a, b)
+// order (FindNewContacts sorts pairs ascending and prepends each) and keeps the
+// surviving old pairs in their order. A body's edge list is then this array
+// restricted to the body's contacts, so the DFS below visits contacts in exactly
+// Box2D's order and the solver reproduces Box2D's rounding sequence.
+//
+// Exactness notes (checked by tests/test_gpu_parity.py against the oracle):
+//   * fixedRotation bodies have invI = 0 and w = 0, so every angular term in the
+//     solver is a signed zero; dropping them can change only the sign of a zero
+//     velocity/impulse component, never a nonzero value or any position.
+//   * circles sit at the body origin, so b2Mul(xf, m_p) == position exactly.
+#include "flock_common.hpp"
+
+namespace macm {
+
+constexpr int W = 64;       // wavefront = envs' agent lanes
+constexpr int TCAP = 256;   // touching contacts per env held in LDS
+constexpr int DEG = 16;     // touching contacts per body
+constexpr int ICAP = W / 2; // islands with >= 1 contact (>= 2 bodies each)
+
+__device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }  // b2Min
+__device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }  // b2Max
+__device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
+
+// b2TestOverlap
+__device__ __forceinline__ bool overlap(float4 a, float4 b) {
+  const float d1x = b.x - a.z, d1y = b.y - a.w;
+  const float d2x = a.x - b.z, d2y = a.y - b.w;
+  if (d1x > 0.0f || d1y > 0.0f) return false;
+  if (d2x > 0.0f || d2y > 0.0f) return false;
+  return true;
+}
+
+// b2Vec2::Normalize
+__device__ __forceinline__ void normalize(float& x, float& y) {
+  const float len = sqrtf(x * x + y * y);
+  if (len < kEps) return;
+  const float inv = 1.0f / len;
+  x *= inv;
+  y *= inv;
+}
+
+__device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
+
+// t = t - np.sign(t) * 2 * np.pi if np.abs(t) > np.pi else t      (mvmnt.py:199,214)
+__device__ __forceinline__ double wrap_pi(double t) {
+  return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t;
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+template <typename OT>
+__device__ __forceinline__ void write_node(OT* o, int coord, double r, double t) {
+  if (coord == MACM_COORD_CARTESIAN) {
+    o[0] = (OT)r;
+    o[1] = (OT)cos(t);
+    o[2] = (OT)sin(t);
+  } else {
+    o[0] = (OT)r;
+    o[1] = (OT)t;
+  }
+}
+
+// Flock.get_obs for agent `lane` given final positions in LDS (mvmnt.py:181-222).
+// best/bj: squared distance and index of the closest other agent.
+template <typename OT>
+__device__ __forceinline__ void write_obs(const StepParams& P, OT* obs_e, int lane, float cx, float cy,
+                                          float ang, float best, int bj, const float* s_cx,
+                                          const float* s_cy, float tdx, float tdy, float td2) {
+  const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+  OT* o = obs_e + (size_t)lane * od;
+  const float rx = s_cx[bj] - cx, ry = s_cy[bj] - cy;  // other.position - agent.position (f32)
+  double t = atan2((double)ry, (double)rx) - (double)ang;
+  write_node(o, P.coord, sqrt((double)best), wrap_pi(t));
+  t = atan2((double)tdy, (double)tdx) - (double)ang;
+  write_node(o + od / 2, P.coord, sqrt((double)td2), wrap_pi(t));
+}
+
+// Nearest other agent by float32 squared distance, strict '<' (lowest index wins
+// ties; the reference compares sqrt() values, a strictly monotone map of these).
+__device__ __forceinline__ void nearest(int N, int lane, float cx, float cy, const float* s_cx,
+                                        const float* s_cy, float& best, int& bj) {
+  best = __builtin_inff();
+  bj = lane == 0 ? 1 : 0;
+  for (int j = 0; j < N; ++j) {
+    const float dx = s_cx[j] - cx, dy = s_cy[j] - cy;
+    const float d2 = dx * dx + dy * dy;
+    if (j != lane && d2 < best) {
+      best = d2;
+      bj = j;
+    }
+  }
+}
+
+// New-pair compaction in descending (a, b) order: lane a owns the bitmask of
+// partners b > a. Returns the total count; writes at most C entries.
+__device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newmask, uint32_t* ocab,
+                                               float2* ocimp, int C) {
+  const int cnt = __popcll(newmask);
+  int incl = cnt;  // sum over lanes >= lane
+  for (int d = 1; d < W; d <<= 1) {
+    const int o = __shfl_down(incl, d, W);
+    if (lane + d < W) incl += o;
+  }
+  const int total = __shfl(incl, 0, W);
+  int w = incl - cnt;
+  unsigned long long m = newmask;
+  while (m) {
+    const int j = 63 - __clzll(m);
+    m &= ~(1ull << j);
+    if (w < C) {
+      ocab[w] = (uint32_t)lane | ((uint32_t)j << 16);
+      ocimp[w] = make_float2(0.0f, 0.0f);
+    }
+    ++w;
+  }
+  return total;
+}
+
+template <typename OT>
+__global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B, int cur,
+                                                    const void* __restrict__ actions,
+                                                    OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
+                                                    float* __restrict__ rew_out,
+                                                    uint8_t* __restrict__ coll_out,
+                                                    uint8_t* __restrict__ done_out) {
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P.n_agents;
+  const int C = P.max_contacts;
+  const bool act = lane < N;
+  const size_t ag = (size_t)e * N + lane;
+  const int nxt = cur ^ 1;
+  const unsigned long long lt = lanemask_lt(lane);
+
+  __shared__ float s_cx[W], s_cy[W], s_vx[W], s_vy[W], s_c0x[W], s_c0y[W];
+  __shared__ float4 s_fo[W], s_fn[W];
+  __shared__ uint32_t s_tab[TCAP];
+  __shared__ float s_tln[TCAP], s_tlt[TCAP], s_tnx[TCAP], s_tny[TCAP];
+  __shared__ uint16_t s_adj[W * DEG];
+  __shared__ uint16_t s_ord[TCAP];
+  __shared__ uint32_t s_cvis[TCAP / 32];
+  __shared__ uint8_t s_deg[W], s_stack[W], s_ibodies[W], s_sleepnow[W];
+  __shared__ int8_t s_bisl[W];
+  __shared__ int16_t s_ic[ICAP + 1], s_ib[ICAP + 1];
+  __shared__ uint8_t s_isolved[ICAP];
+  __shared__ float s_slp[W];
+  __shared__ int s_nisl;
+
+  // ---- load ---------------------------------------------------------------
+  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f);
+  float ang = 0.0f, slp = 0.0f;
+  float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (act) {
+    p = B.pos[ag];
+    v = B.vel[ag];
+    ang = B.angle[ag];
+    fo = B.fat[ag];
+    slp = B.sleep[ag];
+  }
+  s_cx[lane] = p.x;
+  s_cy[lane] = p.y;
+  s_c0x[lane] = p.x;
+  s_c0y[lane] = p.y;
+  s_fo[lane] = fo;
+  if (lane < TCAP / 32) s_cvis[lane] = 0u;
+  const int step_count = B.step_count[e];
+  const int M = B.ccount[cur][e];
+  int status = 0;
+
+  // ---- actions -> angle, force (mvmnt.py:97-129) --------------------------
+  float Fx = 0.0f, Fy = 0.0f;
+  if (act) {
+    if (P.action_mode == MACM_ACTION_DISCRETE) {
+      const uint8_t* a = (const uint8_t*)actions + ag * 3;
+      const int a0 = a[0], a1 = a[1], a2 = a[2];
+      // agent.body.angle = angle + (a2-1) * rotation_speed * (1/hz) -> SetTransform(float32)
+      float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
+      double ad = (double)af;
+      if (fabs(ad) > M_PI) {
+        af = (float)(ad - sgn(ad) * (2.0 * M_PI));
+        ad = (double)af;
+      }
+      ang = af;
+      const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
+      const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
+      const double fx = (cos(ad) * k0 + cos(ad + M_PI / 2) * k1) * cc * P.force;
+      const double fy = (sin(ad) * k0 + sin(ad + M_PI / 2) * k1) * cc * P.force;
+      Fx = (float)fx;  // ApplyForce: b2Vec2(float32) accumulated onto m_force = 0
+      Fy = (float)fy;
+    } else {
+      const float* a = (const float*)actions + ag * 2;
+      float x = a[0], y = a[1];
+      if ((x * x + y * y) > 1.0f) {
+        x = sqrtf(x * x / (x * x + y * y));
+        y = sqrtf(y * y / (x * x + y * y));
+      }
+      Fx = x * P.force_f32;
+      Fy = y * P.force_f32;
+    }
+    Fx = 0.0f + Fx;  // m_force += force, from ClearForces' zero
+    Fy = 0.0f + Fy;
+  }
+  __syncthreads();
+
+  // ---- Collide: touching contacts of the ordered list ---------------------
+  const float rr = (P.radius + P.radius) * (P.radius + P.radius);
+  const float dt_ratio = step_count > 0 ? P.inv_dt * P.dt : 0.0f;  // m_inv_dt0 * dt
+  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
+  const float2* cimp = B.cimp[cur] + (size_t)e * C;
+  int T = 0;
+  for (int k0 = 0; k0 < M; k0 += W) {
+    const int k = k0 + lane;
+    bool touch = false;
+    uint32_t ab = 0;
+    if (k < M) {
+      ab = cab[k];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      const float dx = s_cx[b] - s_cx[a], dy = s_cy[b] - s_cy[a];
+      touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+    }
+    const unsigned long long m = __ballot(touch);
+    if (touch) {
+      const int slot = T + __popcll(m & lt);
+      if (slot < TCAP) {
+        const float2 lam = cimp[k];
+        s_tab[slot] = ab;
+        s_tln[slot] = P.warm_starting ? dt_ratio * lam.x : 0.0f;
+        s_tlt[slot] = P.warm_starting ? dt_ratio * lam.y : 0.0f;
+      }
+    }
+    T += __popcll(m);
+  }
+  if (T > TCAP) {
+    status |= MACM_ST_TOUCH_OVERFLOW;
+    T = TCAP;
+  }
+  __syncthreads();
+
+  // ---- per-body touching edges in list (= Box2D edge) order ----------------
+  {
+    int deg = 0;
+    if (act) {
+      for (int t = 0; t < T; ++t) {
+        const uint32_t ab = s_tab[t];
+        if ((int)(ab & 0xffffu) == lane || (int)(ab >> 16) == lane) {
+          if (deg < DEG) s_adj[lane * DEG + deg] = (uint16_t)t;
+          ++deg;
+        }
+      }
+    }
+    if (deg > DEG) {
+      status |= MACM_ST_DEGREE_OVERFLOW;
+      deg = DEG;
+    }
+    s_deg[lane] = (uint8_t)deg;
+  }
+  __syncthreads();
+
+  // ---- island DFS in Box2D order (b2World::Solve), serial on lane 0 --------
+  if (lane == 0) {
+    unsigned long long vis = 0ull;
+    int nord = 0, nisl = 0, nb = 0;
+    for (int s = N - 1; s >= 0; --s) {  // body list = reverse creation order
+      if ((vis >> s) & 1ull) continue;
+      if (s_deg[s] == 0) {
+        vis |= 1ull << s;
+        s_bisl[s] = -1;
+        continue;
+      }
+      s_ic[nisl] = (int16_t)nord;
+      s_ib[nisl] = (int16_t)nb;
+      int sp = 0;
+      s_stack[sp++] = (uint8_t)s;
+      vis |= 1ull << s;
+      while (sp > 0) {
+        const int b = s_stack[--sp];
+        s_ibodies[nb++] = (uint8_t)b;
+        s_bisl[b] = (int8_t)nisl;
+        const int db = s_deg[b];
+        for (int q = 0; q < db; ++q) {
+          const int t = s_adj[b * DEG + q];
+          const uint32_t bit = 1u << (t & 31);
+          if (s_cvis[t >> 5] & bit) continue;
+          s_cvis[t >> 5] |= bit;
+          s_ord[nord++] = (uint16_t)t;
+          const uint32_t ab = s_tab[t];
+          const int a = ab & 0xffffu, bb = ab >> 16;
+          const int o = (a == b) ? bb : a;
+          if ((vis >> o) & 1ull) continue;
+          vis |= 1ull << o;
+          s_stack[sp++] = (uint8_t)o;
+        }
+      }
+      ++nisl;
+    }
+    s_ic[nisl] = (int16_t)nord;
+    s_ib[nisl] = (int16_t)nb;
+    s_nisl = nisl;
+  }
+
+  // ---- integrate velocities + damping (b2Island::Solve) --------------------
+  float vx = v.x, vy = v.y;
+  if (act) {
+    vx = vx + P.dt * (0.0f + P.inv_mass * Fx);  // gravityScale * gravity == 0
+    vy = vy + P.dt * (0.0f + P.inv_mass * Fy);
+    vx = vx * P.damp;
+    vy = vy * P.damp;
+  }
+  s_vx[lane] = vx;
+  s_vy[lane] = vy;
+
+  // ---- contact normals from start-of-step positions (InitializeVelocityConstraints)
+  for (int t = lane; t < T; t += W) {
+    const uint32_t ab = s_tab[t];
+    const int a = ab & 0xffffu, b = ab >> 16;
+    const float pax = s_cx[a], pay = s_cy[a], pbx = s_cx[b], pby = s_cy[b];
+    float nx = 1.0f, ny = 0.0f;
+    const float ddx = pax - pbx, ddy = pay - pby;
+    if (ddx * ddx + ddy * ddy > kEps * kEps) {
+      nx = pbx - pax;
+      ny = pby - pay;
+      normalize(nx, ny);
+    }
+    s_tnx[t] = nx;
+    s_tny[t] = ny;
+  }
+  __syncthreads();
+
+  const int nisl = s_nisl;
+  const float mA = P.inv_mass, mB = P.inv_mass;
+  const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;  // normalMass == tangentMass
+  const float friction = P.friction;
+
+  // ---- warm start + velocity iterations, one lane per island ---------------
+  for (int I = lane; I < nisl; I += W) {
+    const int c0 = s_ic[I], c1 = s_ic[I + 1];
+    if (P.warm_starting) {
+      for (int k = c0; k < c1; ++k) {
+        const int t = s_ord[k];
+        const uint32_t ab = s_tab[t];
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const float nx = s_tnx[t], ny = s_tny[t];
+        const float tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
+        const float ln = s_tln[t], ltg = s_tlt[t];
+        const float Px = ln * nx + ltg * tx, Py = ln * ny + ltg * ty;
+        s_vx[a] = s_vx[a] - mA * Px;
+        s_vy[a] = s_vy[a] - mA * Py;
+        s_vx[b] = s_vx[b] + mB * Px;
+        s_vy[b] = s_vy[b] + mB * Py;
+      }
+    }
+    for (int it = 0; it < P.vel_iters; ++it) {
+      for (int k = c0; k < c1; ++k) {
+        const int t = s_ord[k];
+        const uint32_t ab = s_tab[t];
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const float nx = s_tnx[t], ny = s_tny[t];
+        const float tx = ny, ty = -nx;
+        float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+        float ln = s_tln[t], ltg = s_tlt[t];
+        {  // tangent first
+          const float dvx = vBx - vAx, dvy = vBy - vAy;
+          const float vt = dvx * tx + dvy * ty;
+          float lambda = kmass * (-vt);
+          const float maxf = friction * ln;
+          const float ni = bclamp(ltg + lambda, -maxf, maxf);
+          lambda = ni - ltg;
+          ltg = ni;
+          const float Px = lambda * tx, Py = lambda * ty;
+          vAx = vAx - mA * Px;
+          vAy = vAy - mA * Py;
+          vBx = vBx + mB * Px;
+          vBy = vBy + mB * Py;
+        }
+        {  // normal
+          const float dvx = vBx - vAx, dvy = vBy - vAy;
+          const float vn = dvx * nx + dvy * ny;
+          float lambda = -kmass * (vn - 0.0f);  // velocityBias == 0 (restitution 0)
+          const float ni = bmax(ln + lambda, 0.0f);
+          lambda = ni - ln;
+          ln = ni;
+          const float Px = lambda * nx, Py = lambda * ny;
+          vAx = vAx - mA * Px;
+          vAy = vAy - mA * Py;
+          vBx = vBx + mB * Px;
+          vBy = vBy + mB * Py;
+        }
+        s_vx[a] = vAx;
+        s_vy[a] = vAy;
+        s_vx[b] = vBx;
+        s_vy[b] = vBy;
+        s_tln[t] = ln;
+        s_tlt[t] = ltg;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- integrate positions --------------------------------------------------
+  float cx = p.x, cy = p.y;
+  if (act) {
+    vx = s_vx[lane];
+    vy = s_vy[lane];
+    const float tx = P.dt * vx, ty = P.dt * vy;
+    if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
+      const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
+      vx = vx * ratio;
+      vy = vy * ratio;
+    }
+    cx = cx + P.dt * vx;
+    cy = cy + P.dt * vy;
+    s_cx[lane] = cx;
+    s_cy[lane] = cy;
+  }
+  __syncthreads();
+
+  // ---- position iterations, one lane per island ------------------------------
+  for (int I = lane; I < nisl; I += W) {
+    const int c0 = s_ic[I], c1 = s_ic[I + 1];
+    int solved = 0;
+    for (int it = 0; it < P.pos_iters; ++it) {
+      float min_sep = 0.0f;
+      for (int k = c0; k < c1; ++k) {
+        const int t = s_ord[k];
+        const uint32_t ab = s_tab[t];
+        const int a = ab & 0xffffu, b = ab >> 16;
+        float cAx = s_cx[a], cAy = s_cy[a], cBx = s_cx[b], cBy = s_cy[b];
+        float nx = cBx - cAx, ny = cBy - cAy;
+        normalize(nx, ny);
+        const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - P.radius - P.radius;
+        min_sep = bmin(min_sep, sep);
+        const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+        const float K = mA + mB;
+        const float imp = K > 0.0f ? -Cc / K : 0.0f;
+        const float Px = imp * nx, Py = imp * ny;
+        cAx = cAx - mA * Px;
+        cAy = cAy - mA * Py;
+        cBx = cBx + mB * Px;
+        cBy = cBy + mB * Py;
+        s_cx[a] = cAx;
+        s_cy[a] = cAy;
+        s_cx[b] = cBx;
+        s_cy[b] = cBy;
+      }
+      if (min_sep >= -3.0f * kLinearSlop) {
+        solved = 1;
+        break;
+      }
+    }
+    s_isolved[I] = (uint8_t)solved;
+  }
+
+  // ---- per-body sleep clock ---------------------------------------------------
+  float ns = 0.0f;
+  if (act) {
+    const bool moving = vx * vx + vy * vy > kLinearSleepTol * kLinearSleepTol;
+    ns = moving ? 0.0f : slp + P.dt;
+    s_slp[lane] = ns;
+  }
+  __syncthreads();
+
+  // ---- island sleep decision ---------------------------------------------------
+  if (act && s_bisl[lane] < 0) s_sleepnow[lane] = (ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
+  for (int I = lane; I < nisl; I += W) {
+    const int b0 = s_ib[I], b1 = s_ib[I + 1];
+    float mn = 3.402823466e+38f;
+    for (int k = b0; k < b1; ++k) mn = bmin(mn, s_slp[s_ibodies[k]]);
+    const uint8_t sl = (mn >= kTimeToSleep && s_isolved[I]) ? 1 : 0;
+    for (int k = b0; k < b1; ++k) s_sleepnow[s_ibodies[k]] = sl;
+  }
+  __syncthreads();
+
+  // ---- SynchronizeFixtures: fat-AABB update ------------------------------------
+  float4 fn = fo;
+  if (act) {
+    cx = s_cx[lane];
+    cy = s_cy[lane];
+    const float r = P.radius;
+    const float c0x = p.x, c0y = p.y;
+    const float lox = bmin(c0x - r, cx - r), loy = bmin(c0y - r, cy - r);
+    const float hix = bmax(c0x + r, cx + r), hiy = bmax(c0y + r, cy + r);
+    const bool contains = fo.x <= lox && fo.y <= loy && hix <= fo.z && hiy <= fo.w;
+    if (!contains) {
+      fn = make_float4(lox - kAabbExtension, loy - kAabbExtension, hix + kAabbExtension, hiy + kAabbExtension);
+      const float dx = kAabbMultiplier * (cx - c0x), dy = kAabbMultiplier * (cy - c0y);
+      if (dx < 0.0f) fn.x += dx; else fn.z += dx;
+      if (dy < 0.0f) fn.y += dy; else fn.w += dy;
+    }
+    if (s_sleepnow[lane]) {
+      vx = 0.0f;
+      vy = 0.0f;
+      ns = 0.0f;
+    }
+  }
+  s_fn[lane] = fn;
+  __syncthreads();
+
+  // ---- contact set, new pairs, nearest neighbour -------------------------------
+  bool coll = false;
+  unsigned long long newmask = 0ull;
+  float best;
+  int bj;
+  if (act) {
+    for (int j = 0; j < N; ++j) {
+      const float4 foj = s_fo[j], fnj = s_fn[j];
+      const bool ovo = overlap(fo, foj), ovn = overlap(fn, fnj);
+      if (j != lane) coll |= ovo | ovn;
+      if (j > lane && ovn && !ovo) newmask |= 1ull << j;
+    }
+    nearest(N, lane, cx, cy, s_cx, s_cy, best, bj);
+  }
+
+  // ---- next ordered list: new pairs (desc) ++ surviving old pairs --------------
+  uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
+  float2* ocimp = B.cimp[nxt] + (size_t)e * C;
+  const int nnew = write_new_pairs(lane, newmask, ocab, ocimp, C);
+  int kept = 0, Tr = 0;
+  for (int k0 = 0; k0 < M; k0 += W) {
+    const int k = k0 + lane;
+    bool keep = false, touch = false;
+    uint32_t ab = 0;
+    if (k < M) {
+      ab = cab[k];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      const float dx = s_c0x[b] - s_c0x[a], dy = s_c0y[b] - s_c0y[a];
+      touch = !(dx * dx + dy * dy > rr);
+      keep = overlap(s_fn[a], s_fn[b]);
+    }
+    const unsigned long long mt = __ballot(touch), mk = __ballot(keep);
+    const int trank = Tr + __popcll(mt & lt);
+    const int krank = kept + __popcll(mk & lt);
+    Tr += __popcll(mt);
+    kept += __popcll(mk);
+    if (keep) {
+      const int w = nnew + krank;
+      if (w < C) {
+        float2 l = make_float2(0.0f, 0.0f);
+        if (touch && trank < TCAP) l = make_float2(s_tln[trank], s_tlt[trank]);
+        ocab[w] = ab;
+        ocimp[w] = l;
+      }
+    }
+  }
+  int total = nnew + kept;
+  if (total > C) {
+    status |= MACM_ST_CONTACT_OVERFLOW;
+    total = C;
+  }
+
+  // ---- rewards (mvmnt.py:160-179) and obs (mvmnt.py:181-222) -------------------
+  float rew = 0.0f;
+  if (act) {
+    const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+    const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
+    const float td2 = tdx * tdx + tdy * tdy;       // b2DistanceSquared(target, position)
+    const double d = sqrt((double)td2);
+    if (coll) rew = -1.0f;
+    else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
+    else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
+    rew_out[ag] = rew;
+    if (coll_out) coll_out[ag] = coll ? 1 : 0;
+    if (nbr_out) nbr_out[ag] = bj;
+    if (obs) write_obs<OT>(P, obs + (size_t)e * N * (P.coord == MACM_COORD_CARTESIAN ? 6 : 4), lane, cx, cy, ang,
+                           best, bj, s_cx, s_cy, tdx, tdy, td2);
+    // ---- state write-back ----
+    B.pos[ag] = make_float2(cx, cy);
+    B.vel[ag] = make_float2(vx, vy);
+    B.angle[ag] = ang;
+    B.fat[ag] = fn;
+    B.sleep[ag] = ns;
+  }
+
+  // ---- per-env bookkeeping + counters -------------------------------------------
+  const unsigned long long mcoll = __ballot(act && coll);
+  const unsigned long long mpos = __ballot(act && rew > 0.0f);
+  const unsigned long long mst1 = __ballot(status & 1), mst2 = __ballot(status & 2), mst4 = __ballot(status & 4);
+  if (lane == 0) {
+    const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz
+    const uint8_t dn = tp > P.time_limit ? 1 : 0;
+    B.time_passed[e] = tp;
+    B.done[e] = dn;
+    if (done_out) done_out[e] = dn;
+    B.step_count[e] = step_count + 1;
+    B.ccount[nxt][e] = total;
+    const int st = (mst1 ? 1 : 0) | (mst2 ? 2 : 0) | (mst4 ? 4 : 0);
+    if (st) atomicOr(&B.status[e], st);
+    atomicAdd(&B.counters[0], (unsigned long long)N);
+    atomicAdd(&B.counters[1], (unsigned long long)__popcll(mcoll));
+    atomicAdd(&B.counters[2], (unsigned long long)__popcll(mpos));
+    atomicAdd(&B.counters[3], (unsigned long long)dn);
+  }
+}
+
+// Initial proxies (b2DynamicTree::CreateProxy: fat = tight +- 0.1), the first
+// FindNewContacts' list (all overlapping pairs, descending), zeroed dynamics,
+// and the initial observation (Flock.obs, mvmnt.py:79).
+template <typename OT>
+__global__ __launch_bounds__(W) void flock_init_w64(StepParams P, WorldBuffers B, int cur,
+                                                    OT* __restrict__ obs, int32_t* __restrict__ nbr_out) {
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P.n_agents;
+  const int C = P.max_contacts;
+  const bool act = lane < N;
+  const size_t ag = (size_t)e * N + lane;
+  __shared__ float s_cx[W], s_cy[W];
+  __shared__ float4 s_f[W];
+  float2 p = make_float2(0.0f, 0.0f);
+  float4 f = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float ang = 0.0f;
+  if (act) {
+    p = B.pos[ag];
+    ang = B.angle[ag];
+    const float r = P.radius;
+    f = make_float4((p.x - r) - kAabbExtension, (p.y - r) - kAabbExtension, (p.x + r) + kAabbExtension,
+                    (p.y + r) + kAabbExtension);
+    B.fat[ag] = f;
+    B.vel[ag] = make_float2(0.0f, 0.0f);
+    B.sleep[ag] = 0.0f;
+  }
+  s_cx[lane] = p.x;
+  s_cy[lane] = p.y;
+  s_f[lane] = f;
+  __syncthreads();
+  unsigned long long m = 0ull;
+  if (act)
+    for (int j = lane + 1; j < N; ++j)
+      if (overlap(f, s_f[j])) m |= 1ull << j;
+  int total = write_new_pairs(lane, m, B.cab[cur] + (size_t)e * C, B.cimp[cur] + (size_t)e * C, C);
+  int st = 0;
+  if (total > C) {
+    st = MACM_ST_CONTACT_OVERFLOW;
+    total = C;
+  }
+  if (act && (obs || nbr_out)) {
+    float best;
+    int bj;
+    nearest(N, lane, p.x, p.y, s_cx, s_cy, best, bj);
+    if (nbr_out) nbr_out[ag] = bj;
+    if (obs) {
+      const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+      const float tdx = tg.x - p.x, tdy = tg.y - p.y;
+      write_obs<OT>(P, obs + (size_t)e * N * (P.coord == MACM_COORD_CARTESIAN ? 6 : 4), lane, p.x, p.y, ang, best,
+                    bj, s_cx, s_cy, tdx, tdy, tdx * tdx + tdy * tdy);
+    }
+  }
+  if (lane == 0) {
+    B.ccount[cur][e] = total;
+    B.step_count[e] = 0;
+    B.time_passed[e] = 0.0;
+    B.done[e] = 0;
+    B.status[e] = st;
+  }
+}
+
+// Observation of the current state (Flock.get_obs) without stepping.
+template <typename OT>
+__global__ __launch_bounds__(W) void flock_observe_w64(StepParams P, WorldBuffers B, OT* __restrict__ obs,
+                                                       int32_t* __restrict__ nbr_out) {
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P.n_agents;
+  const bool act = lane < N;
+  const size_t ag = (size_t)e * N + lane;
+  __shared__ float s_cx[W], s_cy[W];
+  float2 p = make_float2(0.0f, 0.0f);
+  if (act) p = B.pos[ag];
+  s_cx[lane] = p.x;
+  s_cy[lane] = p.y;
+  __syncthreads();
+  if (!act) return;
+  float best;
+  int bj;
+  nearest(N, lane, p.x, p.y, s_cx, s_cy, best, bj);
+  if (nbr_out) nbr_out[ag] = bj;
+  if (obs) {
+    const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+    const float tdx = tg.x - p.x, tdy = tg.y - p.y;
+    write_obs<OT>(P, obs + (size_t)e * N * (P.coord == MACM_COORD_CARTESIAN ? 6 : 4), lane, p.x, p.y,
+                  B.angle[ag], best, bj, s_cx, s_cy, tdx, tdy, tdx * tdx + tdy * tdy);
+  }
+}
+
+// ---- host-side launchers (C++ linkage, used by macm_capi.hip) -----------------
+hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions,
+                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
+                           hipStream_t s) {
+  dim3 grid(P.n_envs), block(W);
+  if (obs_f64)
+    hipLaunchKernelGGL(flock_step_w64<double>, grid, block, 0, s, P, B, cur, actions, (double*)obs, nbr, rew,
+                       coll, done);
+  else
+    hipLaunchKernelGGL(flock_step_w64<float>, grid, block, 0, s, P, B, cur, actions, (float*)obs, nbr, rew, coll,
+                       done);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
+                           int32_t* nbr, hipStream_t s) {
+  dim3 grid(P.n_envs), block(W);
+  if (obs_f64)
+    hipLaunchKernelGGL(flock_init_w64<double>, grid, block, 0, s, P, B, cur, (double*)obs, nbr);
+  else
+    hipLaunchKernelGGL(flock_init_w64<float>, grid, block, 0, s, P, B, cur, (float*)obs, nbr);
+  return hipGetLastError();
+}
+
+hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
+                              hipStream_t s) {
+  dim3 grid(P.n_envs), block(W);
+  if (obs_f64)
+    hipLaunchKernelGGL(flock_observe_w64<double>, grid, block, 0, s, P, B, (double*)obs, nbr);
+  else
+    hipLaunchKernelGGL(flock_observe_w64<float>, grid, block, 0, s, P, B, (float*)obs, nbr);
+  return hipGetLastError();
+}
+
+}  // namespace macm

@@ -1,0 +1,389 @@
+// macm_capi.hip — the C-ABI of libmacm_hip.so (declared in include/macm.h).
+//
+// Owns the per-world device state (SoA, sized for E envs x N agents), derives the
+// step constants from macm_config the way the reference derives them, seeds
+// envs with the reference's RNG order, and launches the HIP kernels on the
+// caller's stream. No torch types, no exceptions across the ABI.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "flock_common.hpp"
+#include "py_mt19937.hpp"
+
+namespace macm {
+hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
+                           bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
+hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
+                           int32_t* nbr, hipStream_t s);
+hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
+                              hipStream_t s);
+}  // namespace macm
+
+using namespace macm;
+
+struct macm_world {
+  macm_config cfg;
+  StepParams P;
+  WorldBuffers B;
+  int cur;  // which contact-list buffer holds the current ordered list
+  int device;
+  std::vector<int32_t> tidx;
+  std::vector<void*> allocs;
+};
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail(MACM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));             \
+  } while (0)
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <typename T>
+int dalloc(macm_world* w, T** p, size_t count) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, count * sizeof(T) > 0 ? count * sizeof(T) : 16);
+  if (e != hipSuccess) return fail(MACM_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  w->allocs.push_back(q);
+  *p = (T*)q;
+  return MACM_OK;
+}
+
+int obs_dim(const macm_config& c) { return c.coord == MACM_COORD_CARTESIAN ? 6 : 4; }
+
+void free_world(macm_world* w) {
+  for (void* p : w->allocs) (void)hipFree(p);
+  w->allocs.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* macm_version(void) { return "macm-hip 0.1.0 (gfx950; Flock N<=64 wave-per-env kernel)"; }
+int macm_abi_version(void) { return MACM_ABI_VERSION; }
+const char* macm_last_error(void) { return g_last_error.c_str(); }
+
+int macm_config_default(macm_config* c) {
+  if (!c) return fail(MACM_E_INVALID, "cfg is NULL");
+  memset(c, 0, sizeof(*c));
+  c->n_agents = 10;  // Flock(n_agents=[10]) default, mvmnt.py:35
+  c->n_targets = 1;
+  c->action_mode = MACM_ACTION_DISCRETE;
+  c->reward_mode = MACM_REWARD_BINARY;
+  c->coord = MACM_COORD_POLAR;
+  c->velocity_iterations = 8;
+  c->position_iterations = 3;
+  c->warm_starting = 1;
+  c->obs_f64 = 0;
+  c->hz = 60.0;
+  c->start_spread = 20.0;
+  c->start_point[0] = 0.0;
+  c->start_point[1] = 0.0;
+  c->agent_rotation_speed = 0.8 * (2 * M_PI);
+  c->agent_force = 20.0;
+  c->time_limit = 60.0;
+  c->reward_radius = 7.0;
+  c->target_mindist = 25.0;
+  c->target_maxdist = 60.0;
+  c->radius = 0.5f;
+  c->density = 1.0f;
+  c->friction = 0.3f;
+  c->linear_damping = 5.0f;
+  return MACM_OK;
+}
+
+int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_t n_envs, int32_t device,
+                      int32_t max_contacts, macm_world** out) {
+  if (!cfg || !out) return fail(MACM_E_INVALID, "cfg/out is NULL");
+  *out = nullptr;
+  const macm_config& c = *cfg;
+  if (n_envs <= 0) return fail(MACM_E_INVALID, "n_envs must be > 0");
+  if (c.n_agents < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2 (get_obs needs another agent)");
+  if (c.n_agents > 64)
+    return fail(MACM_E_UNSUPPORTED, "n_agents > 64 needs the multi-wave kernel (not built in this version)");
+  if (c.n_targets < 1) return fail(MACM_E_INVALID, "n_targets must be >= 1");
+  if (!(c.hz > 0.0)) return fail(MACM_E_INVALID, "hz must be > 0");
+  if (c.velocity_iterations < 0 || c.position_iterations < 0) return fail(MACM_E_INVALID, "iterations < 0");
+  if (c.action_mode != MACM_ACTION_DISCRETE && c.action_mode != MACM_ACTION_CONTINUOUS)
+    return fail(MACM_E_INVALID, "action_mode");
+  if (c.reward_mode != MACM_REWARD_BINARY && c.reward_mode != MACM_REWARD_LINEAR)
+    return fail(MACM_E_INVALID, "reward_mode");
+  if (c.coord != MACM_COORD_POLAR && c.coord != MACM_COORD_CARTESIAN) return fail(MACM_E_INVALID, "coord");
+  if (!(c.radius > 0.0f)) return fail(MACM_E_INVALID, "radius must be > 0");
+  const int N = c.n_agents, T = c.n_targets;
+  std::vector<int32_t> tidx(N, 0);
+  if (targets_idx)
+    for (int i = 0; i < N; ++i) {
+      if (targets_idx[i] < 0 || targets_idx[i] >= T) return fail(MACM_E_INVALID, "targets_idx out of range");
+      tidx[i] = targets_idx[i];
+    }
+  const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
+  int C = max_contacts > 0 ? max_contacts : (int)all_pairs;
+  if (C > all_pairs) C = (int)all_pairs;
+
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MACM_E_INVALID, "device index out of range");
+  DeviceGuard g(device);
+
+  macm_world* w = new macm_world();
+  w->cfg = c;
+  w->device = device;
+  w->cur = 0;
+  w->tidx = tidx;
+  StepParams& P = w->P;
+  P.n_envs = n_envs;
+  P.n_agents = N;
+  P.n_targets = T;
+  P.max_contacts = C;
+  P.vel_iters = c.velocity_iterations;
+  P.pos_iters = c.position_iterations;
+  P.warm_starting = c.warm_starting ? 1 : 0;
+  P.action_mode = c.action_mode;
+  P.reward_mode = c.reward_mode;
+  P.coord = c.coord;
+  // cm_framework.py:182-185 (timeStep = 1.0 / hz, a Python float) -> b2World::Step(float32 dt)
+  volatile double dt64 = 1.0 / c.hz;
+  P.dt = (float)dt64;
+  P.inv_dt = 1.0f / P.dt;
+  {
+    // b2CircleShape::ComputeMass + b2Body::ResetMassData (settings.py:127-133)
+    volatile float mass = c.density * kPi32 * c.radius * c.radius;
+    P.inv_mass = mass > 0.0f ? 1.0f / mass : 1.0f;
+    volatile float den = 1.0f + P.dt * c.linear_damping;
+    P.damp = 1.0f / den;
+    volatile float ff = c.friction * c.friction;
+    P.friction = sqrtf(ff);  // b2MixFriction
+  }
+  P.radius = c.radius;
+  P.force_f32 = (float)c.agent_force;
+  P.rot_step = c.agent_rotation_speed;
+  P.inv_hz = 1.0 / c.hz;
+  P.force = c.agent_force;
+  volatile double two = 2.0;
+  P.diag_c = 1.0 / sqrt(two);  // 1 / np.sqrt(2)
+  P.reward_radius = c.reward_radius;
+  P.time_limit = c.time_limit;
+
+  WorldBuffers& B = w->B;
+  memset(&B, 0, sizeof(B));
+  const size_t EN = (size_t)n_envs * N;
+  int rc = MACM_OK;
+  if ((rc = dalloc(w, &B.pos, EN)) || (rc = dalloc(w, &B.vel, EN)) || (rc = dalloc(w, &B.angle, EN)) ||
+      (rc = dalloc(w, &B.fat, EN)) || (rc = dalloc(w, &B.sleep, EN)) ||
+      (rc = dalloc(w, &B.targets, (size_t)n_envs * T)) || (rc = dalloc(w, &B.tidx, (size_t)N)) ||
+      (rc = dalloc(w, &B.ccount[0], (size_t)n_envs)) || (rc = dalloc(w, &B.ccount[1], (size_t)n_envs)) ||
+      (rc = dalloc(w, &B.cab[0], (size_t)n_envs * C)) || (rc = dalloc(w, &B.cab[1], (size_t)n_envs * C)) ||
+      (rc = dalloc(w, &B.cimp[0], (size_t)n_envs * C)) || (rc = dalloc(w, &B.cimp[1], (size_t)n_envs * C)) ||
+      (rc = dalloc(w, &B.step_count, (size_t)n_envs)) || (rc = dalloc(w, &B.time_passed, (size_t)n_envs)) ||
+      (rc = dalloc(w, &B.done, (size_t)n_envs)) || (rc = dalloc(w, &B.status, (size_t)n_envs)) ||
+      (rc = dalloc(w, &B.counters, 4))) {
+    free_world(w);
+    delete w;
+    return rc;
+  }
+  hipError_t e = hipMemcpy(B.tidx, tidx.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(B.counters, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * n_envs);
+  if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
+  if (e != hipSuccess) {
+    free_world(w);
+    delete w;
+    return fail(MACM_E_HIP, std::string("world init copy: ") + hipGetErrorString(e));
+  }
+  *out = w;
+  return MACM_OK;
+}
+
+int macm_world_destroy(macm_world* w) {
+  if (!w) return MACM_OK;
+  DeviceGuard g(w->device);
+  (void)hipDeviceSynchronize();
+  free_world(w);
+  delete w;
+  return MACM_OK;
+}
+
+int macm_world_info_get(const macm_world* w, macm_world_info* info) {
+  if (!w || !info) return fail(MACM_E_INVALID, "NULL argument");
+  info->n_envs = w->P.n_envs;
+  info->n_agents = w->P.n_agents;
+  info->n_targets = w->P.n_targets;
+  info->obs_dim = obs_dim(w->cfg);
+  info->max_contacts = w->P.max_contacts;
+  info->max_touching = 256;
+  info->device = w->device;
+  info->_pad = 0;
+  return MACM_OK;
+}
+
+int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const macm_outputs* out, void* stream) {
+  if (!w) return fail(MACM_E_INVALID, "world is NULL");
+  DeviceGuard g(w->device);
+  const macm_config& c = w->cfg;
+  const int E = w->P.n_envs, N = w->P.n_agents, T = w->P.n_targets;
+  std::vector<float2> pos((size_t)E * N), tg((size_t)E * T);
+  std::vector<float> ang((size_t)E * N);
+  for (int e = 0; e < E; ++e) {
+    PyMT19937 r(seed + (uint64_t)(env_offset + e));
+    for (int t = 0; t < T; ++t) {  // mvmnt.py:46-52
+      const double rand_angle = 2 * M_PI * r.random();
+      const double rand_dist = c.target_mindist + r.random() * (c.target_maxdist - c.target_mindist);
+      tg[(size_t)e * T + t] = make_float2((float)(rand_dist * cos(rand_angle)), (float)(rand_dist * sin(rand_angle)));
+    }
+    for (int i = 0; i < N; ++i) {  // mvmnt.py:61-64, CreateDynamicBody(position=(x, y), angle=angle)
+      const double x = c.start_spread * (r.random() - 0.5) + c.start_point[0];
+      const double y = c.start_spread * (r.random() - 0.5) + c.start_point[1];
+      const double a = r.uniform(-1, 1) * M_PI;
+      pos[(size_t)e * N + i] = make_float2((float)x, (float)y);
+      ang[(size_t)e * N + i] = (float)a;
+    }
+  }
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(w->B.pos, pos.data(), pos.size() * sizeof(float2), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(w->B.angle, ang.data(), ang.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(w->B.targets, tg.data(), tg.size() * sizeof(float2), hipMemcpyHostToDevice, s));
+  w->cur = 0;
+  HIP_TRY(launch_init_w64(w->P, w->B, w->cur, out ? out->obs : nullptr, c.obs_f64 != 0,
+                          out ? out->nbr_id : nullptr, s));
+  // host vectors are read by the async copies: wait before they go out of scope
+  HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+int macm_world_place(macm_world* w, const void* pos, const void* angle, const void* targets,
+                     const macm_outputs* out, void* stream) {
+  if (!w || !pos || !angle || !targets) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  const size_t EN = (size_t)w->P.n_envs * w->P.n_agents, ET = (size_t)w->P.n_envs * w->P.n_targets;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(w->B.pos, pos, EN * sizeof(float2), hipMemcpyDefault, s));
+  HIP_TRY(hipMemcpyAsync(w->B.angle, angle, EN * sizeof(float), hipMemcpyDefault, s));
+  HIP_TRY(hipMemcpyAsync(w->B.targets, targets, ET * sizeof(float2), hipMemcpyDefault, s));
+  w->cur = 0;
+  HIP_TRY(launch_init_w64(w->P, w->B, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
+                          out ? out->nbr_id : nullptr, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream) {
+  if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
+  DeviceGuard g(w->device);
+  HIP_TRY(launch_step_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
+                          out->collided, out->done, (hipStream_t)stream));
+  w->cur ^= 1;
+  return MACM_OK;
+}
+
+int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
+  if (!w || !out) return fail(MACM_E_INVALID, "world/out is NULL");
+  DeviceGuard g(w->device);
+  HIP_TRY(launch_observe_w64(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
+  return MACM_OK;
+}
+
+static int copy_state(macm_world* w, const macm_state* st, void* stream, bool to_device) {
+  if (!w || !st) return fail(MACM_E_INVALID, "world/state is NULL");
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t E = w->P.n_envs, N = w->P.n_agents, T = w->P.n_targets, C = w->P.max_contacts;
+  struct Item {
+    void* user;
+    void* dev;
+    size_t bytes;
+  } items[] = {
+      {st->pos, w->B.pos, E * N * sizeof(float2)},
+      {st->vel, w->B.vel, E * N * sizeof(float2)},
+      {st->angle, w->B.angle, E * N * sizeof(float)},
+      {st->fat, w->B.fat, E * N * sizeof(float4)},
+      {st->sleep, w->B.sleep, E * N * sizeof(float)},
+      {st->targets, w->B.targets, E * T * sizeof(float2)},
+      {st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t)},
+      {st->contact_ab, w->B.cab[w->cur], E * C * sizeof(uint32_t)},
+      {st->contact_imp, w->B.cimp[w->cur], E * C * sizeof(float2)},
+      {st->step_count, w->B.step_count, E * sizeof(int32_t)},
+      {st->time_passed, w->B.time_passed, E * sizeof(double)},
+  };
+  for (const Item& it : items) {
+    if (!it.user) continue;
+    if (to_device) HIP_TRY(hipMemcpyAsync(it.dev, it.user, it.bytes, hipMemcpyDefault, s));
+    else HIP_TRY(hipMemcpyAsync(it.user, it.dev, it.bytes, hipMemcpyDefault, s));
+  }
+  if (to_device && st->time_passed) {
+    // done flag follows time_passed (mvmnt.py:135-136)
+    std::vector<double> tp(E);
+    std::vector<uint8_t> dn(E);
+    HIP_TRY(hipMemcpyAsync(tp.data(), w->B.time_passed, E * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (size_t e = 0; e < E; ++e) dn[e] = tp[e] > w->P.time_limit ? 1 : 0;
+    HIP_TRY(hipMemcpyAsync(w->B.done, dn.data(), E, hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+int macm_world_get_state(macm_world* w, const macm_state* dst, void* stream) {
+  return copy_state(w, dst, stream, false);
+}
+
+int macm_world_set_state(macm_world* w, const macm_state* src, void* stream) {
+  return copy_state(w, src, stream, true);
+}
+
+int macm_world_status(macm_world* w, int32_t* status_or, void* stream) {
+  if (!w || !status_or) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  std::vector<int32_t> st(w->P.n_envs);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(st.data(), w->B.status, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  int32_t acc = 0;
+  for (int32_t v : st) acc |= v;
+  *status_or = acc;
+  return MACM_OK;
+}
+
+int macm_world_counters(macm_world* w, int64_t out[4], void* stream) {
+  if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  unsigned long long h[4];
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(h, w->B.counters, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+  return MACM_OK;
+}
+
+int macm_world_reset_counters(macm_world* w, void* stream) {
+  if (!w) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  HIP_TRY(hipMemsetAsync(w->B.counters, 0, 4 * sizeof(unsigned long long), (hipStream_t)stream));
+  return MACM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+"""FlockVec — the batched throughput API for cm-flock-v0.
+
+E independent Flock envs (reference gym_macm/envs/mvmnt.py) stepped by one HIP
+launch per step, with actions and outputs as device tensors:
+
+    env = FlockVec(num_envs=4096, n_agents=[64], seed=0)
+    obs, nbr_id = env.obs, env.nbr_id            # initial observation
+    obs, nbr_id, reward, done = env.step(actions)  # actions uint8 [E, N, 3] on the GPU
+
+Env e is the reference env constructed after ``random.seed(seed + env_offset + e)``;
+shard a job over GPUs by giving each rank its contiguous ``env_offset``.
+Settings keyword arguments are the reference's (flockSettings, settings.py:110-146).
+Returned tensors are views of buffers reused by the next call.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from gym_macm.settings import flockSettings, to_config
+from gym_macm.world import World
+
+
+class FlockVec(object):
+    def __init__(self, num_envs, n_agents=(10,), targets=None, seed=0, env_offset=0, device=None,
+                 obs_dtype=torch.float32, max_contacts=0, **kwargs):
+        self.settings = flockSettings(**kwargs)
+        self.num_envs = int(num_envs)
+        self.n_agents = list(n_agents) if not isinstance(n_agents, int) else [n_agents]
+        N = int(sum(self.n_agents))
+        self.n_targets = 1 if targets is None else len(np.unique(targets))
+        self.targets_idx = np.zeros(N, np.int32) if targets is None else np.asarray(targets, np.int32)
+        cfg = to_config(self.settings, N, self.n_targets, obs_f64=(obs_dtype == torch.float64))
+        self.world = World(cfg, self.targets_idx, self.num_envs, device=device, max_contacts=max_contacts)
+        self.device = self.world.device
+        self.N = N
+        self.seed = int(seed)
+        self.env_offset = int(env_offset)
+        self.obs, self.nbr_id = self.world.reset(self.seed, self.env_offset)
+
+    @property
+    def obs_dim(self):
+        return self.world.OD
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.seed = int(seed)
+        self.obs, self.nbr_id = self.world.reset(self.seed, self.env_offset)
+        return self.obs, self.nbr_id
+
+    def step(self, actions):
+        return self.world.step(actions)
+
+    def observe(self):
+        return self.world.observe()
+
+    def get_state(self):
+        return self.world.get_state()
+
+    def set_state(self, state):
+        self.world.set_state(state)
+
+    def status(self):
+        return self.world.status()
+
+    def counters(self):
+        return self.world.counters()

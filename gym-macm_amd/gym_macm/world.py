@@ -1,0 +1,172 @@
+"""Thin Python handle over the C-ABI world (include/macm.h), with torch tensors as
+device memory and torch's current stream as the launch stream.
+
+This replaces the reference's framework plugin point — ``NoRender(FrameworkBase)``
+owning one ``b2World`` per env (gym_macm/backends/no_render.py:4-19,
+gym_macm/cm_framework.py:155-167) — with one device-resident world of E envs.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _abi
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class World:
+    """E independent envs of one Flock configuration on one GPU.
+
+    Outputs are written into preallocated tensors owned by this object and
+    reused by every call (clone them to keep a step's values).
+    """
+
+    def __init__(self, cfg: _abi.MacmConfig, targets_idx=None, n_envs: int = 1, device=None,
+                 max_contacts: int = 0):
+        self.L = _abi.lib()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("the HIP world lives on a GPU device (no CPU fallback)")
+        self.device = device
+        self.cfg = cfg
+        self.E = int(n_envs)
+        self.N = int(cfg.n_agents)
+        self.T = int(cfg.n_targets)
+        ti = None
+        if targets_idx is not None:
+            self._tidx = np.ascontiguousarray(np.asarray(targets_idx, np.int32))
+            if self._tidx.shape != (self.N,):
+                raise ValueError(f"targets_idx must have length n_agents={self.N}")
+            ti = self._tidx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _abi.check(self.L.macm_world_create(ctypes.byref(cfg), ti, self.E, device.index or 0,
+                                                int(max_contacts), ctypes.byref(h)), "macm_world_create")
+        self.h = h
+        info = _abi.MacmWorldInfo()
+        _abi.check(self.L.macm_world_info_get(self.h, ctypes.byref(info)), "macm_world_info_get")
+        self.info = info
+        self.OD = info.obs_dim
+        self.C = info.max_contacts
+        odt = torch.float64 if cfg.obs_f64 else torch.float32
+        kw = dict(device=device)
+        self.obs = torch.empty((self.E, self.N, self.OD), dtype=odt, **kw)
+        self.nbr_id = torch.empty((self.E, self.N), dtype=torch.int32, **kw)
+        self.reward = torch.empty((self.E, self.N), dtype=torch.float32, **kw)
+        self.collided = torch.empty((self.E, self.N), dtype=torch.uint8, **kw)
+        self.done = torch.zeros((self.E,), dtype=torch.uint8, **kw)
+        self._out = _abi.MacmOutputs(_ptr(self.obs), _ptr(self.nbr_id), _ptr(self.reward), _ptr(self.collided),
+                                     _ptr(self.done))
+        self._out_obs = _abi.MacmOutputs(_ptr(self.obs), _ptr(self.nbr_id), None, None, None)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.L.macm_world_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -- lifecycle ---------------------------------------------------------
+    def reset(self, seed: int, env_offset: int = 0):
+        """Env e := Flock(...) after random.seed(seed + env_offset + e); writes the initial obs."""
+        _abi.check(self.L.macm_world_reset(self.h, int(seed), int(env_offset), ctypes.byref(self._out_obs),
+                                           self._stream()), "macm_world_reset")
+        self.done.zero_()
+        return self.obs, self.nbr_id
+
+    def place(self, pos, angle, targets):
+        """Initialise from caller-drawn poses (float32 arrays [E,N,2], [E,N], [E,T,2])."""
+        pos = np.ascontiguousarray(pos, np.float32).reshape(self.E, self.N, 2)
+        angle = np.ascontiguousarray(angle, np.float32).reshape(self.E, self.N)
+        targets = np.ascontiguousarray(targets, np.float32).reshape(self.E, self.T, 2)
+        _abi.check(self.L.macm_world_place(self.h, pos.ctypes.data, angle.ctypes.data, targets.ctypes.data,
+                                           ctypes.byref(self._out_obs), self._stream()), "macm_world_place")
+        self.done.zero_()
+        return self.obs, self.nbr_id
+
+    # -- hot path ------------------------------------------------------------
+    def step(self, actions: torch.Tensor):
+        """actions: discrete uint8/int8 [E,N,3] or continuous float32 [E,N,2], on this device."""
+        if actions.device != self.device or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous tensor on the world's device")
+        if self.cfg.action_mode == _abi.ACTION_DISCRETE:
+            if actions.dtype not in (torch.uint8, torch.int8) or tuple(actions.shape) != (self.E, self.N, 3):
+                raise ValueError(f"discrete actions must be uint8/int8 [{self.E},{self.N},3]")
+        else:
+            if actions.dtype != torch.float32 or tuple(actions.shape) != (self.E, self.N, 2):
+                raise ValueError(f"continuous actions must be float32 [{self.E},{self.N},2]")
+        _abi.check(self.L.macm_world_step(self.h, _ptr(actions), ctypes.byref(self._out), self._stream()),
+                   "macm_world_step")
+        return self.obs, self.nbr_id, self.reward, self.done
+
+    def step_raw(self, actions_ptr: int, stream_handle: int) -> None:
+        """Minimal-overhead launch for timed loops (no validation)."""
+        self.L.macm_world_step(self.h, ctypes.c_void_p(actions_ptr), ctypes.byref(self._out),
+                               ctypes.c_void_p(stream_handle))
+
+    def observe(self):
+        _abi.check(self.L.macm_world_observe(self.h, ctypes.byref(self._out_obs), self._stream()),
+                   "macm_world_observe")
+        return self.obs, self.nbr_id
+
+    # -- state ---------------------------------------------------------------
+    def state_buffers(self):
+        E, N, T, C = self.E, self.N, self.T, self.C
+        return dict(pos=np.zeros((E, N, 2), np.float32), vel=np.zeros((E, N, 2), np.float32),
+                    angle=np.zeros((E, N), np.float32), fat=np.zeros((E, N, 4), np.float32),
+                    sleep=np.zeros((E, N), np.float32), targets=np.zeros((E, T, 2), np.float32),
+                    contact_count=np.zeros((E,), np.int32), contact_ab=np.zeros((E, C), np.uint32),
+                    contact_imp=np.zeros((E, C, 2), np.float32), step_count=np.zeros((E,), np.int32),
+                    time_passed=np.zeros((E,), np.float64))
+
+    def get_state(self) -> dict:
+        s = self.state_buffers()
+        st = _abi.MacmState(*[ctypes.c_void_p(s[k].ctypes.data) for k, _ in _abi.MacmState._fields_])
+        _abi.check(self.L.macm_world_get_state(self.h, ctypes.byref(st), self._stream()), "macm_world_get_state")
+        # entries past each env's contact_count are scratch: zero them so states compare/serialise cleanly
+        idx = np.arange(self.C)[None, :] >= s["contact_count"][:, None]
+        s["contact_ab"][idx] = 0
+        s["contact_imp"][idx] = 0
+        return s
+
+    def set_state(self, s: dict) -> None:
+        ref = self.state_buffers()
+        arrs = {}
+        for k, v in ref.items():
+            a = np.ascontiguousarray(np.asarray(s[k], dtype=v.dtype))
+            if k in ("contact_ab", "contact_imp") and a.shape[1] != self.C:
+                pad = np.zeros_like(v)
+                n = min(a.shape[1], self.C)
+                pad[:, :n] = a[:, :n]
+                a = pad
+            if a.shape != v.shape:
+                raise ValueError(f"state[{k!r}] has shape {a.shape}, expected {v.shape}")
+            arrs[k] = a
+        st = _abi.MacmState(*[ctypes.c_void_p(arrs[k].ctypes.data) for k, _ in _abi.MacmState._fields_])
+        _abi.check(self.L.macm_world_set_state(self.h, ctypes.byref(st), self._stream()), "macm_world_set_state")
+        self.done.copy_(torch.from_numpy((arrs["time_passed"] > self.cfg.time_limit).astype(np.uint8)))
+
+    def status(self) -> int:
+        v = ctypes.c_int32()
+        _abi.check(self.L.macm_world_status(self.h, ctypes.byref(v), self._stream()), "macm_world_status")
+        return int(v.value)
+
+    def counters(self) -> np.ndarray:
+        out = (ctypes.c_int64 * 4)()
+        _abi.check(self.L.macm_world_counters(self.h, out, self._stream()), "macm_world_counters")
+        return np.array(list(out), np.int64)
+
+    def reset_counters(self) -> None:
+        _abi.check(self.L.macm_world_reset_counters(self.h, self._stream()), "macm_world_reset_counters")

@@ -174,6 +174,16 @@ int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const mac
                      void* stream);
 
 /*
+ * Like macm_world_reset, but with caller-drawn poses (host or device pointers):
+ * pos [E, N, 2] float32, angle [E, N] float32, targets [E, T, 2] float32. Used by
+ * the drop-in Flock facade, which draws them from Python's global `random` in
+ * the reference's order (mvmnt.py:47-64) so the caller's RNG stream advances
+ * exactly as the reference's would.
+ */
+int macm_world_place(macm_world* w, const void* pos, const void* angle, const void* targets,
+                     const macm_outputs* out, void* stream);
+
+/*
  * One env.step for all E envs.
  *   actions: device pointer. Discrete: uint8/int8 [E, N, 3] in {0,1,2}
  *   (MultiDiscrete([3,3,3]), mvmnt.py:143-145). Continuous: float32 [E, N, 2] in [-1,1].

@@ -1011,6 +1011,16 @@ void b2l_body_set_state(b2l_world* w, int id, float x, float y, float angle, flo
   }
 }
 
+/* Run the FindNewContacts that b2World::Step performs first when new fixtures
+ * exist (e_newFixture). Doing it before the step is equivalent: the step would
+ * run it on the same fat AABBs before Collide. */
+void b2l_world_flush_new_contacts(b2l_world* w) {
+  if (w->new_fixture) {
+    find_new_contacts(w);
+    w->new_fixture = 0;
+  }
+}
+
 void b2l_world_set_solver_state(b2l_world* w, float inv_dt0, int new_fixture) {
   w->inv_dt0 = inv_dt0;
   w->new_fixture = new_fixture;

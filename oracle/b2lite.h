@@ -71,6 +71,8 @@ void b2l_world_load_contacts(b2l_world* w, int n, const int* ab, const float* im
 /* Direct state injection for parity tests. */
 void b2l_body_set_state(b2l_world* w, int id, float x, float y, float angle, float vx, float vy,
                         float sleep_time, const float* fat4);
+/* Perform the deferred first FindNewContacts now (no-op once stepped). */
+void b2l_world_flush_new_contacts(b2l_world* w);
 /* World-level solver state: inv_dt0 and the "new fixture" flag. */
 void b2l_world_set_solver_state(b2l_world* w, float inv_dt0, int new_fixture);
 

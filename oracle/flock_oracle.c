@@ -318,6 +318,7 @@ void fo_get_state(fo_batch* b, float* pos, float* vel, float* angle, float* fat,
     }
     if (targets) memcpy(targets + (size_t)e * 2 * b->T, en->targets, sizeof(float) * 2 * (size_t)b->T);
     if (contact_count) {
+      b2l_world_flush_new_contacts(en->w);
       int n = b2l_world_contacts(en->w, NULL, 0);
       int* cl = (int*)malloc(sizeof(int) * 3 * (size_t)(n ? n : 1));
       float* im = (float*)malloc(sizeof(float) * 3 * (size_t)(n ? n : 1));

@@ -1,0 +1,42 @@
+"""Helpers comparing the HIP world against the CPU oracle (tests/ only)."""
+import numpy as np
+
+from oracle import OracleFlock
+
+STATE_KEYS = ("pos", "vel", "angle", "fat", "sleep", "targets", "step_count", "time_passed")
+
+
+def assert_state_equal(gs, os_, ctx=""):
+    """Bit-exact state equality (numpy ==, so -0.0 == +0.0; see flock_step_w64.hip
+    'Exactness notes' for why signed zeros of velocity may differ)."""
+    for k in STATE_KEYS:
+        np.testing.assert_array_equal(gs[k], os_[k], err_msg=f"{ctx} state[{k}]")
+    np.testing.assert_array_equal(gs["contact_count"], os_["contact_count"], err_msg=f"{ctx} contact_count")
+    for e in range(gs["contact_count"].shape[0]):
+        n = int(gs["contact_count"][e])
+        np.testing.assert_array_equal(gs["contact_ab"][e, :n], os_["contact_ab"][e, :n],
+                                      err_msg=f"{ctx} env {e} contact order")
+        np.testing.assert_array_equal(gs["contact_imp"][e, :n], os_["contact_imp"][e, :n],
+                                      err_msg=f"{ctx} env {e} impulses")
+
+
+def f32_obs_mismatch(gpu_obs, oracle_obs64):
+    """Count float32 obs entries differing from the oracle's f64 obs rounded to f32."""
+    ref = oracle_obs64.astype(np.float32)
+    d = gpu_obs != ref
+    if not d.any():
+        return 0
+    # tolerate 1-ulp differences (double atan2/cos/sin of ocml vs glibc round differently
+    # in rare cases); anything else is a real mismatch
+    ulp = np.abs(gpu_obs.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    bad = d & (ulp > 1)
+    # angle wrap at exactly +-pi may flip sign: compare modulo 2pi
+    if bad.any():
+        diff = np.abs(((gpu_obs.astype(np.float64) - ref + np.pi) % (2 * np.pi)) - np.pi)
+        bad &= diff > 1e-6
+    assert not bad.any(), f"{int(bad.sum())} obs entries off by more than 1 ulp"
+    return int(d.sum())
+
+
+def oracle_for(cfg, tidx, E, seed, env_offset=0):
+    return OracleFlock(cfg, tidx, E, seed, env_offset)

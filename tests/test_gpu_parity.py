@@ -1,0 +1,193 @@
+"""HIP path vs the CPU oracle, through the C-ABI (libmacm_hip.so).
+
+Bar: bit-exact for positions, velocities, angles, fat AABBs, sleep clocks, the
+ordered contact list with warm-start impulses, neighbour ids, rewards and done;
+observations (float32) equal the oracle's f64 values rounded to f32, with at most
+1 ulp allowed where double atan2/sin/cos of ocml and glibc round differently."""
+import numpy as np
+import pytest
+import torch
+
+import goldens
+from parity import assert_state_equal, f32_obs_mismatch, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+from gym_macm.settings import flockSettings, to_config  # noqa: E402
+from gym_macm.vec import FlockVec  # noqa: E402
+
+
+def make_pair(E, n_agents, seed, targets=None, env_offset=0, obs_dtype=torch.float32, **kw):
+    vec = FlockVec(E, n_agents=n_agents, targets=targets, seed=seed, env_offset=env_offset,
+                   device="cuda:0", obs_dtype=obs_dtype, **kw)
+    N = vec.N
+    cfg = to_config(flockSettings(**kw), N, vec.n_targets, obs_f64=True)
+    orc = oracle_for(cfg, vec.targets_idx, E, seed, env_offset)
+    return vec, orc
+
+
+def rand_actions(rng, E, N):
+    return rng.integers(0, 3, size=(E, N, 3)).astype(np.uint8)
+
+
+def check_rollout(vec, orc, steps, rng, state_every=1, actions_fn=None):
+    E, N = vec.num_envs, vec.N
+    C = vec.world.C
+    assert_state_equal(vec.get_state(), orc.get_state(C), "reset")
+    vec.observe()
+    o0, n0 = orc.observe()
+    np.testing.assert_array_equal(vec.nbr_id.cpu().numpy(), n0)
+    f32_obs_mismatch(vec.obs.cpu().numpy(), o0)
+    ulp_total = 0
+    for t in range(steps):
+        a = actions_fn(t) if actions_fn else rand_actions(rng, E, N)
+        obs, nbr, rew, done = vec.step(torch.from_numpy(a).cuda())
+        r = orc.step(a)
+        np.testing.assert_array_equal(rew.cpu().numpy(), r["reward"].astype(np.float32), err_msg=f"reward step {t}")
+        np.testing.assert_array_equal(nbr.cpu().numpy(), r["nbr_id"], err_msg=f"nbr step {t}")
+        np.testing.assert_array_equal(done.cpu().numpy(), r["done"], err_msg=f"done step {t}")
+        np.testing.assert_array_equal(vec.world.collided.cpu().numpy(), r["collided"], err_msg=f"coll step {t}")
+        ulp_total += f32_obs_mismatch(obs.cpu().numpy(), r["obs"])
+        if (t + 1) % state_every == 0 or t == steps - 1:
+            assert_state_equal(vec.get_state(), orc.get_state(C), f"step {t}")
+    assert vec.status() == 0
+    return ulp_total
+
+
+def test_reset_matches_reference_rng():
+    vec, orc = make_pair(8, [64], seed=1234)
+    assert_state_equal(vec.get_state(), orc.get_state(vec.world.C), "reset")
+
+
+def test_metric_config_rollout_bit_exact():
+    vec, orc = make_pair(32, [64], seed=7)
+    check_rollout(vec, orc, 150, np.random.default_rng(0), state_every=10)
+
+
+def test_dense_start_multibody_islands():
+    # start_spread 6: 64 agents in 36 m^2 -> heavy overlap, large islands, long DFS
+    vec, orc = make_pair(16, [64], seed=3, start_spread=6)
+    check_rollout(vec, orc, 120, np.random.default_rng(1), state_every=5)
+
+
+def test_noop_actions_reach_sleep():
+    # NOOP forces: bodies decelerate and fall asleep (v := 0) after 0.5 s below 0.01 m/s
+    vec, orc = make_pair(8, [16], seed=5, start_spread=8)
+    E, N = 8, 16
+    noop = np.ones((E, N, 3), np.uint8)
+    check_rollout(vec, orc, 160, None, state_every=20, actions_fn=lambda t: noop)
+    s = vec.get_state()
+    assert (s["vel"] == 0).all()
+
+
+def test_small_configs_and_settings():
+    for kw in (dict(n_agents=[4], seed=0), dict(n_agents=[5, 7], seed=21, targets=[0, 1, 2] * 4),
+               dict(n_agents=[16], seed=3, targets=[0] * 8 + [1] * 8, reward_mode="linear", coord="cartesian"),
+               dict(n_agents=[6], seed=2, hz=30.0, time_limit=1.0),
+               dict(n_agents=[33], seed=9, velocityIterations=3, positionIterations=1)):
+        kw = dict(kw)
+        n_agents = kw.pop("n_agents")
+        seed = kw.pop("seed")
+        vec, orc = make_pair(6, n_agents, seed, **kw)
+        check_rollout(vec, orc, 60, np.random.default_rng(seed), state_every=15)
+
+
+def test_continuous_actions():
+    vec, orc = make_pair(8, [12], seed=4, action_mode="continuous")
+    rng = np.random.default_rng(4)
+    E, N = 8, 12
+
+    def acts(t):
+        return rng.uniform(-1, 1, size=(E, N, 2)).astype(np.float32)
+
+    C = vec.world.C
+    for t in range(80):
+        a = acts(t)
+        _, nbr, rew, _ = vec.step(torch.from_numpy(a).cuda())
+        r = orc.step(a)
+        np.testing.assert_array_equal(rew.cpu().numpy(), r["reward"].astype(np.float32))
+        np.testing.assert_array_equal(nbr.cpu().numpy(), r["nbr_id"])
+    assert_state_equal(vec.get_state(), orc.get_state(C), "continuous")
+
+
+def test_state_injection_from_oracle():
+    """Inject an oracle state reached after 40 steps into a fresh GPU world."""
+    E, N = 8, 64
+    vec, orc = make_pair(E, [N], seed=11, start_spread=10)
+    rng = np.random.default_rng(2)
+    for _ in range(40):
+        orc.step(rand_actions(rng, E, N))
+    vec.set_state(orc.get_state(vec.world.C))
+    check_rollout(vec, orc, 40, rng, state_every=10)
+
+
+def test_shard_offsets_are_slices_of_the_full_batch():
+    full = FlockVec(8, n_agents=[64], seed=99, device="cuda:0")
+    part = FlockVec(4, n_agents=[64], seed=99, env_offset=4, device="cuda:0")
+    rng = np.random.default_rng(5)
+    for _ in range(30):
+        a = rand_actions(rng, 8, 64)
+        _, _, rf, _ = full.step(torch.from_numpy(a).cuda())
+        _, _, rp, _ = part.step(torch.from_numpy(a[4:]).cuda())
+        np.testing.assert_array_equal(rf.cpu().numpy()[4:], rp.cpu().numpy())
+    sf, sp = full.get_state(), part.get_state()
+    np.testing.assert_array_equal(sf["pos"][4:], sp["pos"])
+
+
+def test_determinism_two_runs_identical():
+    rng = np.random.default_rng(8)
+    acts = [rand_actions(rng, 16, 64) for _ in range(40)]
+    outs = []
+    for _ in range(2):
+        v = FlockVec(16, n_agents=[64], seed=5, device="cuda:0")
+        for a in acts:
+            v.step(torch.from_numpy(a).cuda())
+        outs.append(v.get_state())
+    assert_state_equal(outs[0], outs[1], "second run")
+
+
+def test_contact_overflow_is_reported():
+    v = FlockVec(4, n_agents=[64], seed=3, device="cuda:0", start_spread=4, max_contacts=8)
+    v.step(torch.ones((4, 64, 3), dtype=torch.uint8, device="cuda:0"))
+    assert v.status() & 1
+
+
+def test_counters():
+    v = FlockVec(8, n_agents=[32], seed=1, device="cuda:0")
+    v.world.reset_counters()
+    a = torch.ones((8, 32, 3), dtype=torch.uint8, device="cuda:0")
+    coll = 0
+    for _ in range(5):
+        v.step(a)
+        coll += int(v.world.collided.sum().item())
+    c = v.counters()
+    assert c[0] == 5 * 8 * 32 and c[1] == coll
+
+
+@pytest.mark.parametrize("name", goldens.names())
+def test_dropin_flock_matches_reference_goldens(name):
+    """The drop-in dict API (gym_macm.envs.Flock over the HIP world) reproduces the
+    reference env's own outputs (tests/golden, made from mvmnt.py)."""
+    import random
+    from gym_macm.envs import Flock
+    g = goldens.load(name)
+    m = g["meta"]
+    random.seed(m["seed"])
+    env = Flock(n_agents=m["n_agents"], targets=m["targets"], device="cuda:0", **m["kwargs"])
+    N = m["N"]
+    for t in range(m["steps"]):
+        if m["policy"] == "random_cont":
+            acts = {i: g["actions"][t][i].astype(np.float32) for i in range(N)}
+        else:
+            acts = {i: g["actions"][t][i].astype(np.int64) for i in range(N)}
+        obs, rewards = env.step(acts)
+        assert [rewards[i] for i in range(N)] == list(g["reward"][t]), f"rewards step {t}"
+        nbr = np.array([obs[i]["nodes"][0]["id"] for i in range(N)])
+        np.testing.assert_array_equal(nbr, g["nbr"][t], err_msg=f"nbr step {t}")
+        pos = np.array([np.concatenate([obs[i]["nodes"][0]["position"], obs[i]["nodes"][1]["position"]])
+                        for i in range(N)])
+        assert goldens.obs_close(pos, g["obs"][t], pos.shape[1]), f"obs step {t}"
+        assert env.done == bool(g["done"][t])
+    s = env.world.get_state()
+    np.testing.assert_array_equal(s["pos"][0], g["pos"][-1])
+    np.testing.assert_array_equal(s["angle"][0], g["angle"][-1])
