@@ -63,6 +63,7 @@ struct WorldBuffers {
   uint8_t* done;       // [E]
   int32_t* status;     // [E]      MACM_ST_* bits
   unsigned long long* counters;  // [4]
+  unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
 };
 
 }  // namespace macm

@@ -40,6 +40,29 @@ constexpr int TCAP = 256;   // touching contacts per env held in LDS
 constexpr int DEG = 16;     // touching contacts per body
 constexpr int ICAP = W / 2; // islands with >= 1 contact (>= 2 bodies each)
 
+// Diagnostic build only (-DMACM_STAMPS, libmacm_hip_stamps.so via `make stamps`):
+// lane 0 records s_memtime at phase boundaries into B.stamps[e][0..13] and per-env
+// sizes into [14..15]. The product library compiles these to nothing.
+#ifdef MACM_STAMPS
+#define STAMP(k)                                                                    \
+  do {                                                                              \
+    __builtin_amdgcn_s_waitcnt(0);                                                  \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                     \
+    if (lane == 0) B.stamps[(size_t)e * 16 + (k)] = _t;                             \
+  } while (0)
+#define STAMP_STAT(k, v)                                                            \
+  do {                                                                              \
+    if (lane == 0) B.stamps[(size_t)e * 16 + (k)] = (unsigned long long)(v);        \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#define STAMP_STAT(k, v) \
+  do {                   \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }  // b2Min
 __device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }  // b2Max
 __device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
@@ -170,6 +193,9 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   __shared__ uint8_t s_isolved[ICAP];
   __shared__ float s_slp[W];
   __shared__ int s_nisl;
+#ifdef MACM_STAMPS
+  __shared__ int s_stat_maxisl;
+#endif
 
   // ---- load ---------------------------------------------------------------
   float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f);
@@ -191,6 +217,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   const int step_count = B.step_count[e];
   const int M = B.ccount[cur][e];
   int status = 0;
+  STAMP(0);
 
   // ---- actions -> angle, force (mvmnt.py:97-129) --------------------------
   float Fx = 0.0f, Fy = 0.0f;
@@ -226,6 +253,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     Fy = 0.0f + Fy;
   }
   __syncthreads();
+  STAMP(1);
 
   // ---- Collide: touching contacts of the ordered list ---------------------
   const float rr = (P.radius + P.radius) * (P.radius + P.radius);
@@ -260,6 +288,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     T = TCAP;
   }
   __syncthreads();
+  STAMP(2);
 
   // ---- per-body touching edges in list (= Box2D edge) order ----------------
   {
@@ -280,6 +309,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     s_deg[lane] = (uint8_t)deg;
   }
   __syncthreads();
+  STAMP(3);
 
   // ---- island DFS in Box2D order (b2World::Solve), serial on lane 0 --------
   if (lane == 0) {
@@ -319,6 +349,13 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       ++nisl;
     }
     s_ic[nisl] = (int16_t)nord;
+#ifdef MACM_STAMPS
+    {
+      int mx = 0;
+      for (int q = 0; q < nisl; ++q) mx = max(mx, (int)s_ic[q + 1] - (int)s_ic[q]);
+      s_stat_maxisl = mx;
+    }
+#endif
     s_ib[nisl] = (int16_t)nb;
     s_nisl = nisl;
   }
@@ -350,6 +387,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     s_tny[t] = ny;
   }
   __syncthreads();
+  STAMP(4);
 
   const int nisl = s_nisl;
   const float mA = P.inv_mass, mB = P.inv_mass;
@@ -420,6 +458,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     }
   }
   __syncthreads();
+  STAMP(5);
 
   // ---- integrate positions --------------------------------------------------
   float cx = p.x, cy = p.y;
@@ -438,6 +477,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     s_cy[lane] = cy;
   }
   __syncthreads();
+  STAMP(6);
 
   // ---- position iterations, one lane per island ------------------------------
   for (int I = lane; I < nisl; I += W) {
@@ -483,6 +523,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     s_slp[lane] = ns;
   }
   __syncthreads();
+  STAMP(7);
 
   // ---- island sleep decision ---------------------------------------------------
   if (act && s_bisl[lane] < 0) s_sleepnow[lane] = (ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
@@ -494,6 +535,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     for (int k = b0; k < b1; ++k) s_sleepnow[s_ibodies[k]] = sl;
   }
   __syncthreads();
+  STAMP(8);
 
   // ---- SynchronizeFixtures: fat-AABB update ------------------------------------
   float4 fn = fo;
@@ -519,6 +561,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   }
   s_fn[lane] = fn;
   __syncthreads();
+  STAMP(9);
 
   // ---- contact set, new pairs, nearest neighbour -------------------------------
   bool coll = false;
@@ -535,6 +578,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     nearest(N, lane, cx, cy, s_cx, s_cy, best, bj);
   }
 
+  STAMP(10);
   // ---- next ordered list: new pairs (desc) ++ surviving old pairs --------------
   uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
   float2* ocimp = B.cimp[nxt] + (size_t)e * C;
@@ -572,6 +616,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     total = C;
   }
 
+  STAMP(11);
   // ---- rewards (mvmnt.py:160-179) and obs (mvmnt.py:181-222) -------------------
   float rew = 0.0f;
   if (act) {
@@ -595,6 +640,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     B.sleep[ag] = ns;
   }
 
+  STAMP(12);
   // ---- per-env bookkeeping + counters -------------------------------------------
   const unsigned long long mcoll = __ballot(act && coll);
   const unsigned long long mpos = __ballot(act && rew > 0.0f);
@@ -614,6 +660,9 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     atomicAdd(&B.counters[2], (unsigned long long)__popcll(mpos));
     atomicAdd(&B.counters[3], (unsigned long long)dn);
   }
+  STAMP(13);
+  STAMP_STAT(14, (unsigned long long)T | ((unsigned long long)nisl << 16) | ((unsigned long long)M << 32));
+  STAMP_STAT(15, (unsigned long long)s_stat_maxisl | ((unsigned long long)total << 32));
 }
 
 // Initial proxies (b2DynamicTree::CreateProxy: fat = tight +- 0.1), the first

@@ -201,7 +201,11 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       (rc = dalloc(w, &B.cimp[0], (size_t)n_envs * C)) || (rc = dalloc(w, &B.cimp[1], (size_t)n_envs * C)) ||
       (rc = dalloc(w, &B.step_count, (size_t)n_envs)) || (rc = dalloc(w, &B.time_passed, (size_t)n_envs)) ||
       (rc = dalloc(w, &B.done, (size_t)n_envs)) || (rc = dalloc(w, &B.status, (size_t)n_envs)) ||
-      (rc = dalloc(w, &B.counters, 4))) {
+      (rc = dalloc(w, &B.counters, 4))
+#ifdef MACM_STAMPS
+      || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 16))
+#endif
+  ) {
     free_world(w);
     delete w;
     return rc;
@@ -385,5 +389,16 @@ int macm_world_reset_counters(macm_world* w, void* stream) {
   HIP_TRY(hipMemsetAsync(w->B.counters, 0, 4 * sizeof(unsigned long long), (hipStream_t)stream));
   return MACM_OK;
 }
+
+#ifdef MACM_STAMPS
+// Diagnostic build only: copy the per-env phase stamps [E, 16] of the last step.
+int macm_debug_stamps(macm_world* w, unsigned long long* out) {
+  if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  HIP_TRY(hipMemcpy(out, w->B.stamps, (size_t)w->P.n_envs * 16 * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  return MACM_OK;
+}
+#endif
 
 }  // extern "C"

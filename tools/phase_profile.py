@@ -1,0 +1,89 @@
+"""Per-phase cycle shares of flock_step_w64 from the diagnostic stamp build.
+
+    make -C gym-macm_amd stamps && python tools/phase_profile.py [--envs 4096] [--steps 20]
+
+Loads build/libmacm_hip_stamps.so (in-kernel s_memtime at phase boundaries; see
+STAMP() in csrc/flock_step_w64.hip). Read SHARES, not absolute time: the stamps'
+s_waitcnt(0) forbids overlaps the product kernel has.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MACM_LIB"] = os.path.join(REPO, "gym-macm_amd", "build", "libmacm_hip_stamps.so")
+sys.path.insert(0, os.path.join(REPO, "gym-macm_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from gym_macm import _abi  # noqa: E402
+from gym_macm.vec import FlockVec  # noqa: E402
+
+PHASES = ["actions", "collide", "adjacency", "dfs+integrate+normals", "velocity_solve", "integrate_pos",
+          "position_solve+sleepclk", "sleep_decision", "sync_fixtures", "pairs+nearest", "list_build",
+          "reward+obs+writeback", "bookkeeping"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--agents", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--spread", type=float, default=20.0)
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    L = _abi.lib()
+    L.macm_debug_stamps.restype = ctypes.c_int
+    L.macm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    E, N = args.envs, args.agents
+    vec = FlockVec(E, n_agents=[N], seed=0x6D61636D, device="cuda:0", start_spread=args.spread)
+    gen = torch.Generator(device="cuda:0")
+    gen.manual_seed(1)
+    buf = np.zeros((E, 16), np.uint64)
+    deltas, stats, walls = [], [], []
+    for s in range(args.warmup + args.steps):
+        a = torch.randint(0, 3, (E, N, 3), dtype=torch.uint8, device="cuda:0", generator=gen)
+        if s >= args.warmup:
+            torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        vec.step(a)
+        if s >= args.warmup:
+            ev1.record()
+            torch.cuda.synchronize()
+            walls.append(ev0.elapsed_time(ev1))
+            _abi.check(L.macm_debug_stamps(vec.world.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))),
+                       "stamps")
+            t = buf[:, :14].astype(np.int64)
+            deltas.append(np.diff(t, axis=1))
+            stats.append(buf[:, 14:].copy())
+    d = np.concatenate(deltas)  # [steps*E, 13]
+    st = np.concatenate(stats)
+    total = d.sum(axis=1)
+    out = {"envs": E, "agents": N, "spread": args.spread, "kernel_ms_stamped": float(np.mean(walls)),
+           "wave_cycles_mean": float(total.mean()), "wave_cycles_p95": float(np.percentile(total, 95)),
+           "wave_cycles_max": float(total.max()), "phases": {}}
+    for k, name in enumerate(PHASES):
+        col = d[:, k]
+        out["phases"][name] = {"mean": float(col.mean()), "p95": float(np.percentile(col, 95)),
+                               "max": float(col.max()), "share": float(col.sum() / total.sum())}
+    T = (st[:, 0] & 0xFFFF).astype(np.int64)
+    nisl = ((st[:, 0] >> 16) & 0xFFFF).astype(np.int64)
+    M = (st[:, 0] >> 32).astype(np.int64)
+    maxisl = (st[:, 1] & 0xFFFFFFFF).astype(np.int64)
+    cnt = (st[:, 1] >> 32).astype(np.int64)
+    for name, v in (("touching", T), ("islands", nisl), ("list_in", M), ("max_island_contacts", maxisl),
+                    ("list_out", cnt)):
+        out[name] = {"mean": float(v.mean()), "p95": float(np.percentile(v, 95)), "max": int(v.max())}
+    print(json.dumps(out, indent=1))
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
