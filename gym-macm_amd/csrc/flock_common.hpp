@@ -62,7 +62,7 @@ struct WorldBuffers {
   double* time_passed; // [E]
   uint8_t* done;       // [E]
   int32_t* status;     // [E]      MACM_ST_* bits
-  unsigned long long* counters;  // [4]
+  unsigned long long* env_counters;  // [E, 4] per-env accumulators (see macm_world_counters)
   unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
 };
 

@@ -1,8 +1,8 @@
 // flock_step_w64.hip — batched Flock env.step for N <= 64 agents per env on gfx950.
 //
 // One 64-lane wavefront advances one env; lane i owns agent i. Per-env state is
-// staged in LDS for the duration of the step (≈11 KB) and written back once.
-// The step restates, in one launch:
+// staged in registers + LDS (< 10 KB, so 16 envs fit a CU and a 4096-env step is
+// one dispatch round) and written back once. The step restates, in one launch:
 //   action -> angle/force                gym_macm/envs/mvmnt.py:97-129
 //   b2World::Step(1/hz, 8, 3)            gym_macm/cm_framework.py:222-223 [EXT-B2D]
 //     Collide (contact persistence, circle manifolds, warm-start carry)
@@ -26,6 +26,14 @@
 // restricted to the body's contacts, so the DFS below visits contacts in exactly
 // Box2D's order and the solver reproduces Box2D's rounding sequence.
 //
+// Where the time goes (tools/phase_profile.py, profiles/r01/): the step is
+// latency-bound, not bandwidth-bound — a few dependent global round trips plus
+// short serial chains (DFS, per-island Gauss-Seidel). Hence: every global load
+// the step needs is issued up front; list entries and their impulses arrive in
+// one round trip and stay in registers; all-pairs loops broadcast lane values
+// with v_readlane (uniform j) instead of LDS round trips; the DFS seeds only
+// bodies that have touching edges; per-env counters instead of global atomics.
+//
 // Exactness notes (checked by tests/test_gpu_parity.py against the oracle):
 //   * fixedRotation bodies have invI = 0 and w = 0, so every angular term in the
 //     solver is a signed zero; dropping them can change only the sign of a zero
@@ -35,12 +43,13 @@
 
 namespace macm {
 
-constexpr int W = 64;       // wavefront = envs' agent lanes
-constexpr int TCAP = 256;   // touching contacts per env held in LDS
+constexpr int W = 64;       // wavefront = one env's agent lanes
+constexpr int TCAP = 256;   // touching contacts per env held in LDS (indices fit uint8)
 constexpr int DEG = 16;     // touching contacts per body
 constexpr int ICAP = W / 2; // islands with >= 1 contact (>= 2 bodies each)
+constexpr int RCH = 2;      // list chunks (of 64 entries) cached in registers
 
-// Diagnostic build only (-DMACM_STAMPS, libmacm_hip_stamps.so via `make stamps`):
+// Diagnostic build only (-DMACM_STAMPS, build/libmacm_hip_stamps.so via `make stamps`):
 // lane 0 records s_memtime at phase boundaries into B.stamps[e][0..13] and per-env
 // sizes into [14..15]. The product library compiles these to nothing.
 #ifdef MACM_STAMPS
@@ -96,47 +105,46 @@ __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// One agent's record for the all-pairs sweep: read by LDS broadcast (2 x ds_read_b128).
+struct __align__(32) PairRec {
+  float4 fn;  // fat AABB after SynchronizeFixtures
+  float2 c;   // final position
+  float2 pad;
+};
+
+// v_readlane with a wave-uniform lane index: broadcast without an LDS round trip.
+__device__ __forceinline__ float bcast(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
 template <typename OT>
-__device__ __forceinline__ void write_node(OT* o, int coord, double r, double t) {
+__device__ __forceinline__ void write_obs_row(OT* o, int coord, double r0, double t0, double r1, double t1) {
   if (coord == MACM_COORD_CARTESIAN) {
-    o[0] = (OT)r;
-    o[1] = (OT)cos(t);
-    o[2] = (OT)sin(t);
+    o[0] = (OT)r0;
+    o[1] = (OT)cos(t0);
+    o[2] = (OT)sin(t0);
+    o[3] = (OT)r1;
+    o[4] = (OT)cos(t1);
+    o[5] = (OT)sin(t1);
+  } else if constexpr (sizeof(OT) == 4) {
+    *reinterpret_cast<float4*>(o) = make_float4((float)r0, (float)t0, (float)r1, (float)t1);
   } else {
-    o[0] = (OT)r;
-    o[1] = (OT)t;
+    o[0] = (OT)r0;
+    o[1] = (OT)t0;
+    o[2] = (OT)r1;
+    o[3] = (OT)t1;
   }
 }
 
-// Flock.get_obs for agent `lane` given final positions in LDS (mvmnt.py:181-222).
-// best/bj: squared distance and index of the closest other agent.
+// Flock.get_obs for one agent (mvmnt.py:181-222): node 0 = closest other agent
+// (squared distance `best`, relative position (rx, ry) = other - self, float32),
+// node 1 = the agent's target (relative position target - self, float32).
 template <typename OT>
-__device__ __forceinline__ void write_obs(const StepParams& P, OT* obs_e, int lane, float cx, float cy,
-                                          float ang, float best, int bj, const float* s_cx,
-                                          const float* s_cy, float tdx, float tdy, float td2) {
-  const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-  OT* o = obs_e + (size_t)lane * od;
-  const float rx = s_cx[bj] - cx, ry = s_cy[bj] - cy;  // other.position - agent.position (f32)
-  double t = atan2((double)ry, (double)rx) - (double)ang;
-  write_node(o, P.coord, sqrt((double)best), wrap_pi(t));
-  t = atan2((double)tdy, (double)tdx) - (double)ang;
-  write_node(o + od / 2, P.coord, sqrt((double)td2), wrap_pi(t));
-}
-
-// Nearest other agent by float32 squared distance, strict '<' (lowest index wins
-// ties; the reference compares sqrt() values, a strictly monotone map of these).
-__device__ __forceinline__ void nearest(int N, int lane, float cx, float cy, const float* s_cx,
-                                        const float* s_cy, float& best, int& bj) {
-  best = __builtin_inff();
-  bj = lane == 0 ? 1 : 0;
-  for (int j = 0; j < N; ++j) {
-    const float dx = s_cx[j] - cx, dy = s_cy[j] - cy;
-    const float d2 = dx * dx + dy * dy;
-    if (j != lane && d2 < best) {
-      best = d2;
-      bj = j;
-    }
-  }
+__device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float best, float rx, float ry, float tdx,
+                                          float tdy, float td2) {
+  const double t0 = wrap_pi(atan2((double)ry, (double)rx) - (double)ang);
+  const double t1 = wrap_pi(atan2((double)tdy, (double)tdx) - (double)ang);
+  write_obs_row(o, coord, sqrt((double)best), t0, sqrt((double)td2), t1);
 }
 
 // New-pair compaction in descending (a, b) order: lane a owns the bitmask of
@@ -180,42 +188,89 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   const int nxt = cur ^ 1;
   const unsigned long long lt = lanemask_lt(lane);
 
-  __shared__ float s_cx[W], s_cy[W], s_vx[W], s_vy[W], s_c0x[W], s_c0y[W];
-  __shared__ float4 s_fo[W], s_fn[W];
+  __shared__ float s_cx[W], s_cy[W], s_vx[W], s_vy[W];
   __shared__ uint32_t s_tab[TCAP];
-  __shared__ float s_tln[TCAP], s_tlt[TCAP], s_tnx[TCAP], s_tny[TCAP];
-  __shared__ uint16_t s_adj[W * DEG];
-  __shared__ uint16_t s_ord[TCAP];
+  __shared__ float s_tln[TCAP], s_tlt[TCAP];
+  // contact normals live until the velocity solve ends; the all-pairs records are
+  // written after it, so both share one LDS region
+  __shared__ __align__(32) float s_tn[2 * TCAP];
+  float* const s_tnx = s_tn;
+  float* const s_tny = s_tn + TCAP;
+  PairRec* const s_pj = reinterpret_cast<PairRec*>(s_tn);
+  static_assert(sizeof(PairRec) * W <= sizeof(float) * 2 * TCAP, "s_pj must fit in s_tn");
+  __shared__ uint8_t s_adj[W * DEG];
+  __shared__ uint8_t s_ord[TCAP];
   __shared__ uint32_t s_cvis[TCAP / 32];
   __shared__ uint8_t s_deg[W], s_stack[W], s_ibodies[W], s_sleepnow[W];
-  __shared__ int8_t s_bisl[W];
-  __shared__ int16_t s_ic[ICAP + 1], s_ib[ICAP + 1];
+  __shared__ uint16_t s_ic[ICAP + 1];
+  __shared__ uint8_t s_ib[ICAP + 1];
   __shared__ uint8_t s_isolved[ICAP];
   __shared__ float s_slp[W];
+  __shared__ uint32_t s_oldm[2 * W];  // per agent: 64-bit mask of partners in the old list
   __shared__ int s_nisl;
 #ifdef MACM_STAMPS
   __shared__ int s_stat_maxisl;
 #endif
 
-  // ---- load ---------------------------------------------------------------
-  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f);
+  // ---- every global load the step needs, issued up front ---------------------
+  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
+  const float2* cimp = B.cimp[cur] + (size_t)e * C;
+  const int step_count = B.step_count[e];
+  const int M = B.ccount[cur][e];
+  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
   float ang = 0.0f, slp = 0.0f;
   float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  int a0 = 1, a1 = 1, a2 = 1;
+  float ax = 0.0f, ay = 0.0f;
   if (act) {
     p = B.pos[ag];
     v = B.vel[ag];
     ang = B.angle[ag];
     fo = B.fat[ag];
     slp = B.sleep[ag];
+    if (P.action_mode == MACM_ACTION_DISCRETE) {
+      const uint8_t* a = (const uint8_t*)actions + ag * 3;
+      a0 = a[0];
+      a1 = a[1];
+      a2 = a[2];
+    } else {
+      const float2 c = ((const float2*)actions)[ag];
+      ax = c.x;
+      ay = c.y;
+    }
+    tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+  }
+  double time_passed = 0.0;
+  int st_prev = 0;
+  unsigned long long ctr[4] = {0ull, 0ull, 0ull, 0ull};
+  if (lane == 0) {
+    time_passed = B.time_passed[e];
+    st_prev = B.status[e];
+    const ulonglong2* ec = reinterpret_cast<const ulonglong2*>(B.env_counters + (size_t)e * 4);
+    const ulonglong2 c01 = ec[0], c23 = ec[1];
+    ctr[0] = c01.x;
+    ctr[1] = c01.y;
+    ctr[2] = c23.x;
+    ctr[3] = c23.y;
+  }
+  // list entries (and their warm-start impulses) of the first RCH chunks stay in registers
+  uint32_t rab[RCH];
+  float2 rim[RCH];
+#pragma unroll
+  for (int c = 0; c < RCH; ++c) {
+    const int k = c * W + lane;
+    rab[c] = 0u;
+    rim[c] = make_float2(0.0f, 0.0f);
+    if (k < M) {
+      rab[c] = cab[k];
+      rim[c] = cimp[k];
+    }
   }
   s_cx[lane] = p.x;
   s_cy[lane] = p.y;
-  s_c0x[lane] = p.x;
-  s_c0y[lane] = p.y;
-  s_fo[lane] = fo;
   if (lane < TCAP / 32) s_cvis[lane] = 0u;
-  const int step_count = B.step_count[e];
-  const int M = B.ccount[cur][e];
+  s_oldm[2 * lane] = 0u;
+  s_oldm[2 * lane + 1] = 0u;
   int status = 0;
   STAMP(0);
 
@@ -223,8 +278,6 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   float Fx = 0.0f, Fy = 0.0f;
   if (act) {
     if (P.action_mode == MACM_ACTION_DISCRETE) {
-      const uint8_t* a = (const uint8_t*)actions + ag * 3;
-      const int a0 = a[0], a1 = a[1], a2 = a[2];
       // agent.body.angle = angle + (a2-1) * rotation_speed * (1/hz) -> SetTransform(float32)
       float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
       double ad = (double)af;
@@ -240,8 +293,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       Fx = (float)fx;  // ApplyForce: b2Vec2(float32) accumulated onto m_force = 0
       Fy = (float)fy;
     } else {
-      const float* a = (const float*)actions + ag * 2;
-      float x = a[0], y = a[1];
+      float x = ax, y = ay;
       if ((x * x + y * y) > 1.0f) {
         x = sqrtf(x * x / (x * x + y * y));
         y = sqrtf(y * y / (x * x + y * y));
@@ -258,24 +310,36 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   // ---- Collide: touching contacts of the ordered list ---------------------
   const float rr = (P.radius + P.radius) * (P.radius + P.radius);
   const float dt_ratio = step_count > 0 ? P.inv_dt * P.dt : 0.0f;  // m_inv_dt0 * dt
-  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
-  const float2* cimp = B.cimp[cur] + (size_t)e * C;
   int T = 0;
-  for (int k0 = 0; k0 < M; k0 += W) {
-    const int k = k0 + lane;
-    bool touch = false;
-    uint32_t ab = 0;
-    if (k < M) {
+  uint32_t tbits = 0u;  // bit c: this lane's entry of chunk c touches (M <= C <= 2016 -> < 32 chunks)
+  for (int c = 0; c * W < M; ++c) {
+    const int k = c * W + lane;
+    uint32_t ab = 0u;
+    float2 lam = make_float2(0.0f, 0.0f);
+    if (c < RCH) {
+#pragma unroll
+      for (int q = 0; q < RCH; ++q)
+        if (q == c) {
+          ab = rab[q];
+          lam = rim[q];
+        }
+    } else if (k < M) {
       ab = cab[k];
+      lam = cimp[k];
+    }
+    bool touch = false;
+    if (k < M) {
       const int a = ab & 0xffffu, b = ab >> 16;
       const float dx = s_cx[b] - s_cx[a], dy = s_cy[b] - s_cy[a];
       touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+      atomicOr(&s_oldm[2 * a + (b >> 5)], 1u << (b & 31));
+      atomicOr(&s_oldm[2 * b + (a >> 5)], 1u << (a & 31));
     }
     const unsigned long long m = __ballot(touch);
     if (touch) {
+      tbits |= 1u << c;
       const int slot = T + __popcll(m & lt);
       if (slot < TCAP) {
-        const float2 lam = cimp[k];
         s_tab[slot] = ab;
         s_tln[slot] = P.warm_starting ? dt_ratio * lam.x : 0.0f;
         s_tlt[slot] = P.warm_starting ? dt_ratio * lam.y : 0.0f;
@@ -291,53 +355,49 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   STAMP(2);
 
   // ---- per-body touching edges in list (= Box2D edge) order ----------------
-  {
-    int deg = 0;
-    if (act) {
-      for (int t = 0; t < T; ++t) {
-        const uint32_t ab = s_tab[t];
-        if ((int)(ab & 0xffffu) == lane || (int)(ab >> 16) == lane) {
-          if (deg < DEG) s_adj[lane * DEG + deg] = (uint16_t)t;
-          ++deg;
-        }
+  int deg = 0;
+  if (act) {
+    for (int t = 0; t < T; ++t) {
+      const uint32_t ab = s_tab[t];
+      if ((int)(ab & 0xffffu) == lane || (int)(ab >> 16) == lane) {
+        if (deg < DEG) s_adj[lane * DEG + deg] = (uint8_t)t;
+        ++deg;
       }
     }
-    if (deg > DEG) {
-      status |= MACM_ST_DEGREE_OVERFLOW;
-      deg = DEG;
-    }
-    s_deg[lane] = (uint8_t)deg;
   }
+  if (deg > DEG) {
+    status |= MACM_ST_DEGREE_OVERFLOW;
+    deg = DEG;
+  }
+  s_deg[lane] = (uint8_t)deg;
+  const unsigned long long hasdeg = __ballot(act && deg > 0);
   __syncthreads();
   STAMP(3);
 
   // ---- island DFS in Box2D order (b2World::Solve), serial on lane 0 --------
-  if (lane == 0) {
-    unsigned long long vis = 0ull;
+  // Seeds in body-list order (reverse creation); bodies without touching
+  // edges are singleton islands and contribute no contact order, so only
+  // bodies in `hasdeg` are walked.
+  if (lane == 0 && hasdeg) {
+    unsigned long long vis = ~hasdeg;
     int nord = 0, nisl = 0, nb = 0;
-    for (int s = N - 1; s >= 0; --s) {  // body list = reverse creation order
-      if ((vis >> s) & 1ull) continue;
-      if (s_deg[s] == 0) {
-        vis |= 1ull << s;
-        s_bisl[s] = -1;
-        continue;
-      }
-      s_ic[nisl] = (int16_t)nord;
-      s_ib[nisl] = (int16_t)nb;
+    for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
+      const int s = 63 - __clzll(todo);
+      s_ic[nisl] = (uint16_t)nord;
+      s_ib[nisl] = (uint8_t)nb;
       int sp = 0;
       s_stack[sp++] = (uint8_t)s;
       vis |= 1ull << s;
       while (sp > 0) {
         const int b = s_stack[--sp];
         s_ibodies[nb++] = (uint8_t)b;
-        s_bisl[b] = (int8_t)nisl;
         const int db = s_deg[b];
         for (int q = 0; q < db; ++q) {
           const int t = s_adj[b * DEG + q];
           const uint32_t bit = 1u << (t & 31);
           if (s_cvis[t >> 5] & bit) continue;
           s_cvis[t >> 5] |= bit;
-          s_ord[nord++] = (uint16_t)t;
+          s_ord[nord++] = (uint8_t)t;
           const uint32_t ab = s_tab[t];
           const int a = ab & 0xffffu, bb = ab >> 16;
           const int o = (a == b) ? bb : a;
@@ -348,7 +408,9 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       }
       ++nisl;
     }
-    s_ic[nisl] = (int16_t)nord;
+    s_ic[nisl] = (uint16_t)nord;
+    s_ib[nisl] = (uint8_t)nb;
+    s_nisl = nisl;
 #ifdef MACM_STAMPS
     {
       int mx = 0;
@@ -356,8 +418,12 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       s_stat_maxisl = mx;
     }
 #endif
-    s_ib[nisl] = (int16_t)nb;
-    s_nisl = nisl;
+  }
+  if (lane == 0 && !hasdeg) {
+    s_nisl = 0;
+#ifdef MACM_STAMPS
+    s_stat_maxisl = 0;
+#endif
   }
 
   // ---- integrate velocities + damping (b2Island::Solve) --------------------
@@ -526,7 +592,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   STAMP(7);
 
   // ---- island sleep decision ---------------------------------------------------
-  if (act && s_bisl[lane] < 0) s_sleepnow[lane] = (ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
+  if (act && deg == 0) s_sleepnow[lane] = (ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
   for (int I = lane; I < nisl; I += W) {
     const int b0 = s_ib[I], b1 = s_ib[I + 1];
     float mn = 3.402823466e+38f;
@@ -559,41 +625,75 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       ns = 0.0f;
     }
   }
-  s_fn[lane] = fn;
-  __syncthreads();
+  {
+    // per-agent record for the all-pairs sweep; lanes >= N hold a dummy whose AABB
+    // overlaps nothing and whose position is infinitely far away
+    PairRec r;
+    r.fn = act ? fn : make_float4(__builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff());
+    r.c = act ? make_float2(cx, cy) : make_float2(__builtin_inff(), __builtin_inff());
+    r.pad = make_float2(0.0f, 0.0f);
+    s_pj[lane] = r;
+  }
+  __syncthreads();  // s_pj and final s_cx/s_cy visible to every lane
   STAMP(9);
 
-  // ---- contact set, new pairs, nearest neighbour -------------------------------
-  bool coll = false;
-  unsigned long long newmask = 0ull;
-  float best;
-  int bj;
-  if (act) {
-    for (int j = 0; j < N; ++j) {
-      const float4 foj = s_fo[j], fnj = s_fn[j];
-      const bool ovo = overlap(fo, foj), ovn = overlap(fn, fnj);
-      if (j != lane) coll |= ovo | ovn;
-      if (j > lane && ovn && !ovo) newmask |= 1ull << j;
+  // ---- contact set, new pairs, nearest neighbour ---------------------------------
+  // The old list IS Ov(F_{t-1}), so only the new fat AABBs are tested here:
+  //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t)        
+  //   FindNewContacts creates        Ov(F_t) \ Ov(F_{t-1})
+  // Overlap is symmetric, so the ballot of ovn at iteration j is agent j's
+  // partner row; lane j keeps it. Agent j's record arrives by LDS broadcast.
+  const unsigned long long valid = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+  unsigned long long myov = 0ull;
+  float best = __builtin_inff();
+  int bj = lane == 0 ? 1 : 0;
+  const int N4 = (N + 3) & ~3;
+  for (int j0 = 0; j0 < N4; j0 += 4) {
+    PairRec q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = s_pj[j0 + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u;
+      const float4 fj = q[u].fn;
+      // b2TestOverlap(fn, fj): (fj.lo - fn.hi > 0) == (fj.lo > fn.hi) for IEEE floats
+      const bool sep = (fj.x > fn.z) | (fj.y > fn.w) | (fn.x > fj.z) | (fn.y > fj.w);
+      const unsigned long long row = __ballot(!sep) & valid;
+      myov = (lane == j) ? row : myov;
+      const float dx = q[u].c.x - cx, dy = q[u].c.y - cy;  // other.position - agent.position
+      const float d2 = dx * dx + dy * dy;                 // b2DistanceSquared(other, agent)
+      const bool better = (j != lane) & (d2 < best);      // strict '<': lowest index wins (mvmnt.py:194)
+      best = better ? d2 : best;
+      bj = better ? j : bj;
     }
-    nearest(N, lane, cx, cy, s_cx, s_cy, best, bj);
   }
-
+  myov &= ~(1ull << lane);
+  const unsigned long long oldm = (unsigned long long)s_oldm[2 * lane] | ((unsigned long long)s_oldm[2 * lane + 1] << 32);
+  const bool coll = act && ((myov | oldm) != 0ull);
+  const unsigned long long above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+  const unsigned long long newmask = act ? (myov & ~oldm & above) : 0ull;
   STAMP(10);
+
   // ---- next ordered list: new pairs (desc) ++ surviving old pairs --------------
   uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
   float2* ocimp = B.cimp[nxt] + (size_t)e * C;
   const int nnew = write_new_pairs(lane, newmask, ocab, ocimp, C);
   int kept = 0, Tr = 0;
-  for (int k0 = 0; k0 < M; k0 += W) {
-    const int k = k0 + lane;
-    bool keep = false, touch = false;
-    uint32_t ab = 0;
-    if (k < M) {
+  for (int c = 0; c * W < M; ++c) {
+    const int k = c * W + lane;
+    uint32_t ab = 0u;
+    if (c < RCH) {
+#pragma unroll
+      for (int q = 0; q < RCH; ++q)
+        if (q == c) ab = rab[q];
+    } else if (k < M) {
       ab = cab[k];
+    }
+    bool keep = false;
+    const bool touch = (tbits >> c) & 1u;
+    if (k < M) {
       const int a = ab & 0xffffu, b = ab >> 16;
-      const float dx = s_c0x[b] - s_c0x[a], dy = s_c0y[b] - s_c0y[a];
-      touch = !(dx * dx + dy * dy > rr);
-      keep = overlap(s_fn[a], s_fn[b]);
+      keep = overlap(s_pj[a].fn, s_pj[b].fn);
     }
     const unsigned long long mt = __ballot(touch), mk = __ballot(keep);
     const int trank = Tr + __popcll(mt & lt);
@@ -615,12 +715,11 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     status |= MACM_ST_CONTACT_OVERFLOW;
     total = C;
   }
-
   STAMP(11);
+
   // ---- rewards (mvmnt.py:160-179) and obs (mvmnt.py:181-222) -------------------
   float rew = 0.0f;
   if (act) {
-    const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
     const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
     const float td2 = tdx * tdx + tdy * tdy;       // b2DistanceSquared(target, position)
     const double d = sqrt((double)td2);
@@ -630,8 +729,11 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     rew_out[ag] = rew;
     if (coll_out) coll_out[ag] = coll ? 1 : 0;
     if (nbr_out) nbr_out[ag] = bj;
-    if (obs) write_obs<OT>(P, obs + (size_t)e * N * (P.coord == MACM_COORD_CARTESIAN ? 6 : 4), lane, cx, cy, ang,
-                           best, bj, s_cx, s_cy, tdx, tdy, td2);
+    if (obs) {
+      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+      const float rx = s_cx[bj] - cx, ry = s_cy[bj] - cy;
+      write_obs<OT>(obs + ag * od, P.coord, ang, best, rx, ry, tdx, tdy, td2);
+    }
     // ---- state write-back ----
     B.pos[ag] = make_float2(cx, cy);
     B.vel[ag] = make_float2(vx, vy);
@@ -639,14 +741,14 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     B.fat[ag] = fn;
     B.sleep[ag] = ns;
   }
-
   STAMP(12);
-  // ---- per-env bookkeeping + counters -------------------------------------------
+
+  // ---- per-env bookkeeping + counters (no cross-env atomics) -------------------
   const unsigned long long mcoll = __ballot(act && coll);
   const unsigned long long mpos = __ballot(act && rew > 0.0f);
   const unsigned long long mst1 = __ballot(status & 1), mst2 = __ballot(status & 2), mst4 = __ballot(status & 4);
   if (lane == 0) {
-    const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz
+    const double tp = time_passed + P.inv_hz;  // time_passed += 1/hz
     const uint8_t dn = tp > P.time_limit ? 1 : 0;
     B.time_passed[e] = tp;
     B.done[e] = dn;
@@ -654,15 +756,16 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     B.step_count[e] = step_count + 1;
     B.ccount[nxt][e] = total;
     const int st = (mst1 ? 1 : 0) | (mst2 ? 2 : 0) | (mst4 ? 4 : 0);
-    if (st) atomicOr(&B.status[e], st);
-    atomicAdd(&B.counters[0], (unsigned long long)N);
-    atomicAdd(&B.counters[1], (unsigned long long)__popcll(mcoll));
-    atomicAdd(&B.counters[2], (unsigned long long)__popcll(mpos));
-    atomicAdd(&B.counters[3], (unsigned long long)dn);
+    if (st) B.status[e] = st_prev | st;
+    ulonglong2* ec = reinterpret_cast<ulonglong2*>(B.env_counters + (size_t)e * 4);
+    ec[0] = make_ulonglong2(ctr[0] + (unsigned long long)N, ctr[1] + (unsigned long long)__popcll(mcoll));
+    ec[1] = make_ulonglong2(ctr[2] + (unsigned long long)__popcll(mpos), ctr[3] + (unsigned long long)dn);
   }
   STAMP(13);
   STAMP_STAT(14, (unsigned long long)T | ((unsigned long long)nisl << 16) | ((unsigned long long)M << 32));
+#ifdef MACM_STAMPS
   STAMP_STAT(15, (unsigned long long)s_stat_maxisl | ((unsigned long long)total << 32));
+#endif
 }
 
 // Initial proxies (b2DynamicTree::CreateProxy: fat = tight +- 0.1), the first
@@ -677,14 +780,14 @@ __global__ __launch_bounds__(W) void flock_init_w64(StepParams P, WorldBuffers B
   const int C = P.max_contacts;
   const bool act = lane < N;
   const size_t ag = (size_t)e * N + lane;
-  __shared__ float s_cx[W], s_cy[W];
-  __shared__ float4 s_f[W];
   float2 p = make_float2(0.0f, 0.0f);
   float4 f = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   float ang = 0.0f;
+  float2 tg = make_float2(0.0f, 0.0f);
   if (act) {
     p = B.pos[ag];
     ang = B.angle[ag];
+    tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
     const float r = P.radius;
     f = make_float4((p.x - r) - kAabbExtension, (p.y - r) - kAabbExtension, (p.x + r) + kAabbExtension,
                     (p.y + r) + kAabbExtension);
@@ -692,30 +795,32 @@ __global__ __launch_bounds__(W) void flock_init_w64(StepParams P, WorldBuffers B
     B.vel[ag] = make_float2(0.0f, 0.0f);
     B.sleep[ag] = 0.0f;
   }
-  s_cx[lane] = p.x;
-  s_cy[lane] = p.y;
-  s_f[lane] = f;
-  __syncthreads();
   unsigned long long m = 0ull;
-  if (act)
-    for (int j = lane + 1; j < N; ++j)
-      if (overlap(f, s_f[j])) m |= 1ull << j;
-  int total = write_new_pairs(lane, m, B.cab[cur] + (size_t)e * C, B.cimp[cur] + (size_t)e * C, C);
+  float best = __builtin_inff();
+  int bj = lane == 0 ? 1 : 0;
+  for (int j = 0; j < N; ++j) {
+    const float4 fj = make_float4(bcast(f.x, j), bcast(f.y, j), bcast(f.z, j), bcast(f.w, j));
+    const float dx = bcast(p.x, j) - p.x, dy = bcast(p.y, j) - p.y;
+    const float d2 = dx * dx + dy * dy;
+    if (j > lane && overlap(f, fj)) m |= 1ull << j;
+    if (j != lane && d2 < best) {
+      best = d2;
+      bj = j;
+    }
+  }
+  int total = write_new_pairs(lane, act ? m : 0ull, B.cab[cur] + (size_t)e * C, B.cimp[cur] + (size_t)e * C, C);
   int st = 0;
   if (total > C) {
     st = MACM_ST_CONTACT_OVERFLOW;
     total = C;
   }
-  if (act && (obs || nbr_out)) {
-    float best;
-    int bj;
-    nearest(N, lane, p.x, p.y, s_cx, s_cy, best, bj);
+  const float bx = __shfl(p.x, bj, W), by = __shfl(p.y, bj, W);
+  if (act) {
     if (nbr_out) nbr_out[ag] = bj;
     if (obs) {
-      const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
       const float tdx = tg.x - p.x, tdy = tg.y - p.y;
-      write_obs<OT>(P, obs + (size_t)e * N * (P.coord == MACM_COORD_CARTESIAN ? 6 : 4), lane, p.x, p.y, ang, best,
-                    bj, s_cx, s_cy, tdx, tdy, tdx * tdx + tdy * tdy);
+      write_obs<OT>(obs + ag * od, P.coord, ang, best, bx - p.x, by - p.y, tdx, tdy, tdx * tdx + tdy * tdy);
     }
   }
   if (lane == 0) {
@@ -736,22 +841,30 @@ __global__ __launch_bounds__(W) void flock_observe_w64(StepParams P, WorldBuffer
   const int N = P.n_agents;
   const bool act = lane < N;
   const size_t ag = (size_t)e * N + lane;
-  __shared__ float s_cx[W], s_cy[W];
-  float2 p = make_float2(0.0f, 0.0f);
-  if (act) p = B.pos[ag];
-  s_cx[lane] = p.x;
-  s_cy[lane] = p.y;
-  __syncthreads();
+  float2 p = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
+  float ang = 0.0f;
+  if (act) {
+    p = B.pos[ag];
+    ang = B.angle[ag];
+    tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+  }
+  float best = __builtin_inff();
+  int bj = lane == 0 ? 1 : 0;
+  for (int j = 0; j < N; ++j) {
+    const float dx = bcast(p.x, j) - p.x, dy = bcast(p.y, j) - p.y;
+    const float d2 = dx * dx + dy * dy;
+    if (j != lane && d2 < best) {
+      best = d2;
+      bj = j;
+    }
+  }
+  const float bx = __shfl(p.x, bj, W), by = __shfl(p.y, bj, W);
   if (!act) return;
-  float best;
-  int bj;
-  nearest(N, lane, p.x, p.y, s_cx, s_cy, best, bj);
   if (nbr_out) nbr_out[ag] = bj;
   if (obs) {
-    const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+    const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
     const float tdx = tg.x - p.x, tdy = tg.y - p.y;
-    write_obs<OT>(P, obs + (size_t)e * N * (P.coord == MACM_COORD_CARTESIAN ? 6 : 4), lane, p.x, p.y,
-                  B.angle[ag], best, bj, s_cx, s_cy, tdx, tdy, tdx * tdx + tdy * tdy);
+    write_obs<OT>(obs + ag * od, P.coord, ang, best, bx - p.x, by - p.y, tdx, tdy, tdx * tdx + tdy * tdy);
   }
 }
 

@@ -201,7 +201,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       (rc = dalloc(w, &B.cimp[0], (size_t)n_envs * C)) || (rc = dalloc(w, &B.cimp[1], (size_t)n_envs * C)) ||
       (rc = dalloc(w, &B.step_count, (size_t)n_envs)) || (rc = dalloc(w, &B.time_passed, (size_t)n_envs)) ||
       (rc = dalloc(w, &B.done, (size_t)n_envs)) || (rc = dalloc(w, &B.status, (size_t)n_envs)) ||
-      (rc = dalloc(w, &B.counters, 4))
+      (rc = dalloc(w, &B.env_counters, (size_t)n_envs * 4))
 #ifdef MACM_STAMPS
       || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 16))
 #endif
@@ -211,7 +211,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
     return rc;
   }
   hipError_t e = hipMemcpy(B.tidx, tidx.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemset(B.counters, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(B.env_counters, 0, (size_t)n_envs * 4 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
   if (e != hipSuccess) {
@@ -375,18 +375,22 @@ int macm_world_status(macm_world* w, int32_t* status_or, void* stream) {
 int macm_world_counters(macm_world* w, int64_t out[4], void* stream) {
   if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
   DeviceGuard g(w->device);
-  unsigned long long h[4];
+  std::vector<unsigned long long> h((size_t)w->P.n_envs * 4);
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemcpyAsync(h, w->B.counters, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(h.data(), w->B.env_counters, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         s));
   HIP_TRY(hipStreamSynchronize(s));
-  for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+  unsigned long long acc[4] = {0, 0, 0, 0};
+  for (size_t i = 0; i < h.size(); ++i) acc[i & 3] += h[i];
+  for (int i = 0; i < 4; ++i) out[i] = (int64_t)acc[i];
   return MACM_OK;
 }
 
 int macm_world_reset_counters(macm_world* w, void* stream) {
   if (!w) return fail(MACM_E_INVALID, "NULL argument");
   DeviceGuard g(w->device);
-  HIP_TRY(hipMemsetAsync(w->B.counters, 0, 4 * sizeof(unsigned long long), (hipStream_t)stream));
+  HIP_TRY(hipMemsetAsync(w->B.env_counters, 0, (size_t)w->P.n_envs * 4 * sizeof(unsigned long long),
+                         (hipStream_t)stream));
   return MACM_OK;
 }
 
