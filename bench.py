@@ -87,8 +87,8 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_flock_step.json"))
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -98,10 +98,11 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    from gym_macm import dist as gdist
     from gym_macm.vec import FlockVec
 
     E, N, K, W = args.envs, args.agents, args.steps, args.warmup
-    vec = FlockVec(E, n_agents=[N], seed=args.seed, env_offset=rank * E, device=dev)
+    vec = FlockVec(E, n_agents=[N], seed=args.seed, env_offset=gdist.env_offset(rank, E), device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 1 + rank)
     acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
@@ -130,17 +131,10 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / K  # per launch, on the launch stream
-    status = vec.status()
-    cnt = torch.tensor(vec.counters(), dtype=torch.int64, device=dev)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        st = torch.tensor([status], dtype=torch.int32, device=dev)
-        dist.all_reduce(st, op=dist.ReduceOp.MAX)
-        status = int(st.item())
-    elapsed = float(el.item())
-    cnt = cnt.cpu().numpy()
+    # one small RCCL all-reduce of counters after the timed region (no data-path collective)
+    status = int(gdist.reduce_counters([vec.status()], device=dev, op="max")[0])
+    cnt = gdist.reduce_counters(vec.counters(), device=dev)
+    elapsed = gdist.reduce_max(elapsed, device=dev)
     total_agent_steps = world * E * N * K
     assert int(cnt[0]) == total_agent_steps, (cnt, total_agent_steps)
     if status != 0:

@@ -656,15 +656,19 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     for (int u = 0; u < 4; ++u) {
       const int j = j0 + u;
       const float4 fj = q[u].fn;
-      // b2TestOverlap(fn, fj): (fj.lo - fn.hi > 0) == (fj.lo > fn.hi) for IEEE floats
-      const bool sep = (fj.x > fn.z) | (fj.y > fn.w) | (fn.x > fj.z) | (fn.y > fj.w);
-      const unsigned long long row = __ballot(!sep) & valid;
-      myov = (lane == j) ? row : myov;
+      // b2TestOverlap(fn, fj) separates iff one of (fj.lo - fn.hi, fn.lo - fj.hi) > 0;
+      // for finite AABBs (and the +-inf dummies) that is max(...) > 0, all on VALU
+      const float sepv = fmaxf(fmaxf(fj.x - fn.z, fj.y - fn.w), fmaxf(fn.x - fj.z, fn.y - fj.w));
+      const unsigned long long row = __ballot(!(sepv > 0.0f)) & valid;
+      const bool self = lane == j;
+      myov = self ? row : myov;
       const float dx = q[u].c.x - cx, dy = q[u].c.y - cy;  // other.position - agent.position
       const float d2 = dx * dx + dy * dy;                 // b2DistanceSquared(other, agent)
-      const bool better = (j != lane) & (d2 < best);      // strict '<': lowest index wins (mvmnt.py:194)
-      best = better ? d2 : best;
-      bj = better ? j : bj;
+      const float d2o = self ? __builtin_inff() : d2;
+      if (d2o < best) {  // strict '<': lowest index wins ties (mvmnt.py:194)
+        best = d2o;
+        bj = j;
+      }
     }
   }
   myov &= ~(1ull << lane);

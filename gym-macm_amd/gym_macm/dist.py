@@ -1,0 +1,58 @@
+"""Env-sharded multi-GPU helpers (one process per GPU, torch.distributed).
+
+The reference has no parallelism at all (one Box2D world per env, single thread;
+SURVEY.md §2). Its envs are fully independent, so the MI355X layout is weak
+scaling with no data-path collective: rank r owns the contiguous global env ids
+[r*E, (r+1)*E), and because every env is seeded by its GLOBAL id (env e ==
+Flock after random.seed(seed + e)) its trajectory is identical whatever the
+number of ranks. The only collective is one small all-reduce of counters after
+a measurement window (RCCL over xGMI when backend="nccl", gloo in CPU tests).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def rank_info():
+    """(rank, world_size, local_rank) from the torchrun environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def env_offset(rank: int, envs_per_rank: int) -> int:
+    """First global env id of `rank` under weak scaling."""
+    return rank * envs_per_rank
+
+
+def shard_slice(rank: int, envs_per_rank: int) -> slice:
+    o = env_offset(rank, envs_per_rank)
+    return slice(o, o + envs_per_rank)
+
+
+def reduce_counters(counters, device=None, op="sum"):
+    """All-reduce an int64 counter vector across ranks (no-op without a process group)."""
+    t = torch.as_tensor(np.asarray(counters, np.int64), dtype=torch.int64)
+    if device is not None:
+        t = t.to(device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+    return t.cpu().numpy()
+
+
+def reduce_max(value: float, device=None) -> float:
+    """Max over ranks (the job's wall time is its slowest rank's)."""
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def step_counters(reward: np.ndarray, collided: np.ndarray, done: np.ndarray) -> np.ndarray:
+    """Host-side counters of one step with the device counters' meaning
+    (macm_world_counters): agent-steps, collided agent-steps, positive-reward
+    agent-steps, env-steps with done set."""
+    return np.array([reward.size, int(collided.sum()), int((reward > 0).sum()), int(done.sum())], np.int64)

@@ -1,0 +1,61 @@
+"""Summarise rocprofv3 PMC passes (tools/pmc.sh) for the step kernel into a JSON
+that bench.py reads for `roofline.traffic`.
+
+    python tools/pmc_summary.py gpurun_out/<dir> --envs 4096 --agents 64 -o profiles/pmc_flock_step.json
+
+HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE
+and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced read, so reads are doubled; WRITE_SIZE is taken as is. The step kernel's
+accesses are 1-16 B per lane (uncalibrated widths per the guide), so the figure
+is reported together with both raw counters.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+
+
+def kernel_means(path, kernel):
+    agg = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", default="flock_step_w64<float>")
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--agents", type=int, default=64)
+    ap.add_argument("-o", "--out", default="")
+    a = ap.parse_args()
+    res = {}
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
+        p = os.path.join(a.dir, sub, "run_counter_collection.csv")
+        if os.path.exists(p):
+            res.update(kernel_means(p, a.kernel))
+    fetch_b = res["FETCH_SIZE"] * 1024.0
+    write_b = res["WRITE_SIZE"] * 1024.0
+    agents = a.envs * a.agents
+    out = {
+        "kernel": a.kernel, "envs": a.envs, "agents": a.agents,
+        "fetch_size_kib": res["FETCH_SIZE"], "write_size_kib": res["WRITE_SIZE"],
+        "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
+        "hbm_bytes_per_agent_step": (2.0 * fetch_b + write_b) / agents,
+        "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE",
+        "per_wave": {k: v / res.get("SQ_WAVES", 1.0) for k, v in res.items() if k.startswith("SQ_")},
+        "source": a.dir,
+    }
+    s = json.dumps(out, indent=1)
+    print(s)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
