@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=64)
+    ap.add_argument("--flocks", type=int, default=1, help="targets = i // (agents / flocks) (config 3: 4)")
     ap.add_argument("--seed", type=int, default=0x6D61636D)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
@@ -102,7 +103,9 @@ def main():
     from gym_macm.vec import FlockVec
 
     E, N, K, W = args.envs, args.agents, args.steps, args.warmup
-    vec = FlockVec(E, n_agents=[N], seed=args.seed, env_offset=gdist.env_offset(rank, E), device=dev)
+    targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
+    vec = FlockVec(E, n_agents=[N], targets=targets, seed=args.seed, env_offset=gdist.env_offset(rank, E),
+                   device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 1 + rank)
     acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
@@ -143,9 +146,10 @@ def main():
 
     if rank == 0:
         achieved_gbs = B_ALG * E * N / (kernel_ms * 1e-3) / 1e9
+        kname = "flock_step_w64<float>" if N <= 64 else "flock_step_wg<float>"
         traffic = None
         tj = load_traffic(args.traffic_json)
-        if tj and tj.get("envs") == E and tj.get("agents") == N:
+        if tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname:
             traffic = tj.get("hbm_bytes_per_launch")
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
@@ -163,7 +167,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"cm-flock-v0 n_agents=[{N}] x {E} envs per GPU, uniform random discrete actions "
+                "workload": f"cm-flock-v0 n_agents=[{N}]{f' targets=i//{N // args.flocks}' if args.flocks > 1 else ''} "
+                            f"x {E} envs per GPU, uniform random discrete actions "
                             f"(MultiDiscrete[3,3,3]) pre-generated on device, from reset (seed {args.seed:#x})",
                 "envs_per_gpu": E, "n_agents": N, "total_envs": E * world,
                 "parallelism": f"env-sharded x{world} (no data-path collective)",
@@ -171,7 +176,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "flock_step_w64<float>", "kernel_ms": kernel_ms,
+                "kernel": kname, "kernel_ms": kernel_ms,
                 "bytes_alg_per_launch": B_ALG * E * N,
             },
             "counters": {"agent_steps": int(cnt[0]), "collided_agent_steps": int(cnt[1]),

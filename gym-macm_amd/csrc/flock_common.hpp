@@ -64,6 +64,7 @@ struct WorldBuffers {
   int32_t* status;     // [E]      MACM_ST_* bits
   unsigned long long* env_counters;  // [E, 4] per-env accumulators (see macm_world_counters)
   unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
+  float2* scratch;               // [E, tcap] list-order impulses (workgroup kernel only)
 };
 
 }  // namespace macm

@@ -21,6 +21,16 @@ hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, 
                            int32_t* nbr, hipStream_t s);
 hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
                               hipStream_t s);
+hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
+                          void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
+                          hipStream_t s);
+hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr,
+                          hipStream_t s);
+hipError_t launch_observe_wg(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
+                             hipStream_t s);
+hipError_t wg_configure(int N, int tcap);
+int wg_block(int N);
+int wg_lds_bytes(int N, int tcap);
 }  // namespace macm
 
 using namespace macm;
@@ -31,6 +41,8 @@ struct macm_world {
   WorldBuffers B;
   int cur;  // which contact-list buffer holds the current ordered list
   int device;
+  bool wave;  // N <= 64: one wavefront per env (flock_step_w64); else one workgroup per env
+  int tcap;   // touching-contact capacity per env
   std::vector<int32_t> tidx;
   std::vector<void*> allocs;
 };
@@ -79,11 +91,20 @@ void free_world(macm_world* w) {
   w->allocs.clear();
 }
 
+hipError_t launch_init(macm_world* w, const macm_outputs* out, hipStream_t s) {
+  void* obs = out ? out->obs : nullptr;
+  int32_t* nbr = out ? out->nbr_id : nullptr;
+  if (w->wave) return launch_init_w64(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, s);
+  return launch_init_wg(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, s);
+}
+
 }  // namespace
 
 extern "C" {
 
-const char* macm_version(void) { return "macm-hip 0.1.0 (gfx950; Flock N<=64 wave-per-env kernel)"; }
+const char* macm_version(void) {
+  return "macm-hip 0.2.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernel N<=1024)";
+}
 int macm_abi_version(void) { return MACM_ABI_VERSION; }
 const char* macm_last_error(void) { return g_last_error.c_str(); }
 
@@ -123,8 +144,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   const macm_config& c = *cfg;
   if (n_envs <= 0) return fail(MACM_E_INVALID, "n_envs must be > 0");
   if (c.n_agents < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2 (get_obs needs another agent)");
-  if (c.n_agents > 64)
-    return fail(MACM_E_UNSUPPORTED, "n_agents > 64 needs the multi-wave kernel (not built in this version)");
+  if (c.n_agents > 1024)
+    return fail(MACM_E_UNSUPPORTED, "n_agents > 1024 is not built (one workgroup per env, <= 1024 threads)");
   if (c.n_targets < 1) return fail(MACM_E_INVALID, "n_targets must be >= 1");
   if (!(c.hz > 0.0)) return fail(MACM_E_INVALID, "hz must be > 0");
   if (c.velocity_iterations < 0 || c.position_iterations < 0) return fail(MACM_E_INVALID, "iterations < 0");
@@ -142,7 +163,10 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       tidx[i] = targets_idx[i];
     }
   const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
-  int C = max_contacts > 0 ? max_contacts : (int)all_pairs;
+  // N <= 64: room for every pair (never overflows). Larger N: 32 list entries per
+  // agent by default (fat-AABB pairs; ~7.3 per agent even in C5's dense start).
+  const int64_t dflt = N <= 64 ? all_pairs : (all_pairs < 32LL * N ? all_pairs : 32LL * N);
+  int C = max_contacts > 0 ? max_contacts : (int)dflt;
   if (C > all_pairs) C = (int)all_pairs;
 
   int ndev = 0;
@@ -155,6 +179,12 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   w->device = device;
   w->cur = 0;
   w->tidx = tidx;
+  w->wave = N <= 64;
+  {
+    const int bs = N <= 64 ? 64 : wg_block(N);
+    const int want = N <= 64 ? 256 : 5 * bs;  // register staging holds 5 records per thread
+    w->tcap = want < 4608 ? want : 4608;
+  }
   StepParams& P = w->P;
   P.n_envs = n_envs;
   P.n_agents = N;
@@ -205,6 +235,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
 #ifdef MACM_STAMPS
       || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 16))
 #endif
+      || (!w->wave && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap)))
   ) {
     free_world(w);
     delete w;
@@ -214,6 +245,16 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   if (e == hipSuccess) e = hipMemset(B.env_counters, 0, (size_t)n_envs * 4 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
+  if (e == hipSuccess && !w->wave) {
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e == hipSuccess && (size_t)wg_lds_bytes(N, w->tcap) > prop.sharedMemPerBlock) {
+      free_world(w);
+      delete w;
+      return fail(MACM_E_UNSUPPORTED, "per-env LDS layout exceeds the device's LDS per workgroup");
+    }
+    if (e == hipSuccess) e = wg_configure(N, w->tcap);
+  }
   if (e != hipSuccess) {
     free_world(w);
     delete w;
@@ -239,7 +280,7 @@ int macm_world_info_get(const macm_world* w, macm_world_info* info) {
   info->n_targets = w->P.n_targets;
   info->obs_dim = obs_dim(w->cfg);
   info->max_contacts = w->P.max_contacts;
-  info->max_touching = 256;
+  info->max_touching = w->tcap;
   info->device = w->device;
   info->_pad = 0;
   return MACM_OK;
@@ -272,8 +313,7 @@ int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const mac
   HIP_TRY(hipMemcpyAsync(w->B.angle, ang.data(), ang.size() * sizeof(float), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w->B.targets, tg.data(), tg.size() * sizeof(float2), hipMemcpyHostToDevice, s));
   w->cur = 0;
-  HIP_TRY(launch_init_w64(w->P, w->B, w->cur, out ? out->obs : nullptr, c.obs_f64 != 0,
-                          out ? out->nbr_id : nullptr, s));
+  HIP_TRY(launch_init(w, out, s));
   // host vectors are read by the async copies: wait before they go out of scope
   HIP_TRY(hipStreamSynchronize(s));
   return MACM_OK;
@@ -289,8 +329,7 @@ int macm_world_place(macm_world* w, const void* pos, const void* angle, const vo
   HIP_TRY(hipMemcpyAsync(w->B.angle, angle, EN * sizeof(float), hipMemcpyDefault, s));
   HIP_TRY(hipMemcpyAsync(w->B.targets, targets, ET * sizeof(float2), hipMemcpyDefault, s));
   w->cur = 0;
-  HIP_TRY(launch_init_w64(w->P, w->B, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
-                          out ? out->nbr_id : nullptr, s));
+  HIP_TRY(launch_init(w, out, s));
   HIP_TRY(hipStreamSynchronize(s));
   return MACM_OK;
 }
@@ -298,8 +337,12 @@ int macm_world_place(macm_world* w, const void* pos, const void* angle, const vo
 int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream) {
   if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
   DeviceGuard g(w->device);
-  HIP_TRY(launch_step_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
-                          out->collided, out->done, (hipStream_t)stream));
+  if (w->wave)
+    HIP_TRY(launch_step_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
+                            out->collided, out->done, (hipStream_t)stream));
+  else
+    HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
+                           out->reward, out->collided, out->done, (hipStream_t)stream));
   w->cur ^= 1;
   return MACM_OK;
 }
@@ -307,7 +350,10 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
   if (!w || !out) return fail(MACM_E_INVALID, "world/out is NULL");
   DeviceGuard g(w->device);
-  HIP_TRY(launch_observe_w64(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
+  if (w->wave)
+    HIP_TRY(launch_observe_w64(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
+  else
+    HIP_TRY(launch_observe_wg(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
   return MACM_OK;
 }
 

@@ -56,7 +56,7 @@ def test_invalid_config_is_rejected_with_message():
     h = ctypes.c_void_p()
     rc = L.macm_world_create(ctypes.byref(c), None, 4, 0, 0, ctypes.byref(h))
     assert rc == -1 and b"n_agents" in L.macm_last_error()
-    c.n_agents = 65
+    c.n_agents = 1025
     assert L.macm_world_create(ctypes.byref(c), None, 4, 0, 0, ctypes.byref(h)) == -4
 
 

@@ -191,3 +191,27 @@ def test_dropin_flock_matches_reference_goldens(name):
     s = env.world.get_state()
     np.testing.assert_array_equal(s["pos"][0], g["pos"][-1])
     np.testing.assert_array_equal(s["angle"][0], g["angle"][-1])
+
+
+# ---- workgroup-per-env kernel (64 < N <= 1024) ---------------------------------------
+
+
+@pytest.mark.parametrize("n", [65, 100, 128])
+def test_workgroup_kernel_sizes(n):
+    vec, orc = make_pair(6, [n], seed=n, start_spread=12)
+    check_rollout(vec, orc, 50, np.random.default_rng(n), state_every=10)
+
+
+def test_c3_multiflock_256_agents_4_targets():
+    """BASELINE config 3: n_agents=256, targets = i // 64 (4 flocks, README.md:44)."""
+    tg = [i // 64 for i in range(256)]
+    vec, orc = make_pair(4, [256], seed=33, targets=tg)
+    assert vec.n_targets == 4
+    check_rollout(vec, orc, 40, np.random.default_rng(3), state_every=10)
+
+
+def test_c5_dense_1024_agents():
+    """BASELINE config 5 shape: 1024 agents in the default 20 m spread (804 m^2 of
+    circles in 400 m^2): one giant island, thousands of touching contacts."""
+    vec, orc = make_pair(2, [1024], seed=55)
+    check_rollout(vec, orc, 6, np.random.default_rng(5), state_every=2)
