@@ -66,6 +66,45 @@ def cpu_baseline(n_agents, seed, budget_s=15.0):
                        f"{dt:.1f} s")
 
 
+def b_alg_tdm(n_agents):
+    """Algorithmic bytes per TDM agent-step (float32 obs): state r+w 2 x 40 (as Flock),
+    action 4, health/cd_atk/cd_mov f64 + alive u8 r+w 2 x 25, obs (N-1) x 16, mask N-1,
+    health/alive outputs 9."""
+    return 80 + 4 + 50 + (n_agents - 1) * 16 + (n_agents - 1) + 9
+
+
+def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0):
+    """Time the CPU TDM oracle (oracle/tdm_oracle.c, OpenMP over envs) on a bounded sample."""
+    from oracle import OracleTDM
+    from gym_macm.tdm_world import tdm_config
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    E = max(4 * threads, 64)
+    N = sum(team_sizes)
+    orc = OracleTDM(tdm_config(team_sizes, obs_f64=True), E, seed)
+    rng = np.random.default_rng(seed + 1)
+    acts = [tdm_random_actions_np(rng, E, N) for _ in range(16)]
+    t0 = time.perf_counter()
+    for a in acts[:3]:
+        orc.step(a, threads)
+    per_step = (time.perf_counter() - t0) / 3
+    steps = int(max(10, min(3000, budget_s / max(per_step, 1e-6))))
+    t0 = time.perf_counter()
+    for s in range(steps):
+        orc.step(acts[s % 16], threads)
+    dt = time.perf_counter() - t0
+    return dict(value=E * N * steps / dt, unit="agent·steps/s", cores=threads, kind="port",
+                sample=f"oracle/ C restatement of TDM, {E} envs x {N} agents x {steps} steps (after 3 warm-up "
+                       f"steps) from reset, uniform random actions (attack p=0.5), OpenMP {threads} threads, "
+                       f"{dt:.1f} s")
+
+
+def tdm_random_actions_np(rng, E, N):
+    a = rng.integers(0, 3, size=(E, N, 4)).astype(np.uint8)
+    a[..., 3] = rng.integers(0, 2, size=(E, N))
+    return a
+
+
 def load_traffic(path):
     if not path or not os.path.exists(path):
         return None
@@ -85,8 +124,14 @@ def main():
     ap.add_argument("--seed", type=int, default=0x6D61636D)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_flock_step.json"))
+    ap.add_argument("--env", choices=("flock", "tdm"), default="flock",
+                    help="flock: cm-flock-v0 (the metric); tdm: cm-tdm-v0 (config 4, --teams)")
+    ap.add_argument("--teams", default="16,16", help="TDM team sizes (config 4: 16,16)")
+    ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(REPO, "profiles", "pmc_flock_step.json" if args.env == "flock"
+                                         else "pmc_tdm_step.json")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,25 +145,38 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from gym_macm import dist as gdist
-    from gym_macm.vec import FlockVec
 
-    E, N, K, W = args.envs, args.agents, args.steps, args.warmup
-    targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
-    vec = FlockVec(E, n_agents=[N], targets=targets, seed=args.seed, env_offset=gdist.env_offset(rank, E),
-                   device=dev)
+    E, K, W = args.envs, args.steps, args.warmup
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 1 + rank)
-    acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
+    if args.env == "flock":
+        from gym_macm.vec import FlockVec
+        N = args.agents
+        targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
+        vec = FlockVec(E, n_agents=[N], targets=targets, seed=args.seed, env_offset=gdist.env_offset(rank, E),
+                       device=dev)
+        world_h = vec.world
+        acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
+        stride = E * N * 3
+    else:
+        from gym_macm.tdm_world import TdmWorld, tdm_config
+        teams = [int(x) for x in args.teams.split(",")]
+        N = sum(teams)
+        world_h = TdmWorld(tdm_config(teams), E, device=dev)
+        world_h.reset(args.seed, gdist.env_offset(rank, E))
+        acts = torch.randint(0, 3, (W + K, E, N, 4), dtype=torch.uint8, device=dev, generator=gen)
+        acts[..., 3] = torch.randint(0, 2, (W + K, E, N), dtype=torch.uint8, device=dev, generator=gen)
+        stride = E * N * 4
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    step = vec.world.step_raw
+    step = world_h.step_raw
     base = acts.data_ptr()
-    stride = E * N * 3
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}")
     for w in range(W):
         step(base + w * stride, sh)
     torch.cuda.synchronize(dev)
-    vec.world.reset_counters()
+    if args.env == "flock":
+        world_h.reset_counters()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -135,24 +193,38 @@ def main():
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / K  # per launch, on the launch stream
     # one small RCCL all-reduce of counters after the timed region (no data-path collective)
-    status = int(gdist.reduce_counters([vec.status()], device=dev, op="max")[0])
-    cnt = gdist.reduce_counters(vec.counters(), device=dev)
+    status = int(gdist.reduce_counters([world_h.status()], device=dev, op="max")[0])
+    cnt = gdist.reduce_counters(world_h.counters(), device=dev)
     elapsed = gdist.reduce_max(elapsed, device=dev)
     total_agent_steps = world * E * N * K
-    assert int(cnt[0]) == total_agent_steps, (cnt, total_agent_steps)
+    if args.env == "flock":
+        assert int(cnt[0]) == total_agent_steps, (cnt, total_agent_steps)
     if status != 0:
         raise RuntimeError(f"device status bits {status}: a capacity overflowed, results invalid")
     value = total_agent_steps / elapsed
 
     if rank == 0:
-        achieved_gbs = B_ALG * E * N / (kernel_ms * 1e-3) / 1e9
-        kname = "flock_step_w64<float>" if N <= 64 else "flock_step_wg<float>"
+        b_alg = B_ALG if args.env == "flock" else b_alg_tdm(N)
+        achieved_gbs = b_alg * E * N / (kernel_ms * 1e-3) / 1e9
+        if args.env == "tdm":
+            kname = "env_step_w64<1, float>"
+        else:
+            kname = "env_step_w64<0, float>" if N <= 64 else "flock_step_wg<float>"
         traffic = None
         tj = load_traffic(args.traffic_json)
         if tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname:
             traffic = tj.get("hbm_bytes_per_launch")
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
+        if args.env == "tdm":
+            metric = "agent·steps/sec, cm-tdm-v0 (config 4)"
+            workload = (f"cm-tdm-v0 n_agents={teams} x {E} envs per GPU, uniform random actions "
+                        f"(MultiDiscrete[3,3,3,2]) pre-generated on device, from reset (seed {args.seed:#x}); "
+                        f"agent-steps count every agent slot")
+        else:
+            workload = (f"cm-flock-v0 n_agents=[{N}]{f' targets=i//{N // args.flocks}' if args.flocks > 1 else ''} "
+                        f"x {E} envs per GPU, uniform random discrete actions "
+                        f"(MultiDiscrete[3,3,3]) pre-generated on device, from reset (seed {args.seed:#x})")
         out = {
             "metric": metric,
             "value": value,
@@ -167,9 +239,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"cm-flock-v0 n_agents=[{N}]{f' targets=i//{N // args.flocks}' if args.flocks > 1 else ''} "
-                            f"x {E} envs per GPU, uniform random discrete actions "
-                            f"(MultiDiscrete[3,3,3]) pre-generated on device, from reset (seed {args.seed:#x})",
+                "workload": workload,
                 "envs_per_gpu": E, "n_agents": N, "total_envs": E * world,
                 "parallelism": f"env-sharded x{world} (no data-path collective)",
             },
@@ -177,14 +247,21 @@ def main():
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": kname, "kernel_ms": kernel_ms,
-                "bytes_alg_per_launch": B_ALG * E * N,
+                "bytes_alg_per_launch": b_alg * E * N,
             },
-            "counters": {"agent_steps": int(cnt[0]), "collided_agent_steps": int(cnt[1]),
-                         "positive_reward_agent_steps": int(cnt[2]), "done_env_steps": int(cnt[3])},
         }
+        if args.env == "flock":
+            out["counters"] = {"agent_steps": int(cnt[0]), "collided_agent_steps": int(cnt[1]),
+                               "positive_reward_agent_steps": int(cnt[2]), "done_env_steps": int(cnt[3])}
+        else:
+            out["counters"] = {"alive_agent_steps": int(cnt[0]), "melee_attacks": int(cnt[1]),
+                               "deaths": int(cnt[2]), "done_env_steps": int(cnt[3])}
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
-            out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget)
+            if args.env == "flock":
+                out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget)
+            else:
+                out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

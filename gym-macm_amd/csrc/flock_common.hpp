@@ -28,7 +28,7 @@ constexpr float kPi32 = 3.14159265359f;  // b2_pi
 // Per-launch parameters derived on the host from macm_config exactly as the
 // reference derives them (Python double arithmetic / SWIG float conversion).
 struct StepParams {
-  int32_t n_envs, n_agents, n_targets, max_contacts;
+  int32_t n_envs, n_agents, n_targets, max_contacts;  // TDM: n_targets = 0
   int32_t vel_iters, pos_iters, warm_starting;
   int32_t action_mode, reward_mode, coord;
   float dt;          // fl32(1.0 / hz)                       cm_framework.py:182-185 -> world.Step
@@ -66,5 +66,43 @@ struct WorldBuffers {
   unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
   float2* scratch;               // [E, tcap] list-order impulses (workgroup kernel only)
 };
+
+// Env modes of the wave-per-env kernel: same physics, different env layer.
+enum EnvMode : int { kFlock = 0, kTdm = 1 };
+
+// TDM env constants (gym_macm/envs/combat.py:13-49, combatSettings settings.py:149-177).
+struct TdmParams {
+  int32_t n_teams;
+  int32_t team_end[4];          // agent i is in team t iff team_end[t-1] <= i < team_end[t]
+  int32_t fresh_raycast;        // 0: the reference's shared, never-reset listener (literal)
+  int32_t decay_mov_penalty;    // 0: cooldown_mov_penalty never decrements (literal)
+  int32_t _pad;
+  double melee_range;           // 2
+  double melee_dmg;             // 0.25
+  double cooldown_atk;          // 1
+  double cooldown_mov_penalty;  // 0.5
+  double percent_mov_penalty;   // 0.2
+  double init_health;           // 1
+};
+
+struct TdmBuffers {
+  double* health;        // [E, N]
+  double* cd_atk;        // [E, N]
+  double* cd_mov;        // [E, N]
+  uint8_t* alive;        // [E, N]
+  int2* listener;        // [E]  (RayCastClosestCallback.hit, body of .fixture or -1)
+  int32_t* winner;       // [E]  -1 = none
+  // optional per-step outputs (NULL = not wanted)
+  uint8_t* mask_out;     // [E, N, N-1]
+  double* health_out;    // [E, N]
+  uint8_t* alive_out;    // [E, N]
+  int32_t* winner_out;   // [E]
+};
+
+__host__ __device__ inline int tdm_team_of(const TdmParams& T, int i) {
+  int t = 0;
+  while (t < T.n_teams - 1 && i >= T.team_end[t]) ++t;
+  return t;
+}
 
 }  // namespace macm

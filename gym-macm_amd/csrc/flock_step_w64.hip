@@ -1,4 +1,4 @@
-// flock_step_w64.hip — batched Flock env.step for N <= 64 agents per env on gfx950.
+// flock_step_w64.hip — batched Flock / TDM env.step for N <= 64 agents per env on gfx950.
 //
 // One 64-lane wavefront advances one env; lane i owns agent i. Per-env state is
 // staged in registers + LDS (< 10 KB, so 16 envs fit a CU and a 4096-env step is
@@ -147,6 +147,48 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
   write_obs_row(o, coord, sqrt((double)best), t0, sqrt((double)td2), t1);
 }
 
+template <typename OT>
+__device__ __forceinline__ void store4(OT* o, double a, double b, double c, double d) {
+  if constexpr (sizeof(OT) == 4) {
+    *reinterpret_cast<float4*>(o) = make_float4((float)a, (float)b, (float)c, (float)d);
+  } else {
+    reinterpret_cast<double2*>(o)[0] = make_double2(a, b);
+    reinterpret_cast<double2*>(o)[1] = make_double2(c, d);
+  }
+}
+
+// TDM.get_obs (combat.py:206-227) as fixed slots: slot k of agent i is the other
+// agent j = k < i ? k : k + 1, holding (r, t, p, is_ally) with rel = other - agent
+// (float32), r = sqrt(b2DistanceSquared), t = atan2(rel) - angle_i and
+// p = angle_j - angle_i each wrapped once; mask = both alive, masked slots zero.
+// Lane k writes slot k of row i, so each row is one contiguous store.
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_rows(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
+                                             unsigned long long livem, const TdmParams& TP, const float* sx,
+                                             const float* sy, const float* sa) {
+  for (int i = 0; i < N; ++i) {
+    const float xi = sx[i], yi = sy[i], ai = sa[i];
+    const bool li = (livem >> i) & 1ull;
+    const int ti = tdm_team_of(TP, i);
+    if (lane < N - 1) {
+      const int j = lane < i ? lane : lane + 1;
+      const bool m = li && ((livem >> j) & 1ull);
+      double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
+      if (m) {
+        const float rx = sx[j] - xi, ry = sy[j] - yi;  // other.position - agent.position
+        const float d2 = rx * rx + ry * ry;           // b2DistanceSquared(other, agent)
+        r = sqrt((double)d2);
+        t = wrap_pi(atan2((double)ry, (double)rx) - (double)ai);
+        p = wrap_pi((double)sa[j] - (double)ai);
+        ty = tdm_team_of(TP, j) == ti ? 1.0 : 0.0;
+      }
+      const size_t slot = (size_t)i * (N - 1) + lane;
+      if (obs) store4<OT>(obs + slot * 4, r, t, p, ty);
+      if (mask) mask[slot] = m ? 1 : 0;
+    }
+  }
+}
+
 // New-pair compaction in descending (a, b) order: lane a owns the bitmask of
 // partners b > a. Returns the total count; writes at most C entries.
 __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newmask, uint32_t* ocab,
@@ -172,18 +214,24 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
   return total;
 }
 
-template <typename OT>
-__global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B, int cur,
-                                                    const void* __restrict__ actions,
-                                                    OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
-                                                    float* __restrict__ rew_out,
-                                                    uint8_t* __restrict__ coll_out,
-                                                    uint8_t* __restrict__ done_out) {
+// MODE kFlock: Flock.step. MODE kTdm: TDM.step (combat.py:104-184) — the same
+// physics with alive masks, plus melee ray casts, health, deaths and the full
+// relative observation; `TP`/`TB` are unused for Flock.
+template <int MODE, typename OT>
+__global__ __launch_bounds__(W) void env_step_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
+                                                  int cur, const void* __restrict__ actions,
+                                                  OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
+                                                  float* __restrict__ rew_out,
+                                                  uint8_t* __restrict__ coll_out,
+                                                  uint8_t* __restrict__ done_out) {
+  constexpr bool kT = MODE == kTdm;
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int N = P.n_agents;
   const int C = P.max_contacts;
-  const bool act = lane < N;
+  // a body that takes part in the physics: every agent (Flock) / alive agents (TDM;
+  // body.active = False removes the proxy and its contacts, combat.py:162)
+  bool act = lane < N;
   const size_t ag = (size_t)e * N + lane;
   const int nxt = cur ^ 1;
   const unsigned long long lt = lanemask_lt(lane);
@@ -208,6 +256,10 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   __shared__ float s_slp[W];
   __shared__ uint32_t s_oldm[2 * W];  // per agent: 64-bit mask of partners in the old list
   __shared__ int s_nisl;
+  // TDM only (unreferenced, hence not allocated, in the Flock instantiation)
+  __shared__ double s_hpd[W];
+  __shared__ int8_t s_hit[W];
+  __shared__ float s_ang[W];
 #ifdef MACM_STAMPS
   __shared__ int s_stat_maxisl;
 #endif
@@ -220,15 +272,26 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
   float ang = 0.0f, slp = 0.0f;
   float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  int a0 = 1, a1 = 1, a2 = 1;
+  int a0 = 1, a1 = 1, a2 = 1, a3 = 0;
   float ax = 0.0f, ay = 0.0f;
+  double hp = 0.0, cda = 0.0, cdm = 0.0;  // TDM: health, cooldown_atk, cooldown_mov_penalty
   if (act) {
     p = B.pos[ag];
     v = B.vel[ag];
     ang = B.angle[ag];
     fo = B.fat[ag];
     slp = B.sleep[ag];
-    if (P.action_mode == MACM_ACTION_DISCRETE) {
+    if constexpr (kT) {
+      const uchar4 a = reinterpret_cast<const uchar4*>(actions)[ag];
+      a0 = a.x;
+      a1 = a.y;
+      a2 = a.z;
+      a3 = a.w;
+      act = TB.alive[ag] != 0;
+      hp = TB.health[ag];
+      cda = TB.cd_atk[ag];
+      cdm = TB.cd_mov[ag];
+    } else if (P.action_mode == MACM_ACTION_DISCRETE) {
       const uint8_t* a = (const uint8_t*)actions + ag * 3;
       a0 = a[0];
       a1 = a[1];
@@ -238,14 +301,23 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       ax = c.x;
       ay = c.y;
     }
-    tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
+    if constexpr (!kT) tg = B.targets[(size_t)e * P.n_targets + B.tidx[lane]];
   }
+  const bool act0 = act;  // TDM: alive when the step starts (acts this step)
   double time_passed = 0.0;
   int st_prev = 0;
   unsigned long long ctr[4] = {0ull, 0ull, 0ull, 0ull};
+  int2 lis = make_int2(0, -1);
+  int win_prev = -1;
+  uint8_t done_prev = 0;
   if (lane == 0) {
     time_passed = B.time_passed[e];
     st_prev = B.status[e];
+    if constexpr (kT) {
+      lis = TB.listener[e];
+      win_prev = TB.winner[e];
+      done_prev = B.done[e];
+    }
     const ulonglong2* ec = reinterpret_cast<const ulonglong2*>(B.env_counters + (size_t)e * 4);
     const ulonglong2 c01 = ec[0], c23 = ec[1];
     ctr[0] = c01.x;
@@ -274,8 +346,10 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   int status = 0;
   STAMP(0);
 
-  // ---- actions -> angle, force (mvmnt.py:97-129) --------------------------
+  // ---- actions -> angle, force (mvmnt.py:97-129, combat.py:121-139) ----------
   float Fx = 0.0f, Fy = 0.0f;
+  bool attacking = false;
+  float ray_x = 0.0f, ray_y = 0.0f;
   if (act) {
     if (P.action_mode == MACM_ACTION_DISCRETE) {
       // agent.body.angle = angle + (a2-1) * rotation_speed * (1/hz) -> SetTransform(float32)
@@ -288,10 +362,29 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       ang = af;
       const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
       const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
-      const double fx = (cos(ad) * k0 + cos(ad + M_PI / 2) * k1) * cc * P.force;
-      const double fy = (sin(ad) * k0 + sin(ad + M_PI / 2) * k1) * cc * P.force;
+      double force = P.force;
+      // Agent.force = _force * (1 - percent_mov_penalty * int(cooldown_mov_penalty > 0))   combat.py:46-49
+      if constexpr (kT) force = P.force * (1.0 - TP.percent_mov_penalty * (double)(cdm > 0.0));
+      const double fx = (cos(ad) * k0 + cos(ad + M_PI / 2) * k1) * cc * force;
+      const double fy = (sin(ad) * k0 + sin(ad + M_PI / 2) * k1) * cc * force;
       Fx = (float)fx;  // ApplyForce: b2Vec2(float32) accumulated onto m_force = 0
       Fy = (float)fy;
+      if constexpr (kT) {  // melee (combat.py:141-155)
+        if (cda <= 0.0) {
+          if (a3) {
+            attacking = true;
+            // point2 = point1 + (range*cos(angle), range*sin(angle)): b2Vec2 + tuple is a
+            // float32 add of the float32-converted tuple
+            ray_x = p.x + (float)(TP.melee_range * cos(ad));
+            ray_y = p.y + (float)(TP.melee_range * sin(ad));
+            cda = TP.cooldown_atk;
+            cdm = TP.cooldown_mov_penalty;
+          }
+        } else {
+          cda -= P.inv_hz;
+          if (TP.decay_mov_penalty) cdm -= P.inv_hz;
+        }
+      }
     } else {
       float x = ax, y = ay;
       if ((x * x + y * y) > 1.0f) {
@@ -304,6 +397,60 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     Fx = 0.0f + Fx;  // m_force += force, from ClearForces' zero
     Fy = 0.0f + Fy;
   }
+  unsigned long long att_m = 0ull, alive0_m = 0ull;
+  if constexpr (kT) {
+    // Ray casts. Bodies do not move during the action loop (SetTransform keeps the
+    // position) and deaths come after it, so every cast sees the same world: all
+    // rays are cast in parallel; only the listener update is ordered.
+    alive0_m = __ballot(act);
+    att_m = __ballot(attacking);
+    s_hpd[lane] = hp;
+    __syncthreads();  // s_cx / s_cy / s_hpd visible
+    if (att_m) {
+      // b2World::RayCast + RayCastClosestCallback (cm_framework.py:56-86): each
+      // b2CircleShape::RayCast hit clips maxFraction to its fraction; candidates in
+      // body order, as the oracle (b2l_world_raycast)
+      int hit = -1;
+      const float rvx = ray_x - p.x, rvy = ray_y - p.y;  // r = p2 - p1
+      const float rrr = rvx * rvx + rvy * rvy;
+      const float rad2 = P.radius * P.radius;
+      float maxf = 1.0f;
+      for (unsigned long long m = alive0_m; m; m &= m - 1ull) {
+        const int j = __builtin_ctzll(m);
+        const float sx = p.x - s_cx[j], sy = p.y - s_cy[j];  // s = p1 - position
+        const float bb = (sx * sx + sy * sy) - rad2;
+        const float c = sx * rvx + sy * rvy;
+        const float sigma = c * c - rrr * bb;
+        if (sigma < 0.0f || rrr < kEps) continue;
+        float a = -(c + sqrtf(sigma));
+        if (0.0f <= a && a <= maxf * rrr) {
+          a /= rrr;
+          maxf = a;
+          hit = j;
+        }
+      }
+      s_hit[lane] = (int8_t)(attacking ? hit : -1);
+      __syncthreads();
+      if (lane == 0) {
+        // listener.hit / listener.fixture persist across casts and steps (literal), or
+        // reset per cast (fresh_raycast); damage in agent order (combat.py:152-153)
+        for (unsigned long long m = att_m; m; m &= m - 1ull) {
+          const int h = s_hit[__builtin_ctzll(m)];
+          if (TP.fresh_raycast) {
+            if (h >= 0) s_hpd[h] -= TP.melee_dmg;
+          } else {
+            if (h >= 0) lis = make_int2(1, h);
+            if (lis.x) s_hpd[lis.y] -= TP.melee_dmg;
+          }
+        }
+      }
+      __syncthreads();
+      hp = s_hpd[lane];
+    }
+    if (act && hp <= 0.0) act = false;  // deaths: body.active = False (combat.py:157-165)
+  }
+  // bodies in the physics step (Flock: all N; TDM: alive after this step's deaths)
+  const unsigned long long livem = __ballot(act);
   __syncthreads();
   STAMP(1);
 
@@ -330,10 +477,13 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     bool touch = false;
     if (k < M) {
       const int a = ab & 0xffffu, b = ab >> 16;
-      const float dx = s_cx[b] - s_cx[a], dy = s_cy[b] - s_cy[a];
-      touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
-      atomicOr(&s_oldm[2 * a + (b >> 5)], 1u << (b & 31));
-      atomicOr(&s_oldm[2 * b + (a >> 5)], 1u << (a & 31));
+      // TDM: contacts of a body that died this step were destroyed with its proxy
+      if (!kT || ((livem >> a) & (livem >> b) & 1ull)) {
+        const float dx = s_cx[b] - s_cx[a], dy = s_cy[b] - s_cy[a];
+        touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+        atomicOr(&s_oldm[2 * a + (b >> 5)], 1u << (b & 31));
+        atomicOr(&s_oldm[2 * b + (a >> 5)], 1u << (a & 31));
+      }
     }
     const unsigned long long m = __ballot(touch);
     if (touch) {
@@ -643,7 +793,7 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
   //   FindNewContacts creates        Ov(F_t) \ Ov(F_{t-1})
   // Overlap is symmetric, so the ballot of ovn at iteration j is agent j's
   // partner row; lane j keeps it. Agent j's record arrives by LDS broadcast.
-  const unsigned long long valid = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+  const unsigned long long valid = livem;
   unsigned long long myov = 0ull;
   float best = __builtin_inff();
   int bj = lane == 0 ? 1 : 0;
@@ -662,12 +812,14 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
       const unsigned long long row = __ballot(!(sepv > 0.0f)) & valid;
       const bool self = lane == j;
       myov = self ? row : myov;
-      const float dx = q[u].c.x - cx, dy = q[u].c.y - cy;  // other.position - agent.position
-      const float d2 = dx * dx + dy * dy;                 // b2DistanceSquared(other, agent)
-      const float d2o = self ? __builtin_inff() : d2;
-      if (d2o < best) {  // strict '<': lowest index wins ties (mvmnt.py:194)
-        best = d2o;
-        bj = j;
+      if constexpr (!kT) {
+        const float dx = q[u].c.x - cx, dy = q[u].c.y - cy;  // other.position - agent.position
+        const float d2 = dx * dx + dy * dy;                 // b2DistanceSquared(other, agent)
+        const float d2o = self ? __builtin_inff() : d2;
+        if (d2o < best) {  // strict '<': lowest index wins ties (mvmnt.py:194)
+          best = d2o;
+          bj = j;
+        }
       }
     }
   }
@@ -723,37 +875,89 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
 
   // ---- rewards (mvmnt.py:160-179) and obs (mvmnt.py:181-222) -------------------
   float rew = 0.0f;
-  if (act) {
-    const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
-    const float td2 = tdx * tdx + tdy * tdy;       // b2DistanceSquared(target, position)
-    const double d = sqrt((double)td2);
-    if (coll) rew = -1.0f;
-    else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
-    else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
-    rew_out[ag] = rew;
-    if (coll_out) coll_out[ag] = coll ? 1 : 0;
-    if (nbr_out) nbr_out[ag] = bj;
-    if (obs) {
-      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-      const float rx = s_cx[bj] - cx, ry = s_cy[bj] - cy;
-      write_obs<OT>(obs + ag * od, P.coord, ang, best, rx, ry, tdx, tdy, td2);
+  if constexpr (!kT) {
+    if (act) {
+      const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
+      const float td2 = tdx * tdx + tdy * tdy;       // b2DistanceSquared(target, position)
+      const double d = sqrt((double)td2);
+      if (coll) rew = -1.0f;
+      else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
+      else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
+      rew_out[ag] = rew;
+      if (coll_out) coll_out[ag] = coll ? 1 : 0;
+      if (nbr_out) nbr_out[ag] = bj;
+      if (obs) {
+        const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+        const float rx = s_cx[bj] - cx, ry = s_cy[bj] - cy;
+        write_obs<OT>(obs + ag * od, P.coord, ang, best, rx, ry, tdx, tdy, td2);
+      }
+      // ---- state write-back ----
+      B.pos[ag] = make_float2(cx, cy);
+      B.vel[ag] = make_float2(vx, vy);
+      B.angle[ag] = ang;
+      B.fat[ag] = fn;
+      B.sleep[ag] = ns;
     }
-    // ---- state write-back ----
-    B.pos[ag] = make_float2(cx, cy);
-    B.vel[ag] = make_float2(vx, vy);
-    B.angle[ag] = ang;
-    B.fat[ag] = fn;
-    B.sleep[ag] = ns;
+  } else {
+    // ---- TDM state write-back + TDM.get_obs (combat.py:166-167, 206-227) -------
+    if (lane < N) {
+      if (act) {  // in the physics step
+        B.pos[ag] = make_float2(cx, cy);
+        B.vel[ag] = make_float2(vx, vy);
+        B.fat[ag] = fn;
+        B.sleep[ag] = ns;
+      }
+      if (act0) {  // acted this step (possibly died after acting)
+        B.angle[ag] = ang;
+        TB.cd_atk[ag] = cda;
+        TB.cd_mov[ag] = cdm;
+      }
+      TB.health[ag] = hp;  // the stale listener can damage dead bodies too
+      TB.alive[ag] = act ? 1 : 0;
+      if (TB.health_out) TB.health_out[ag] = hp;
+      if (TB.alive_out) TB.alive_out[ag] = act ? 1 : 0;
+    }
+    s_ang[lane] = ang;
+    __syncthreads();
+    const size_t rows = (size_t)e * N * (N - 1);
+    tdm_obs_rows<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+                     s_cx, s_cy, s_ang);
   }
   STAMP(12);
 
   // ---- per-env bookkeeping + counters (no cross-env atomics) -------------------
-  const unsigned long long mcoll = __ballot(act && coll);
-  const unsigned long long mpos = __ballot(act && rew > 0.0f);
   const unsigned long long mst1 = __ballot(status & 1), mst2 = __ballot(status & 2), mst4 = __ballot(status & 4);
+  unsigned long long c1 = 0ull, c2 = 0ull;
+  int alive_teams = 0, last_team = -1;
+  if constexpr (!kT) {
+    c1 = __popcll(__ballot(act && coll));        // collided agent-steps
+    c2 = __popcll(__ballot(act && rew > 0.0f));  // positive-reward agent-steps
+  } else {
+    c1 = __popcll(att_m);               // melee attacks
+    c2 = __popcll(alive0_m & ~livem);   // deaths
+    const int myteam = tdm_team_of(TP, lane);
+    for (int t = 0; t < TP.n_teams; ++t)
+      if (__ballot(act && myteam == t)) {
+        ++alive_teams;
+        last_team = t;
+      }
+  }
   if (lane == 0) {
     const double tp = time_passed + P.inv_hz;  // time_passed += 1/hz
-    const uint8_t dn = tp > P.time_limit ? 1 : 0;
+    uint8_t dn = tp > P.time_limit ? 1 : 0;
+    if constexpr (kT) {
+      // combat.py:172-182: done latches; winner = the last team standing
+      int win = win_prev;
+      if (done_prev) dn = 1;
+      if (alive_teams == 1) {
+        dn = 1;
+        win = last_team;
+      }
+      if (alive_teams == 0) dn = 1;
+      TB.winner[e] = win;
+      if (TB.winner_out) TB.winner_out[e] = win;
+      TB.listener[e] = lis;
+    }
     B.time_passed[e] = tp;
     B.done[e] = dn;
     if (done_out) done_out[e] = dn;
@@ -761,9 +965,10 @@ __global__ __launch_bounds__(W) void flock_step_w64(StepParams P, WorldBuffers B
     B.ccount[nxt][e] = total;
     const int st = (mst1 ? 1 : 0) | (mst2 ? 2 : 0) | (mst4 ? 4 : 0);
     if (st) B.status[e] = st_prev | st;
+    const unsigned long long c0 = kT ? (unsigned long long)__popcll(alive0_m) : (unsigned long long)N;
     ulonglong2* ec = reinterpret_cast<ulonglong2*>(B.env_counters + (size_t)e * 4);
-    ec[0] = make_ulonglong2(ctr[0] + (unsigned long long)N, ctr[1] + (unsigned long long)__popcll(mcoll));
-    ec[1] = make_ulonglong2(ctr[2] + (unsigned long long)__popcll(mpos), ctr[3] + (unsigned long long)dn);
+    ec[0] = make_ulonglong2(ctr[0] + c0, ctr[1] + c1);
+    ec[1] = make_ulonglong2(ctr[2] + c2, ctr[3] + (unsigned long long)dn);
   }
   STAMP(13);
   STAMP_STAT(14, (unsigned long long)T | ((unsigned long long)nisl << 16) | ((unsigned long long)M << 32));
@@ -872,17 +1077,139 @@ __global__ __launch_bounds__(W) void flock_observe_w64(StepParams P, WorldBuffer
   }
 }
 
+// TDM world creation (combat.py:78-101): every body active with init_health, zero
+// cooldowns, the fresh listener, initial proxies / pairs as flock_init_w64, and
+// the initial observation (self.obs = self.get_obs(), combat.py:102).
+template <typename OT>
+__global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
+                                                  int cur, OT* __restrict__ obs) {
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P.n_agents;
+  const int C = P.max_contacts;
+  const bool act = lane < N;
+  const size_t ag = (size_t)e * N + lane;
+  __shared__ float s_x[W], s_y[W], s_a[W];
+  float2 p = make_float2(0.0f, 0.0f);
+  float4 f = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float ang = 0.0f;
+  if (act) {
+    p = B.pos[ag];
+    ang = B.angle[ag];
+    const float r = P.radius;
+    f = make_float4((p.x - r) - kAabbExtension, (p.y - r) - kAabbExtension, (p.x + r) + kAabbExtension,
+                    (p.y + r) + kAabbExtension);
+    B.fat[ag] = f;
+    B.vel[ag] = make_float2(0.0f, 0.0f);
+    B.sleep[ag] = 0.0f;
+    TB.health[ag] = TP.init_health;
+    TB.cd_atk[ag] = 0.0;
+    TB.cd_mov[ag] = 0.0;
+    TB.alive[ag] = 1;
+    if (TB.health_out) TB.health_out[ag] = TP.init_health;
+    if (TB.alive_out) TB.alive_out[ag] = 1;
+  }
+  unsigned long long m = 0ull;
+  for (int j = 0; j < N; ++j) {
+    const float4 fj = make_float4(bcast(f.x, j), bcast(f.y, j), bcast(f.z, j), bcast(f.w, j));
+    if (j > lane && overlap(f, fj)) m |= 1ull << j;
+  }
+  int total = write_new_pairs(lane, act ? m : 0ull, B.cab[cur] + (size_t)e * C, B.cimp[cur] + (size_t)e * C, C);
+  int st = 0;
+  if (total > C) {
+    st = MACM_ST_CONTACT_OVERFLOW;
+    total = C;
+  }
+  s_x[lane] = p.x;
+  s_y[lane] = p.y;
+  s_a[lane] = ang;
+  const unsigned long long livem = __ballot(act);
+  __syncthreads();
+  const size_t rows = (size_t)e * N * (N - 1);
+  tdm_obs_rows<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+                   s_x, s_y, s_a);
+  if (lane == 0) {
+    B.ccount[cur][e] = total;
+    B.step_count[e] = 0;
+    B.time_passed[e] = 0.0;
+    B.done[e] = 0;
+    B.status[e] = st;
+    TB.listener[e] = make_int2(0, -1);
+    TB.winner[e] = -1;
+    if (TB.winner_out) TB.winner_out[e] = -1;
+  }
+}
+
+// TDM.get_obs of the current state without stepping.
+template <typename OT>
+__global__ __launch_bounds__(W) void tdm_observe_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
+                                                     OT* __restrict__ obs) {
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = P.n_agents;
+  const size_t ag = (size_t)e * N + lane;
+  __shared__ float s_x[W], s_y[W], s_a[W];
+  bool live = false;
+  if (lane < N) {
+    const float2 p = B.pos[ag];
+    s_x[lane] = p.x;
+    s_y[lane] = p.y;
+    s_a[lane] = B.angle[ag];
+    live = TB.alive[ag] != 0;
+  }
+  const unsigned long long livem = __ballot(live);
+  __syncthreads();
+  const size_t rows = (size_t)e * N * (N - 1);
+  tdm_obs_rows<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+                   s_x, s_y, s_a);
+}
+
 // ---- host-side launchers (C++ linkage, used by macm_capi.hip) -----------------
 hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions,
                            void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
                            hipStream_t s) {
   dim3 grid(P.n_envs), block(W);
+  const TdmParams TP{};
+  const TdmBuffers TB{};
   if (obs_f64)
-    hipLaunchKernelGGL(flock_step_w64<double>, grid, block, 0, s, P, B, cur, actions, (double*)obs, nbr, rew,
-                       coll, done);
+    hipLaunchKernelGGL((env_step_w64<kFlock, double>), grid, block, 0, s, P, B, TP, TB, cur, actions, (double*)obs,
+                       nbr, rew, coll, done);
   else
-    hipLaunchKernelGGL(flock_step_w64<float>, grid, block, 0, s, P, B, cur, actions, (float*)obs, nbr, rew, coll,
-                       done);
+    hipLaunchKernelGGL((env_step_w64<kFlock, float>), grid, block, 0, s, P, B, TP, TB, cur, actions, (float*)obs,
+                       nbr, rew, coll, done);
+  return hipGetLastError();
+}
+
+hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                               const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
+                               uint8_t* done, hipStream_t s) {
+  dim3 grid(P.n_envs), block(W);
+  if (obs_f64)
+    hipLaunchKernelGGL((env_step_w64<kTdm, double>), grid, block, 0, s, P, B, TP, TB, cur, actions, (double*)obs,
+                       nullptr, nullptr, nullptr, done);
+  else
+    hipLaunchKernelGGL((env_step_w64<kTdm, float>), grid, block, 0, s, P, B, TP, TB, cur, actions, (float*)obs,
+                       nullptr, nullptr, nullptr, done);
+  return hipGetLastError();
+}
+
+hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                               const TdmBuffers& TB, int cur, void* obs, bool obs_f64, hipStream_t s) {
+  dim3 grid(P.n_envs), block(W);
+  if (obs_f64)
+    hipLaunchKernelGGL(tdm_init_w64<double>, grid, block, 0, s, P, B, TP, TB, cur, (double*)obs);
+  else
+    hipLaunchKernelGGL(tdm_init_w64<float>, grid, block, 0, s, P, B, TP, TB, cur, (float*)obs);
+  return hipGetLastError();
+}
+
+hipError_t launch_tdm_observe_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                                  const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s) {
+  dim3 grid(P.n_envs), block(W);
+  if (obs_f64)
+    hipLaunchKernelGGL(tdm_observe_w64<double>, grid, block, 0, s, P, B, TP, TB, (double*)obs);
+  else
+    hipLaunchKernelGGL(tdm_observe_w64<float>, grid, block, 0, s, P, B, TP, TB, (float*)obs);
   return hipGetLastError();
 }
 

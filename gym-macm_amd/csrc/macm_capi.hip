@@ -28,6 +28,13 @@ hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, v
                           hipStream_t s);
 hipError_t launch_observe_wg(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
                              hipStream_t s);
+hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                               const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
+                               uint8_t* done, hipStream_t s);
+hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                               const TdmBuffers& TB, int cur, void* obs, bool obs_f64, hipStream_t s);
+hipError_t launch_tdm_observe_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                                  const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s);
 hipError_t wg_configure(int N, int tcap);
 int wg_block(int N);
 int wg_lds_bytes(int N, int tcap);
@@ -44,6 +51,18 @@ struct macm_world {
   bool wave;  // N <= 64: one wavefront per env (flock_step_w64); else one workgroup per env
   int tcap;   // touching-contact capacity per env
   std::vector<int32_t> tidx;
+  std::vector<void*> allocs;
+};
+
+struct macm_tdm {
+  macm_tdm_config cfg;
+  StepParams P;
+  WorldBuffers B;
+  TdmParams TP;
+  TdmBuffers TB;  // state pointers; output pointers are filled per call
+  int cur;
+  int device;
+  std::vector<int> team;  // agent -> team
   std::vector<void*> allocs;
 };
 
@@ -75,16 +94,46 @@ struct DeviceGuard {
 };
 
 template <typename T>
-int dalloc(macm_world* w, T** p, size_t count) {
+int dalloc(std::vector<void*>& allocs, T** p, size_t count) {
   void* q = nullptr;
   hipError_t e = hipMalloc(&q, count * sizeof(T) > 0 ? count * sizeof(T) : 16);
   if (e != hipSuccess) return fail(MACM_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
-  w->allocs.push_back(q);
+  allocs.push_back(q);
   *p = (T*)q;
   return MACM_OK;
 }
 
+template <typename T>
+int dalloc(macm_world* w, T** p, size_t count) {
+  return dalloc(w->allocs, p, count);
+}
+
 int obs_dim(const macm_config& c) { return c.coord == MACM_COORD_CARTESIAN ? 6 : 4; }
+
+// Step constants shared by Flock and TDM, derived as the reference derives them.
+void fill_body_params(StepParams& P, double hz, float radius, float density, float friction, float damping,
+                      double agent_force, double rotation_speed) {
+  // cm_framework.py:182-185 (timeStep = 1.0 / hz, a Python float) -> b2World::Step(float32 dt)
+  volatile double dt64 = 1.0 / hz;
+  P.dt = (float)dt64;
+  P.inv_dt = 1.0f / P.dt;
+  {
+    // b2CircleShape::ComputeMass + b2Body::ResetMassData (settings.py:127-133)
+    volatile float mass = density * kPi32 * radius * radius;
+    P.inv_mass = mass > 0.0f ? 1.0f / mass : 1.0f;
+    volatile float den = 1.0f + P.dt * damping;
+    P.damp = 1.0f / den;
+    volatile float ff = friction * friction;
+    P.friction = sqrtf(ff);  // b2MixFriction
+  }
+  P.radius = radius;
+  P.force_f32 = (float)agent_force;
+  P.rot_step = rotation_speed;
+  P.inv_hz = 1.0 / hz;
+  P.force = agent_force;
+  volatile double two = 2.0;
+  P.diag_c = 1.0 / sqrt(two);  // 1 / np.sqrt(2)
+}
 
 void free_world(macm_world* w) {
   for (void* p : w->allocs) (void)hipFree(p);
@@ -103,7 +152,8 @@ hipError_t launch_init(macm_world* w, const macm_outputs* out, hipStream_t s) {
 extern "C" {
 
 const char* macm_version(void) {
-  return "macm-hip 0.2.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernel N<=1024)";
+  return "macm-hip 0.3.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernel N<=1024; "
+         "TDM: wave-per-env kernel N<=64)";
 }
 int macm_abi_version(void) { return MACM_ABI_VERSION; }
 const char* macm_last_error(void) { return g_last_error.c_str(); }
@@ -196,26 +246,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   P.action_mode = c.action_mode;
   P.reward_mode = c.reward_mode;
   P.coord = c.coord;
-  // cm_framework.py:182-185 (timeStep = 1.0 / hz, a Python float) -> b2World::Step(float32 dt)
-  volatile double dt64 = 1.0 / c.hz;
-  P.dt = (float)dt64;
-  P.inv_dt = 1.0f / P.dt;
-  {
-    // b2CircleShape::ComputeMass + b2Body::ResetMassData (settings.py:127-133)
-    volatile float mass = c.density * kPi32 * c.radius * c.radius;
-    P.inv_mass = mass > 0.0f ? 1.0f / mass : 1.0f;
-    volatile float den = 1.0f + P.dt * c.linear_damping;
-    P.damp = 1.0f / den;
-    volatile float ff = c.friction * c.friction;
-    P.friction = sqrtf(ff);  // b2MixFriction
-  }
-  P.radius = c.radius;
-  P.force_f32 = (float)c.agent_force;
-  P.rot_step = c.agent_rotation_speed;
-  P.inv_hz = 1.0 / c.hz;
-  P.force = c.agent_force;
-  volatile double two = 2.0;
-  P.diag_c = 1.0 / sqrt(two);  // 1 / np.sqrt(2)
+  fill_body_params(P, c.hz, c.radius, c.density, c.friction, c.linear_damping, c.agent_force,
+                   c.agent_rotation_speed);
   P.reward_radius = c.reward_radius;
   P.time_limit = c.time_limit;
 
@@ -437,6 +469,300 @@ int macm_world_reset_counters(macm_world* w, void* stream) {
   DeviceGuard g(w->device);
   HIP_TRY(hipMemsetAsync(w->B.env_counters, 0, (size_t)w->P.n_envs * 4 * sizeof(unsigned long long),
                          (hipStream_t)stream));
+  return MACM_OK;
+}
+
+// ============================ TDM =============================================
+
+int macm_tdm_config_default(macm_tdm_config* c) {
+  if (!c) return fail(MACM_E_INVALID, "cfg is NULL");
+  memset(c, 0, sizeof(*c));
+  c->n_teams = 2;  // TDM(n_agents=[1, 1]) default, combat.py:62
+  c->team_size[0] = 1;
+  c->team_size[1] = 1;
+  c->n_agents = 2;
+  c->velocity_iterations = 8;
+  c->position_iterations = 3;
+  c->warm_starting = 1;
+  c->obs_f64 = 0;
+  c->fresh_raycast = 0;
+  c->decay_mov_penalty = 0;
+  c->hz = 60.0;
+  c->world_width = 30.0;
+  c->world_height = 30.0;
+  c->agent_rotation_speed = 0.8 * (2 * M_PI);
+  c->agent_force = 20.0;
+  c->percent_mov_penalty = 0.2;
+  c->melee_range = 2.0;
+  c->melee_dmg = 0.25;
+  c->init_health = 1.0;
+  c->cooldown_atk = 1.0;
+  c->cooldown_mov_penalty = 0.5;
+  c->time_limit = 60.0;
+  c->radius = 0.5f;
+  c->density = 1.0f;
+  c->friction = 0.3f;
+  c->linear_damping = 5.0f;
+  return MACM_OK;
+}
+
+static void free_tdm(macm_tdm* w) {
+  for (void* p : w->allocs) (void)hipFree(p);
+  w->allocs.clear();
+}
+
+int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, macm_tdm** out) {
+  if (!cfg || !out) return fail(MACM_E_INVALID, "cfg/out is NULL");
+  *out = nullptr;
+  const macm_tdm_config& c = *cfg;
+  if (n_envs <= 0) return fail(MACM_E_INVALID, "n_envs must be > 0");
+  if (c.n_teams < 1 || c.n_teams > 4) return fail(MACM_E_INVALID, "n_teams must be in [1, 4]");
+  int N = 0;
+  for (int t = 0; t < c.n_teams; ++t) {
+    if (c.team_size[t] < 0) return fail(MACM_E_INVALID, "team_size < 0");
+    N += c.team_size[t];
+  }
+  if (N != c.n_agents) return fail(MACM_E_INVALID, "n_agents != sum(team_size)");
+  if (N < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2");
+  if (N > 64) return fail(MACM_E_UNSUPPORTED, "TDM with more than 64 agents per env is not built");
+  if (!(c.hz > 0.0)) return fail(MACM_E_INVALID, "hz must be > 0");
+  if (c.velocity_iterations < 0 || c.position_iterations < 0) return fail(MACM_E_INVALID, "iterations < 0");
+  if (!(c.radius > 0.0f)) return fail(MACM_E_INVALID, "radius must be > 0");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MACM_E_INVALID, "device index out of range");
+  DeviceGuard g(device);
+
+  macm_tdm* w = new macm_tdm();
+  w->cfg = c;
+  w->device = device;
+  w->cur = 0;
+  const int C = N * (N - 1) / 2;  // every pair: the list never overflows
+  StepParams& P = w->P;
+  memset(&P, 0, sizeof(P));
+  P.n_envs = n_envs;
+  P.n_agents = N;
+  P.n_targets = 0;
+  P.max_contacts = C;
+  P.vel_iters = c.velocity_iterations;
+  P.pos_iters = c.position_iterations;
+  P.warm_starting = c.warm_starting ? 1 : 0;
+  P.action_mode = MACM_ACTION_DISCRETE;
+  P.reward_mode = MACM_REWARD_BINARY;
+  P.coord = MACM_COORD_POLAR;
+  fill_body_params(P, c.hz, c.radius, c.density, c.friction, c.linear_damping, c.agent_force,
+                   c.agent_rotation_speed);
+  P.time_limit = c.time_limit;
+  TdmParams& TP = w->TP;
+  memset(&TP, 0, sizeof(TP));
+  TP.n_teams = c.n_teams;
+  for (int t = 0, acc = 0; t < 4; ++t) {
+    acc += t < c.n_teams ? c.team_size[t] : 0;
+    TP.team_end[t] = acc;
+  }
+  TP.fresh_raycast = c.fresh_raycast ? 1 : 0;
+  TP.decay_mov_penalty = c.decay_mov_penalty ? 1 : 0;
+  TP.melee_range = c.melee_range;
+  TP.melee_dmg = c.melee_dmg;
+  TP.cooldown_atk = c.cooldown_atk;
+  TP.cooldown_mov_penalty = c.cooldown_mov_penalty;
+  TP.percent_mov_penalty = c.percent_mov_penalty;
+  TP.init_health = c.init_health;
+  w->team.resize(N);
+  for (int i = 0; i < N; ++i) w->team[i] = tdm_team_of(TP, i);
+
+  WorldBuffers& B = w->B;
+  TdmBuffers& TB = w->TB;
+  memset(&B, 0, sizeof(B));
+  memset(&TB, 0, sizeof(TB));
+  const size_t EN = (size_t)n_envs * N, E = (size_t)n_envs;
+  std::vector<void*>& A = w->allocs;
+  int rc = MACM_OK;
+  if ((rc = dalloc(A, &B.pos, EN)) || (rc = dalloc(A, &B.vel, EN)) || (rc = dalloc(A, &B.angle, EN)) ||
+      (rc = dalloc(A, &B.fat, EN)) || (rc = dalloc(A, &B.sleep, EN)) || (rc = dalloc(A, &B.ccount[0], E)) ||
+      (rc = dalloc(A, &B.ccount[1], E)) || (rc = dalloc(A, &B.cab[0], E * C)) ||
+      (rc = dalloc(A, &B.cab[1], E * C)) || (rc = dalloc(A, &B.cimp[0], E * C)) ||
+      (rc = dalloc(A, &B.cimp[1], E * C)) || (rc = dalloc(A, &B.step_count, E)) ||
+      (rc = dalloc(A, &B.time_passed, E)) || (rc = dalloc(A, &B.done, E)) || (rc = dalloc(A, &B.status, E)) ||
+      (rc = dalloc(A, &B.env_counters, E * 4)) || (rc = dalloc(A, &TB.health, EN)) ||
+      (rc = dalloc(A, &TB.cd_atk, EN)) || (rc = dalloc(A, &TB.cd_mov, EN)) || (rc = dalloc(A, &TB.alive, EN)) ||
+      (rc = dalloc(A, &TB.listener, E)) || (rc = dalloc(A, &TB.winner, E))) {
+    free_tdm(w);
+    delete w;
+    return rc;
+  }
+  hipError_t e = hipMemset(B.env_counters, 0, E * 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * E);
+  if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * E);
+  if (e != hipSuccess) {
+    free_tdm(w);
+    delete w;
+    return fail(MACM_E_HIP, std::string("tdm init: ") + hipGetErrorString(e));
+  }
+  *out = w;
+  return MACM_OK;
+}
+
+int macm_tdm_destroy(macm_tdm* w) {
+  if (!w) return MACM_OK;
+  DeviceGuard g(w->device);
+  (void)hipDeviceSynchronize();
+  free_tdm(w);
+  delete w;
+  return MACM_OK;
+}
+
+static TdmBuffers tdm_with_outputs(const macm_tdm* w, const macm_tdm_outputs* out) {
+  TdmBuffers TB = w->TB;
+  if (out) {
+    TB.mask_out = out->mask;
+    TB.health_out = out->health;
+    TB.alive_out = out->alive;
+    TB.winner_out = out->winner;
+  }
+  return TB;
+}
+
+static int tdm_init(macm_tdm* w, const macm_tdm_outputs* out, hipStream_t s) {
+  w->cur = 0;
+  const TdmBuffers TB = tdm_with_outputs(w, out);
+  HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0, s));
+  if (out && out->done) HIP_TRY(hipMemsetAsync(out->done, 0, (size_t)w->P.n_envs, s));
+  return MACM_OK;
+}
+
+int macm_tdm_reset(macm_tdm* w, uint64_t seed, int64_t env_offset, const macm_tdm_outputs* out, void* stream) {
+  if (!w) return fail(MACM_E_INVALID, "tdm is NULL");
+  DeviceGuard g(w->device);
+  const macm_tdm_config& c = w->cfg;
+  const int E = w->P.n_envs, N = w->P.n_agents;
+  std::vector<float2> pos((size_t)E * N);
+  std::vector<float> ang((size_t)E * N);
+  for (int e = 0; e < E; ++e) {
+    PyMT19937 r(seed + (uint64_t)(env_offset + e));
+    for (int i = 0; i < N; ++i) {  // combat.py:80-95
+      const double x = r.random() * (w->team[i] + c.world_width / 2);
+      const double y = r.random() * c.world_height;
+      const double a = r.uniform(-1, 1) * M_PI;
+      pos[(size_t)e * N + i] = make_float2((float)x, (float)y);
+      ang[(size_t)e * N + i] = (float)a;
+    }
+  }
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(w->B.pos, pos.data(), pos.size() * sizeof(float2), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(w->B.angle, ang.data(), ang.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  int rc = tdm_init(w, out, s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s));  // host vectors feed the async copies
+  return MACM_OK;
+}
+
+int macm_tdm_place(macm_tdm* w, const void* pos, const void* angle, const macm_tdm_outputs* out, void* stream) {
+  if (!w || !pos || !angle) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  const size_t EN = (size_t)w->P.n_envs * w->P.n_agents;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(w->B.pos, pos, EN * sizeof(float2), hipMemcpyDefault, s));
+  HIP_TRY(hipMemcpyAsync(w->B.angle, angle, EN * sizeof(float), hipMemcpyDefault, s));
+  int rc = tdm_init(w, out, s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream) {
+  if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
+  DeviceGuard g(w->device);
+  const TdmBuffers TB = tdm_with_outputs(w, out);
+  HIP_TRY(launch_tdm_step_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
+                              w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream));
+  w->cur ^= 1;
+  return MACM_OK;
+}
+
+int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream) {
+  if (!w || !out) return fail(MACM_E_INVALID, "tdm/out is NULL");
+  DeviceGuard g(w->device);
+  const TdmBuffers TB = tdm_with_outputs(w, out);
+  HIP_TRY(launch_tdm_observe_w64(w->P, w->B, w->TP, TB, out->obs, w->cfg.obs_f64 != 0, (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t EN = (size_t)w->P.n_envs * w->P.n_agents, E = (size_t)w->P.n_envs;
+  if (out->health) HIP_TRY(hipMemcpyAsync(out->health, w->TB.health, EN * sizeof(double), hipMemcpyDefault, s));
+  if (out->alive) HIP_TRY(hipMemcpyAsync(out->alive, w->TB.alive, EN, hipMemcpyDefault, s));
+  if (out->done) HIP_TRY(hipMemcpyAsync(out->done, w->B.done, E, hipMemcpyDefault, s));
+  if (out->winner) HIP_TRY(hipMemcpyAsync(out->winner, w->TB.winner, E * sizeof(int32_t), hipMemcpyDefault, s));
+  return MACM_OK;
+}
+
+static int tdm_copy_state(macm_tdm* w, const macm_tdm_state* st, void* stream, bool to_device) {
+  if (!w || !st) return fail(MACM_E_INVALID, "tdm/state is NULL");
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t E = w->P.n_envs, N = w->P.n_agents, C = w->P.max_contacts;
+  struct Item {
+    void* user;
+    void* dev;
+    size_t bytes;
+  } items[] = {
+      {st->pos, w->B.pos, E * N * sizeof(float2)},
+      {st->vel, w->B.vel, E * N * sizeof(float2)},
+      {st->angle, w->B.angle, E * N * sizeof(float)},
+      {st->fat, w->B.fat, E * N * sizeof(float4)},
+      {st->sleep, w->B.sleep, E * N * sizeof(float)},
+      {st->health, w->TB.health, E * N * sizeof(double)},
+      {st->cd_atk, w->TB.cd_atk, E * N * sizeof(double)},
+      {st->cd_mov, w->TB.cd_mov, E * N * sizeof(double)},
+      {st->alive, w->TB.alive, E * N},
+      {st->listener, w->TB.listener, E * sizeof(int2)},
+      {st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t)},
+      {st->contact_ab, w->B.cab[w->cur], E * C * sizeof(uint32_t)},
+      {st->contact_imp, w->B.cimp[w->cur], E * C * sizeof(float2)},
+      {st->step_count, w->B.step_count, E * sizeof(int32_t)},
+      {st->time_passed, w->B.time_passed, E * sizeof(double)},
+      {st->done, w->B.done, E},
+      {st->winner, w->TB.winner, E * sizeof(int32_t)},
+  };
+  for (const Item& it : items) {
+    if (!it.user) continue;
+    if (to_device) HIP_TRY(hipMemcpyAsync(it.dev, it.user, it.bytes, hipMemcpyDefault, s));
+    else HIP_TRY(hipMemcpyAsync(it.user, it.dev, it.bytes, hipMemcpyDefault, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+int macm_tdm_get_state(macm_tdm* w, const macm_tdm_state* dst, void* stream) {
+  return tdm_copy_state(w, dst, stream, false);
+}
+
+int macm_tdm_set_state(macm_tdm* w, const macm_tdm_state* src, void* stream) {
+  return tdm_copy_state(w, src, stream, true);
+}
+
+int macm_tdm_status(macm_tdm* w, int32_t* status_or, void* stream) {
+  if (!w || !status_or) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  std::vector<int32_t> st(w->P.n_envs);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(st.data(), w->B.status, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  int32_t acc = 0;
+  for (int32_t v : st) acc |= v;
+  *status_or = acc;
+  return MACM_OK;
+}
+
+int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream) {
+  if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  std::vector<unsigned long long> h((size_t)w->P.n_envs * 4);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(h.data(), w->B.env_counters, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         s));
+  HIP_TRY(hipStreamSynchronize(s));
+  unsigned long long acc[4] = {0, 0, 0, 0};
+  for (size_t i = 0; i < h.size(); ++i) acc[i & 3] += h[i];
+  for (int i = 0; i < 4; ++i) out[i] = (int64_t)acc[i];
   return MACM_OK;
 }
 

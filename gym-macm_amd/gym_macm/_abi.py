@@ -82,6 +82,66 @@ class MacmWorldInfo(Structure):
     ]
 
 
+class MacmTdmConfig(Structure):
+    _fields_ = [
+        ("n_teams", c_int32),
+        ("team_size", c_int32 * 4),
+        ("n_agents", c_int32),
+        ("velocity_iterations", c_int32),
+        ("position_iterations", c_int32),
+        ("warm_starting", c_int32),
+        ("obs_f64", c_int32),
+        ("fresh_raycast", c_int32),
+        ("decay_mov_penalty", c_int32),
+        ("hz", c_double),
+        ("world_width", c_double),
+        ("world_height", c_double),
+        ("agent_rotation_speed", c_double),
+        ("agent_force", c_double),
+        ("percent_mov_penalty", c_double),
+        ("melee_range", c_double),
+        ("melee_dmg", c_double),
+        ("init_health", c_double),
+        ("cooldown_atk", c_double),
+        ("cooldown_mov_penalty", c_double),
+        ("time_limit", c_double),
+        ("radius", c_float),
+        ("density", c_float),
+        ("friction", c_float),
+        ("linear_damping", c_float),
+    ]
+
+
+class MacmTdmOutputs(Structure):
+    _fields_ = [(n, c_void_p) for n in ("obs", "mask", "health", "alive", "done", "winner")]
+
+
+TDM_STATE_FIELDS = ("pos", "vel", "angle", "fat", "sleep", "health", "cd_atk", "cd_mov", "alive", "listener",
+                    "contact_count", "contact_ab", "contact_imp", "step_count", "time_passed", "done", "winner")
+
+
+class MacmTdmState(Structure):
+    _fields_ = [(n, c_void_p) for n in TDM_STATE_FIELDS]
+
+
+def tdm_config_from_defaults() -> "MacmTdmConfig":
+    """macm_tdm_config_default without the HIP library (used by the CPU oracle too)."""
+    import math
+    c = MacmTdmConfig()
+    c.n_teams = 2
+    c.team_size[0] = 1
+    c.team_size[1] = 1
+    c.n_agents = 2
+    c.velocity_iterations, c.position_iterations, c.warm_starting = 8, 3, 1
+    c.hz, c.world_width, c.world_height = 60.0, 30.0, 30.0
+    c.agent_rotation_speed = 0.8 * (2 * math.pi)
+    c.agent_force, c.percent_mov_penalty = 20.0, 0.2
+    c.melee_range, c.melee_dmg, c.init_health = 2.0, 0.25, 1.0
+    c.cooldown_atk, c.cooldown_mov_penalty, c.time_limit = 1.0, 0.5, 60.0
+    c.radius, c.density, c.friction, c.linear_damping = 0.5, 1.0, 0.3, 5.0
+    return c
+
+
 class MacmLibraryError(RuntimeError):
     """The HIP library could not be loaded: the product path refuses to run."""
 
@@ -114,6 +174,17 @@ SIGNATURES = {
     "macm_world_status": (c_int, [c_void_p, POINTER(c_int32), c_void_p]),
     "macm_world_counters": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_world_reset_counters": (c_int, [c_void_p, c_void_p]),
+    "macm_tdm_config_default": (c_int, [POINTER(MacmTdmConfig)]),
+    "macm_tdm_create": (c_int, [POINTER(MacmTdmConfig), c_int32, c_int32, POINTER(c_void_p)]),
+    "macm_tdm_destroy": (c_int, [c_void_p]),
+    "macm_tdm_reset": (c_int, [c_void_p, c_uint64, c_int64, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_place": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_step": (c_int, [c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_observe": (c_int, [c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_get_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),
+    "macm_tdm_set_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),
+    "macm_tdm_status": (c_int, [c_void_p, POINTER(c_int32), c_void_p]),
+    "macm_tdm_counters": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
 }
 
 _lib = None

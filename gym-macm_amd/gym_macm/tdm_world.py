@@ -1,0 +1,165 @@
+"""Python handle over the TDM C-ABI (macm_tdm_*, include/macm.h).
+
+Replaces the per-env ``TDM`` world of the reference (gym_macm/envs/combat.py:57-102,
+one pybox2d ``b2World`` per env behind ``NoRender``) with one device-resident
+world of E team-deathmatch envs; torch tensors are the device memory and torch's
+current stream is the launch stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _abi
+from .world import _ptr
+
+
+def tdm_config(n_agents=(1, 1), obs_f64=False, fresh_raycast=False, decay_mov_penalty=False, **overrides):
+    """macm_tdm_config for TDM(n_agents=[...]) with combatSettings values
+    (settings.py:149-177); keyword overrides use the config field names."""
+    sizes = [int(n) for n in n_agents]
+    if not 1 <= len(sizes) <= 4:
+        raise ValueError("TDM supports 1 to 4 teams")
+    c = _abi.tdm_config_from_defaults()
+    c.n_teams = len(sizes)
+    for t in range(4):
+        c.team_size[t] = sizes[t] if t < len(sizes) else 0
+    c.n_agents = sum(sizes)
+    c.obs_f64 = 1 if obs_f64 else 0
+    c.fresh_raycast = 1 if fresh_raycast else 0
+    c.decay_mov_penalty = 1 if decay_mov_penalty else 0
+    names = {f for f, _ in _abi.MacmTdmConfig._fields_}
+    for k, v in overrides.items():
+        if k not in names:
+            raise TypeError(f"unknown TDM setting {k!r}")
+        setattr(c, k, v)
+    return c
+
+
+class TdmWorld:
+    """E independent TDM envs of one configuration on one GPU. Output tensors are
+    owned by this object and overwritten by every call."""
+
+    def __init__(self, cfg: _abi.MacmTdmConfig, n_envs: int = 1, device=None):
+        self.L = _abi.lib()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("the HIP world lives on a GPU device (no CPU fallback)")
+        self.device = device
+        self.cfg = cfg
+        self.E = int(n_envs)
+        self.N = int(cfg.n_agents)
+        self.C = self.N * (self.N - 1) // 2
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _abi.check(self.L.macm_tdm_create(ctypes.byref(cfg), self.E, device.index or 0, ctypes.byref(h)),
+                       "macm_tdm_create")
+        self.h = h
+        odt = torch.float64 if cfg.obs_f64 else torch.float32
+        E, N = self.E, self.N
+        kw = dict(device=device)
+        self.obs = torch.empty((E, N, N - 1, 4), dtype=odt, **kw)
+        self.mask = torch.empty((E, N, N - 1), dtype=torch.uint8, **kw)
+        self.health = torch.empty((E, N), dtype=torch.float64, **kw)
+        self.alive = torch.empty((E, N), dtype=torch.uint8, **kw)
+        self.done = torch.zeros((E,), dtype=torch.uint8, **kw)
+        self.winner = torch.full((E,), -1, dtype=torch.int32, **kw)
+        self._out = _abi.MacmTdmOutputs(_ptr(self.obs), _ptr(self.mask), _ptr(self.health), _ptr(self.alive),
+                                        _ptr(self.done), _ptr(self.winner))
+        team = []
+        for t in range(cfg.n_teams):
+            team += [t] * cfg.team_size[t]
+        self.team = np.array(team, np.int32)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.L.macm_tdm_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def outputs(self):
+        return self.obs, self.mask, self.health, self.alive, self.done, self.winner
+
+    def reset(self, seed: int, env_offset: int = 0):
+        """Env e := TDM(...) after random.seed(seed + env_offset + e); writes the initial obs."""
+        _abi.check(self.L.macm_tdm_reset(self.h, int(seed), int(env_offset), ctypes.byref(self._out),
+                                         self._stream()), "macm_tdm_reset")
+        return self.outputs()
+
+    def place(self, pos, angle):
+        pos = np.ascontiguousarray(pos, np.float32).reshape(self.E, self.N, 2)
+        angle = np.ascontiguousarray(angle, np.float32).reshape(self.E, self.N)
+        _abi.check(self.L.macm_tdm_place(self.h, pos.ctypes.data, angle.ctypes.data, ctypes.byref(self._out),
+                                         self._stream()), "macm_tdm_place")
+        return self.outputs()
+
+    def step(self, actions: torch.Tensor):
+        """actions: uint8 [E, N, 4] (forward, lateral, rotation, attack) on this device."""
+        if actions.device != self.device or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous tensor on the world's device")
+        if actions.dtype not in (torch.uint8, torch.int8) or tuple(actions.shape) != (self.E, self.N, 4):
+            raise ValueError(f"TDM actions must be uint8 [{self.E},{self.N},4]")
+        _abi.check(self.L.macm_tdm_step(self.h, _ptr(actions), ctypes.byref(self._out), self._stream()),
+                   "macm_tdm_step")
+        return self.outputs()
+
+    def step_raw(self, actions_ptr: int, stream_handle: int) -> None:
+        """Minimal-overhead launch for timed loops (no validation)."""
+        self.L.macm_tdm_step(self.h, ctypes.c_void_p(actions_ptr), ctypes.byref(self._out),
+                             ctypes.c_void_p(stream_handle))
+
+    def observe(self):
+        _abi.check(self.L.macm_tdm_observe(self.h, ctypes.byref(self._out), self._stream()), "macm_tdm_observe")
+        return self.outputs()
+
+    def state_buffers(self):
+        E, N, C = self.E, self.N, self.C
+        return dict(pos=np.zeros((E, N, 2), np.float32), vel=np.zeros((E, N, 2), np.float32),
+                    angle=np.zeros((E, N), np.float32), fat=np.zeros((E, N, 4), np.float32),
+                    sleep=np.zeros((E, N), np.float32), health=np.zeros((E, N), np.float64),
+                    cd_atk=np.zeros((E, N), np.float64), cd_mov=np.zeros((E, N), np.float64),
+                    alive=np.zeros((E, N), np.uint8), listener=np.zeros((E, 2), np.int32),
+                    contact_count=np.zeros((E,), np.int32), contact_ab=np.zeros((E, C), np.uint32),
+                    contact_imp=np.zeros((E, C, 2), np.float32), step_count=np.zeros((E,), np.int32),
+                    time_passed=np.zeros((E,), np.float64), done=np.zeros((E,), np.uint8),
+                    winner=np.zeros((E,), np.int32))
+
+    def get_state(self) -> dict:
+        s = self.state_buffers()
+        st = _abi.MacmTdmState(*[ctypes.c_void_p(s[k].ctypes.data) for k in _abi.TDM_STATE_FIELDS])
+        _abi.check(self.L.macm_tdm_get_state(self.h, ctypes.byref(st), self._stream()), "macm_tdm_get_state")
+        idx = np.arange(self.C)[None, :] >= s["contact_count"][:, None]
+        s["contact_ab"][idx] = 0
+        s["contact_imp"][idx] = 0
+        return s
+
+    def set_state(self, s: dict) -> None:
+        ref = self.state_buffers()
+        arrs = {}
+        for k, v in ref.items():
+            a = np.ascontiguousarray(np.asarray(s[k], dtype=v.dtype))
+            if a.shape != v.shape:
+                raise ValueError(f"state[{k!r}] has shape {a.shape}, expected {v.shape}")
+            arrs[k] = a
+        st = _abi.MacmTdmState(*[ctypes.c_void_p(arrs[k].ctypes.data) for k in _abi.TDM_STATE_FIELDS])
+        _abi.check(self.L.macm_tdm_set_state(self.h, ctypes.byref(st), self._stream()), "macm_tdm_set_state")
+
+    def status(self) -> int:
+        v = ctypes.c_int32()
+        _abi.check(self.L.macm_tdm_status(self.h, ctypes.byref(v), self._stream()), "macm_tdm_status")
+        return int(v.value)
+
+    def counters(self) -> np.ndarray:
+        out = (ctypes.c_int64 * 4)()
+        _abi.check(self.L.macm_tdm_counters(self.h, out, self._stream()), "macm_tdm_counters")
+        return np.array(list(out), np.int64)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 1
+#define MACM_ABI_VERSION 2
 
 enum {
   MACM_OK = 0,
@@ -88,6 +88,86 @@ typedef struct macm_config {
   float friction;              /* 0.3                                                */
   float linear_damping;        /* 5                                 settings.py:133  */
 } macm_config;
+
+/*
+ * macm_tdm_config — the team-deathmatch env (gym_macm/envs/combat.py:13-264,
+ * combatSettings settings.py:149-177). The reference's TDM cannot be built as
+ * shipped (combat.py:65 NameError; :150-151,173 read attributes that do not
+ * exist); this is its semantics with those four names supplied from
+ * combatSettings, everything else literal (see DESIGN.md "TDM").
+ */
+typedef struct macm_tdm_config {
+  int32_t n_teams;              /* len(n_agents)                      combat.py:70-73 */
+  int32_t team_size[4];         /* n_agents[i]                                        */
+  int32_t n_agents;             /* sum(n_agents) (<= 64)                              */
+  int32_t velocity_iterations;  /* 8                                                  */
+  int32_t position_iterations;  /* 3                                                  */
+  int32_t warm_starting;        /* 1                                                  */
+  int32_t obs_f64;              /* obs written as float32 (0) or float64 (1)          */
+  int32_t fresh_raycast;        /* 0 (reference): ONE RayCastClosestCallback whose hit /
+                                   fixture are never reset (cm_framework.py:62-65,76,
+                                   combat.py:147-153), so after the first hit every
+                                   attack damages the last-hit body. 1: per-cast hit.  */
+  int32_t decay_mov_penalty;    /* 0 (reference): cooldown_mov_penalty is never
+                                   decremented (combat.py:151,155). 1: decremented by
+                                   1/hz alongside cooldown_atk.                        */
+  double hz;                    /* 60                                                 */
+  double world_width;           /* 30                                 combat.py:76    */
+  double world_height;          /* 30                                 combat.py:77    */
+  double agent_rotation_speed;  /* 0.8 * 2pi                          combat.py:18    */
+  double agent_force;           /* 20                                 combat.py:19    */
+  double percent_mov_penalty;   /* 0.2                                combat.py:22    */
+  double melee_range;           /* 2                                  combat.py:20    */
+  double melee_dmg;             /* 0.25                               combat.py:21    */
+  double init_health;           /* 1                                  combat.py:14    */
+  double cooldown_atk;          /* 1                                  settings.py:164 */
+  double cooldown_mov_penalty;  /* 0.5                                settings.py:165 */
+  double time_limit;            /* 60                                 settings.py:163 */
+  float radius, density, friction, linear_damping;
+} macm_tdm_config;
+
+/*
+ * Device-side outputs of one TDM step (device pointers; NULL = not wanted).
+ * TDM.get_obs (combat.py:206-227) as fixed slots: slot k of agent i is agent
+ * j = k < i ? k : k + 1 and holds (r, t, p, is_ally); the dict API lists the alive
+ * j in the same order. mask = agents i and j both alive; masked slots are zero.
+ */
+typedef struct macm_tdm_outputs {
+  void* obs;        /* [E, N, N-1, 4] float32 or float64 (config.obs_f64)     */
+  uint8_t* mask;    /* [E, N, N-1]                                           */
+  double* health;   /* [E, N]  Agent.health                                  */
+  uint8_t* alive;   /* [E, N]  Agent.alive                                   */
+  uint8_t* done;    /* [E]     TDM.done (latches)                            */
+  int32_t* winner;  /* [E]     TDM.winner, -1 = None                         */
+} macm_tdm_outputs;
+
+/*
+ * TDM state, SoA (host or device pointers, NULL = skip). Physics fields as
+ * macm_state; plus
+ *   health, cd_atk, cd_mov [E, N] float64   Agent.health / cooldown_atk / cooldown_mov_penalty
+ *   alive                  [E, N] uint8
+ *   listener               [E, 2] int32     (RayCastClosestCallback.hit, body of .fixture or -1)
+ *   done [E] uint8, winner [E] int32
+ */
+typedef struct macm_tdm_state {
+  void* pos;
+  void* vel;
+  void* angle;
+  void* fat;
+  void* sleep;
+  void* health;
+  void* cd_atk;
+  void* cd_mov;
+  void* alive;
+  void* listener;
+  void* contact_count;
+  void* contact_ab;
+  void* contact_imp;
+  void* step_count;
+  void* time_passed;
+  void* done;
+  void* winner;
+} macm_tdm_state;
 
 /*
  * Device-side outputs of one step (all device pointers; NULL = not wanted,
@@ -209,6 +289,47 @@ int macm_world_status(macm_world* w, int32_t* status_or, void* stream);
  */
 int macm_world_counters(macm_world* w, int64_t out[4], void* stream);
 int macm_world_reset_counters(macm_world* w, void* stream);
+
+/* ---- TDM (gym_macm:cm-tdm-v0, combat.py:57-264) -------------------------- */
+
+typedef struct macm_tdm macm_tdm;
+
+/* combatSettings / Agent defaults (settings.py:149-177, combat.py:13-29), n_agents=[1,1]. */
+int macm_tdm_config_default(macm_tdm_config* cfg);
+
+/*
+ * Create E TDM envs (N = sum(team_size) <= 64 agents). Replaces TDM.__init__'s
+ * world + body creation (combat.py:61-102). State is undefined until reset/place.
+ */
+int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, macm_tdm** out);
+int macm_tdm_destroy(macm_tdm* w);
+
+/*
+ * Initialise every env as TDM.__init__ after random.seed(seed + env_offset + e):
+ * per agent in team order x = random()*(team + width/2), y = random()*height,
+ * angle = uniform(-1, 1)*pi (combat.py:80-95). Writes the initial obs into `out`.
+ */
+int macm_tdm_reset(macm_tdm* w, uint64_t seed, int64_t env_offset, const macm_tdm_outputs* out, void* stream);
+
+/* As reset with caller-drawn poses: pos [E, N, 2] float32, angle [E, N] float32. */
+int macm_tdm_place(macm_tdm* w, const void* pos, const void* angle, const macm_tdm_outputs* out, void* stream);
+
+/*
+ * One TDM.step for all E envs (combat.py:104-184). actions: device uint8
+ * [E, N, 4] (MultiDiscrete([3,3,3,2]): forward, lateral, rotation, attack);
+ * rows of dead agents are ignored.
+ */
+int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream);
+
+/* TDM.get_obs of the current state without stepping. */
+int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream);
+
+int macm_tdm_get_state(macm_tdm* w, const macm_tdm_state* dst, void* stream);
+int macm_tdm_set_state(macm_tdm* w, const macm_tdm_state* src, void* stream);
+int macm_tdm_status(macm_tdm* w, int32_t* status_or, void* stream);
+
+/* out[0] alive agent-steps, out[1] melee attacks, out[2] deaths, out[3] env-steps with done. */
+int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream);
 
 #ifdef __cplusplus
 }

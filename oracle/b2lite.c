@@ -483,6 +483,7 @@ static void find_new_contacts(b2l_world* w) {
     aabb qa = w->fat[q];
     for (int p = 0; p < w->nb; ++p) {
       if (p == q) continue;
+      if ((w->bodies[p].flags & BF_ACTIVE) == 0) continue; /* proxy destroyed */
       if (!aabb_overlap(w->fat[p], qa)) continue;
       if (w->pair_count == w->pair_cap) {
         w->pair_cap = w->pair_cap ? 2 * w->pair_cap : 64;
@@ -1019,6 +1020,58 @@ void b2l_world_flush_new_contacts(b2l_world* w) {
     find_new_contacts(w);
     w->new_fixture = 0;
   }
+}
+
+/* b2Body::SetActive(false): DestroyProxies (+ UnBufferMove) and destroy every
+ * attached contact. Reactivation is not needed by the reference (TDM deaths,
+ * gym_macm/envs/combat.py:157-165). */
+void b2l_body_set_active(b2l_world* w, int id, int flag) {
+  body* b = &w->bodies[id];
+  if (flag || (b->flags & BF_ACTIVE) == 0) return;
+  b->flags &= ~BF_ACTIVE;
+  for (int i = 0; i < w->move_count; ++i)
+    if (w->move_buf[i] == b->proxy_id) w->move_buf[i] = -1;
+  int e = b->contact_list;
+  while (e >= 0) {
+    int next = *edge_next(w, e);
+    contact_destroy(w, edge_contact(e));
+    e = next;
+  }
+  b->contact_list = -1;
+}
+
+int b2l_body_active(const b2l_world* w, int id) { return (w->bodies[id].flags & BF_ACTIVE) != 0; }
+
+/* b2World::RayCast with a closest-hit callback that returns the reported
+ * fraction (cm_framework.py:56-86): b2CircleShape::RayCast per proxy with the
+ * clipped maxFraction. The dynamic tree visits candidates in a tree-dependent
+ * order; only exactly equal fractions could make that order matter, and here
+ * candidates are visited in proxy order. Returns the body of the last reported
+ * fixture (= closest hit) or -1. */
+int b2l_world_raycast(const b2l_world* w, float x1, float y1, float x2, float y2, float* fraction_out) {
+  float max_fraction = 1.0f;
+  int best = -1;
+  v2 p1 = V(x1, y1), p2 = V(x2, y2);
+  for (int i = 0; i < w->nb; ++i) {
+    const body* b = &w->bodies[i];
+    if ((b->flags & BF_ACTIVE) == 0) continue;
+    v2 position = vadd(b->xf.p, rot_mul(b->xf.q, b->shape_p));
+    v2 s = vsub(p1, position);
+    float bb = vdot(s, s) - b->radius * b->radius;
+    v2 r = vsub(p2, p1);
+    float c = vdot(s, r);
+    float rr = vdot(r, r);
+    float sigma = c * c - rr * bb;
+    if (sigma < 0.0f || rr < B2_EPS) continue;
+    float a = -(c + sqrtf(sigma));
+    if (0.0f <= a && a <= max_fraction * rr) {
+      a /= rr;
+      max_fraction = a; /* ReportFixture returns fraction */
+      best = i;
+    }
+  }
+  if (fraction_out) *fraction_out = max_fraction;
+  return best;
 }
 
 void b2l_world_set_solver_state(b2l_world* w, float inv_dt0, int new_fixture) {

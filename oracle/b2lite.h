@@ -73,6 +73,11 @@ void b2l_body_set_state(b2l_world* w, int id, float x, float y, float angle, flo
                         float sleep_time, const float* fat4);
 /* Perform the deferred first FindNewContacts now (no-op once stepped). */
 void b2l_world_flush_new_contacts(b2l_world* w);
+/* b2Body::SetActive(false) (destroys the proxy and every attached contact). */
+void b2l_body_set_active(b2l_world* w, int id, int flag);
+int b2l_body_active(const b2l_world* w, int id);
+/* b2World::RayCast(closest-hit callback); returns the hit body or -1. */
+int b2l_world_raycast(const b2l_world* w, float x1, float y1, float x2, float y2, float* fraction_out);
 /* World-level solver state: inv_dt0 and the "new fixture" flag. */
 void b2l_world_set_solver_state(b2l_world* w, float inv_dt0, int new_fixture);
 

@@ -294,55 +294,85 @@ static int fat_overlap(const float* a, const float* b) {
 }
 
 /*
- * Export env state in the product's macm_state layout (include/macm.h). The
- * ordered contact list is the world list filtered to the pairs whose CURRENT fat
- * AABBs overlap (the contacts that survive the next Collide), with the warm-start
- * impulses of contacts that carry a manifold point.
+ * Export one world's bodies and contacts in the product's macm_state layout
+ * (include/macm.h), env slot e. The ordered contact list is the world list
+ * filtered to the pairs whose CURRENT fat AABBs overlap (the contacts that survive
+ * the next Collide), with the warm-start impulses of contacts that carry a
+ * manifold point. Shared with tdm_oracle.c.
  */
+void fo_export_world(b2l_world* w, int N, size_t e, float* pos, float* vel, float* angle, float* fat,
+                     float* sleep, int32_t* contact_count, uint32_t* contact_ab, float* contact_imp,
+                     int max_contacts) {
+  for (int i = 0; i < N; ++i) {
+    float s[7], f[4];
+    b2l_body_get(w, i, s);
+    b2l_body_get_fat(w, i, f);
+    size_t k = e * N + i;
+    if (pos) { pos[2 * k] = s[0]; pos[2 * k + 1] = s[1]; }
+    if (vel) { vel[2 * k] = s[3]; vel[2 * k + 1] = s[4]; }
+    if (angle) angle[k] = s[2];
+    if (sleep) sleep[k] = s[5];
+    if (fat) memcpy(fat + 4 * k, f, sizeof(f));
+  }
+  if (!contact_count) return;
+  b2l_world_flush_new_contacts(w);
+  int n = b2l_world_contacts(w, NULL, 0);
+  int* cl = (int*)malloc(sizeof(int) * 3 * (size_t)(n ? n : 1));
+  float* im = (float*)malloc(sizeof(float) * 3 * (size_t)(n ? n : 1));
+  b2l_world_contacts(w, cl, n);
+  b2l_world_contact_impulses(w, im, n);
+  int m = 0;
+  for (int k = 0; k < n; ++k) {
+    float fa[4], fb[4];
+    b2l_body_get_fat(w, cl[3 * k], fa);
+    b2l_body_get_fat(w, cl[3 * k + 1], fb);
+    if (!fat_overlap(fa, fb)) continue;
+    if (m < max_contacts) {
+      size_t o = e * max_contacts + m;
+      contact_ab[o] = (uint32_t)cl[3 * k] | ((uint32_t)cl[3 * k + 1] << 16);
+      int pc = (int)im[3 * k + 2];
+      contact_imp[2 * o] = pc > 0 ? im[3 * k] : 0.0f;
+      contact_imp[2 * o + 1] = pc > 0 ? im[3 * k + 1] : 0.0f;
+    }
+    ++m;
+  }
+  contact_count[e] = m;
+  free(cl);
+  free(im);
+}
+
+/* Inverse of fo_export_world: body states, then the ordered list (see b2l_world_load_contacts). */
+void fo_import_world(b2l_world* w, int N, size_t e, const float* pos, const float* vel, const float* angle,
+                     const float* fat, const float* sleep, const int32_t* contact_count,
+                     const uint32_t* contact_ab, const float* contact_imp, int max_contacts) {
+  for (int i = 0; i < N; ++i) {
+    size_t k = e * N + i;
+    b2l_body_set_state(w, i, pos[2 * k], pos[2 * k + 1], angle[k], vel[2 * k], vel[2 * k + 1], sleep[k],
+                       fat + 4 * k);
+  }
+  int n = contact_count[e];
+  int* ab = (int*)malloc(sizeof(int) * 2 * (size_t)(n ? n : 1));
+  int* pc = (int*)malloc(sizeof(int) * (size_t)(n ? n : 1));
+  for (int k = 0; k < n; ++k) {
+    uint32_t v = contact_ab[e * max_contacts + k];
+    ab[2 * k] = (int)(v & 0xffffu);
+    ab[2 * k + 1] = (int)(v >> 16);
+    const float* im = contact_imp + 2 * (e * max_contacts + k);
+    pc[k] = (im[0] != 0.0f || im[1] != 0.0f) ? 1 : 0;
+  }
+  b2l_world_load_contacts(w, n, ab, contact_imp + 2 * e * max_contacts, pc);
+  free(ab);
+  free(pc);
+}
+
 void fo_get_state(fo_batch* b, float* pos, float* vel, float* angle, float* fat, float* sleep,
                   float* targets, int32_t* contact_count, uint32_t* contact_ab, float* contact_imp,
                   int max_contacts, int32_t* step_count, double* time_passed) {
-  const int N = b->N;
   for (int e = 0; e < b->E; ++e) {
     fo_env* en = &b->envs[e];
-    for (int i = 0; i < N; ++i) {
-      float s[7], f[4];
-      b2l_body_get(en->w, i, s);
-      b2l_body_get_fat(en->w, i, f);
-      size_t k = (size_t)e * N + i;
-      if (pos) { pos[2 * k] = s[0]; pos[2 * k + 1] = s[1]; }
-      if (vel) { vel[2 * k] = s[3]; vel[2 * k + 1] = s[4]; }
-      if (angle) angle[k] = s[2];
-      if (sleep) sleep[k] = s[5];
-      if (fat) memcpy(fat + 4 * k, f, sizeof(f));
-    }
+    fo_export_world(en->w, b->N, (size_t)e, pos, vel, angle, fat, sleep, contact_count, contact_ab, contact_imp,
+                    max_contacts);
     if (targets) memcpy(targets + (size_t)e * 2 * b->T, en->targets, sizeof(float) * 2 * (size_t)b->T);
-    if (contact_count) {
-      b2l_world_flush_new_contacts(en->w);
-      int n = b2l_world_contacts(en->w, NULL, 0);
-      int* cl = (int*)malloc(sizeof(int) * 3 * (size_t)(n ? n : 1));
-      float* im = (float*)malloc(sizeof(float) * 3 * (size_t)(n ? n : 1));
-      b2l_world_contacts(en->w, cl, n);
-      b2l_world_contact_impulses(en->w, im, n);
-      int m = 0;
-      for (int k = 0; k < n; ++k) {
-        float fa[4], fb[4];
-        b2l_body_get_fat(en->w, cl[3 * k], fa);
-        b2l_body_get_fat(en->w, cl[3 * k + 1], fb);
-        if (!fat_overlap(fa, fb)) continue;
-        if (m < max_contacts) {
-          size_t o = (size_t)e * max_contacts + m;
-          contact_ab[o] = (uint32_t)cl[3 * k] | ((uint32_t)cl[3 * k + 1] << 16);
-          int pc = (int)im[3 * k + 2];
-          contact_imp[2 * o] = pc > 0 ? im[3 * k] : 0.0f;
-          contact_imp[2 * o + 1] = pc > 0 ? im[3 * k + 1] : 0.0f;
-        }
-        ++m;
-      }
-      contact_count[e] = m;
-      free(cl);
-      free(im);
-    }
     if (step_count) step_count[e] = en->step_count;
     if (time_passed) time_passed[e] = en->time_passed;
   }
@@ -352,28 +382,11 @@ void fo_set_state(fo_batch* b, const float* pos, const float* vel, const float* 
                   const float* fat, const float* sleep, const float* targets,
                   const int32_t* contact_count, const uint32_t* contact_ab, const float* contact_imp,
                   int max_contacts, const int32_t* step_count, const double* time_passed) {
-  const int N = b->N;
   for (int e = 0; e < b->E; ++e) {
     fo_env* en = &b->envs[e];
-    for (int i = 0; i < N; ++i) {
-      size_t k = (size_t)e * N + i;
-      b2l_body_set_state(en->w, i, pos[2 * k], pos[2 * k + 1], angle[k], vel[2 * k], vel[2 * k + 1],
-                         sleep[k], fat + 4 * k);
-    }
+    fo_import_world(en->w, b->N, (size_t)e, pos, vel, angle, fat, sleep, contact_count, contact_ab, contact_imp,
+                    max_contacts);
     memcpy(en->targets, targets + (size_t)e * 2 * b->T, sizeof(float) * 2 * (size_t)b->T);
-    int n = contact_count[e];
-    int* ab = (int*)malloc(sizeof(int) * 2 * (size_t)(n ? n : 1));
-    int* pc = (int*)malloc(sizeof(int) * (size_t)(n ? n : 1));
-    for (int k = 0; k < n; ++k) {
-      uint32_t v = contact_ab[(size_t)e * max_contacts + k];
-      ab[2 * k] = (int)(v & 0xffffu);
-      ab[2 * k + 1] = (int)(v >> 16);
-      const float* im = contact_imp + 2 * ((size_t)e * max_contacts + k);
-      pc[k] = (im[0] != 0.0f || im[1] != 0.0f) ? 1 : 0;
-    }
-    b2l_world_load_contacts(en->w, n, ab, contact_imp + 2 * (size_t)e * max_contacts, pc);
-    free(ab);
-    free(pc);
     en->step_count = step_count[e];
     en->time_passed = time_passed[e];
     en->done = en->time_passed > b->cfg.time_limit;

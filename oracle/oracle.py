@@ -78,6 +78,19 @@ def lib():
         "b2l_world_clear_forces": (None, [c_void_p]),
         "b2l_world_contacts": (c_int, [c_void_p, P(c_int), c_int]),
         "b2l_world_contact_impulses": (c_int, [c_void_p, P(c_float), c_int]),
+        "b2l_body_set_active": (None, [c_void_p, c_int, c_int]),
+        "b2l_body_active": (c_int, [c_void_p, c_int]),
+        "b2l_world_raycast": (c_int, [c_void_p, c_float, c_float, c_float, c_float, P(c_float)]),
+        "to_create": (c_void_p, [c_void_p, c_int, c_uint64, c_int64]),
+        "to_free": (None, [c_void_p]),
+        "to_n_agents": (c_int, [c_void_p]),
+        "to_observe": (None, [c_void_p, P(c_double), P(c_uint8)]),
+        "to_step": (None, [c_void_p, c_void_p, P(c_double), P(c_uint8), P(c_double), P(c_uint8), P(c_uint8),
+                           P(c_int32), c_int]),
+        "to_get_extras": (None, [c_void_p, P(c_double), P(c_double), P(c_int32)]),
+        "to_world": (c_void_p, [c_void_p, c_int]),
+        "to_get_state": (None, [c_void_p] + [c_void_p] * 13 + [c_int] + [c_void_p] * 4),
+        "to_set_state": (None, [c_void_p] + [c_void_p] * 13 + [c_int] + [c_void_p] * 4),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -208,8 +221,110 @@ class B2World:
     def clear_forces(self):
         self.L.b2l_world_clear_forces(self.h)
 
+    def set_active(self, i, flag):
+        self.L.b2l_body_set_active(self.h, i, int(flag))
+
+    def active(self, i):
+        return self.L.b2l_body_active(self.h, i)
+
+    def raycast(self, x1, y1, x2, y2):
+        fr = c_float()
+        hit = self.L.b2l_world_raycast(self.h, x1, y1, x2, y2, ctypes.byref(fr))
+        return hit, fr.value
+
     def contacts(self):
         n = self.L.b2l_world_contacts(self.h, None, 0)
         out = (c_int * (3 * max(n, 1)))()
         self.L.b2l_world_contacts(self.h, out, n)
         return [(out[3 * k], out[3 * k + 1], out[3 * k + 2]) for k in range(n)]
+
+
+class OracleTDM:
+    """E reference TDM envs on the CPU (oracle/tdm_oracle.c); env e == TDM after
+    random.seed(seed + env_offset + e), with combat.py's missing names patched in."""
+
+    def __init__(self, cfg, n_envs: int, seed: int, env_offset: int = 0):
+        self.L = lib()
+        self.cfg = cfg
+        self.h = self.L.to_create(ctypes.addressof(cfg), n_envs, seed, env_offset)
+        if not self.h:
+            raise ValueError("to_create rejected the config")
+        self.E = n_envs
+        self.N = self.L.to_n_agents(self.h)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.L.to_free(h)
+            self.h = None
+
+    def _bufs(self):
+        E, N = self.E, self.N
+        return (np.zeros((E, N, N - 1, 4), np.float64), np.zeros((E, N, N - 1), np.uint8))
+
+    def observe(self):
+        obs, mask = self._bufs()
+        self.L.to_observe(self.h, _p(obs, c_double), _p(mask, c_uint8))
+        return obs, mask
+
+    def step(self, actions, n_threads=1):
+        E, N = self.E, self.N
+        a = np.ascontiguousarray(actions, np.uint8).reshape(E, N, 4)
+        obs, mask = self._bufs()
+        health = np.zeros((E, N), np.float64)
+        alive = np.zeros((E, N), np.uint8)
+        done = np.zeros((E,), np.uint8)
+        winner = np.zeros((E,), np.int32)
+        self.L.to_step(self.h, a.ctypes.data, _p(obs, c_double), _p(mask, c_uint8), _p(health, c_double),
+                       _p(alive, c_uint8), _p(done, c_uint8), _p(winner, c_int32), n_threads)
+        return dict(obs=obs, mask=mask, health=health, alive=alive, done=done, winner=winner)
+
+    def extras(self):
+        E, N = self.E, self.N
+        cd_atk = np.zeros((E, N), np.float64)
+        cd_mov = np.zeros((E, N), np.float64)
+        lis = np.zeros((E, 2), np.int32)
+        self.L.to_get_extras(self.h, _p(cd_atk, c_double), _p(cd_mov, c_double), _p(lis, c_int32))
+        return dict(cd_atk=cd_atk, cd_mov=cd_mov, listener=lis)
+
+    def state_buffers(self):
+        E, N = self.E, self.N
+        C = N * (N - 1) // 2
+        return dict(pos=np.zeros((E, N, 2), np.float32), vel=np.zeros((E, N, 2), np.float32),
+                    angle=np.zeros((E, N), np.float32), fat=np.zeros((E, N, 4), np.float32),
+                    sleep=np.zeros((E, N), np.float32), health=np.zeros((E, N), np.float64),
+                    cd_atk=np.zeros((E, N), np.float64), cd_mov=np.zeros((E, N), np.float64),
+                    alive=np.zeros((E, N), np.uint8), listener=np.zeros((E, 2), np.int32),
+                    contact_count=np.zeros((E,), np.int32), contact_ab=np.zeros((E, C), np.uint32),
+                    contact_imp=np.zeros((E, C, 2), np.float32), step_count=np.zeros((E,), np.int32),
+                    time_passed=np.zeros((E,), np.float64), done=np.zeros((E,), np.uint8),
+                    winner=np.zeros((E,), np.int32))
+
+    _ORDER = ("pos", "vel", "angle", "fat", "sleep", "health", "cd_atk", "cd_mov", "alive", "listener",
+              "contact_count", "contact_ab", "contact_imp")
+    _TAIL = ("step_count", "time_passed", "done", "winner")
+
+    def get_state(self):
+        """State in the macm_tdm_state layout (contact list capacity N(N-1)/2)."""
+        st = self.state_buffers()
+        C = self.N * (self.N - 1) // 2
+        self.L.to_get_state(self.h, *[st[k].ctypes.data for k in self._ORDER], C,
+                            *[st[k].ctypes.data for k in self._TAIL])
+        return st
+
+    def set_state(self, st):
+        C = self.N * (self.N - 1) // 2
+        ref = self.state_buffers()
+        arrs = {k: np.ascontiguousarray(st[k], ref[k].dtype).reshape(ref[k].shape) for k in ref}
+        self.L.to_set_state(self.h, *[arrs[k].ctypes.data for k in self._ORDER], C,
+                            *[arrs[k].ctypes.data for k in self._TAIL])
+
+    def bodies(self, e):
+        """[(x, y, angle, vx, vy, sleep, awake)] of env e."""
+        w = self.L.to_world(self.h, e)
+        buf = (c_float * 7)()
+        out = []
+        for i in range(self.N):
+            self.L.b2l_body_get(w, i, buf)
+            out.append(tuple(buf))
+        return np.array(out, np.float32)

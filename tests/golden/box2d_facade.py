@@ -38,6 +38,11 @@ class b2Vec2(object):
         o = o if isinstance(o, b2Vec2) else b2Vec2(o)
         return b2Vec2(f32(self.x - o.x), f32(self.y - o.y))
 
+    def __add__(self, o):
+        # pybox2d: b2Vec2 __add__(b2Vec2*) in C++, a tuple converted to float32 first
+        o = o if isinstance(o, b2Vec2) else b2Vec2(o)
+        return b2Vec2(f32(self.x + o.x), f32(self.y + o.y))
+
     def __getitem__(self, i):
         return float((self.x, self.y)[i])
 
@@ -175,6 +180,14 @@ class b2Body(object):
         s = self._w._core.body(self._i)
         return b2Vec2(s[3], s[4])
 
+    @property
+    def active(self):
+        return bool(self._w._core.active(self._i))
+
+    @active.setter
+    def active(self, flag):
+        self._w._core.set_active(self._i, bool(flag))
+
     def ApplyForce(self, force, point, wake):
         fx, fy = force
         p = point if isinstance(point, b2Vec2) else b2Vec2(point)
@@ -209,6 +222,17 @@ class b2World(object):
 
     def ClearForces(self):
         self._core.clear_forces()
+
+    def RayCast(self, callback, point1, point2):
+        """b2World::RayCast; the oracle returns the closest hit, which is the
+        fixture a fraction-returning callback ends on (cm_framework.py:56-86)."""
+        p1 = point1 if isinstance(point1, b2Vec2) else b2Vec2(point1)
+        p2 = point2 if isinstance(point2, b2Vec2) else b2Vec2(point2)
+        hit, fraction = self._core.raycast(float(p1.x), float(p1.y), float(p2.x), float(p2.y))
+        if hit >= 0:
+            fr = f32(fraction)
+            point = b2Vec2(f32(f32(f32(1.0) - fr) * p1.x + fr * p2.x), f32(f32(f32(1.0) - fr) * p1.y + fr * p2.y))
+            callback.ReportFixture(_Fixture(self._bodies[hit]), point, b2Vec2(0.0, 0.0), float(fr))
 
     @property
     def contacts(self):

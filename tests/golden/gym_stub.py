@@ -27,8 +27,11 @@ class Discrete(Space):
 
 
 class Box(Space):
-    def __init__(self, low, high, dtype=np.float32):
+    def __init__(self, low, high, shape=None, dtype=np.float32):
         self.dtype = np.dtype(dtype)
+        if shape is not None:  # gym 0.21: scalar bounds broadcast to `shape`
+            low = np.full(shape, low) if np.isscalar(low) else low
+            high = np.full(shape, high) if np.isscalar(high) else high
         self.low = np.asarray(low).astype(self.dtype)
         self.high = np.asarray(high).astype(self.dtype)
         self.shape = self.low.shape

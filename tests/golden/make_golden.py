@@ -46,6 +46,20 @@ SCENARIOS = [
          policy="bots"),
 ]
 
+# TDM (combat.py). Stepped until done or `steps`.
+TDM_SCENARIOS = [
+    dict(name="tdm_2x4_bots", seed=1, n_agents=[4, 4], steps=900, policy="combat"),
+    dict(name="tdm_2x8_random", seed=2, n_agents=[8, 8], steps=300, policy="random"),
+    dict(name="tdm_3x3_bots", seed=3, n_agents=[3, 3, 3], steps=900, policy="combat"),
+    dict(name="tdm_2x16_bots", seed=4, n_agents=[16, 16], steps=700, policy="combat"),
+    dict(name="tdm_1x2_4x1_mixed", seed=5, n_agents=[2, 1, 1, 1], steps=600, policy="combat"),
+]
+
+TDM_NOTE = ("combat.py as shipped cannot run: it never imports combatSettings (:65) and reads "
+            "self.cooldown_atk/.cooldown_mov_penalty/.time_limit (:150-151,:173) that are never set. "
+            "This script supplies exactly those four names from gym_macm.settings.combatSettings at run "
+            "time and changes nothing else.")
+
 
 def flatten_obs(obs, N):
     nbr = np.zeros(N, np.int32)
@@ -128,6 +142,104 @@ def run(sc):
     return out
 
 
+def tdm_slots(obs, agents, N):
+    """obs dict -> fixed slots [N, N-1, 4] (r, t, p, type) + mask; slot k of agent i is
+    agent j = k if k < i else k + 1 (the reference lists alive others in agent order)."""
+    o = np.zeros((N, N - 1, 4), np.float64)
+    m = np.zeros((N, N - 1), np.uint8)
+    for i, ag in enumerate(agents):
+        if ag.id not in obs:
+            assert not ag.alive
+            continue
+        others = [j for j in range(N) if j != i and agents[j].alive]
+        lst = obs[ag.id]["agents"]
+        assert len(lst) == len(others)
+        assert float(obs[ag.id]["myHealth"][0]) == ag.health and obs[ag.id]["myTeam"] == ag.team
+        for j, d in zip(others, lst):
+            k = j if j < i else j - 1
+            o[i, k, :3] = d["position"]
+            o[i, k, 3] = d["type"]
+            m[i, k] = 1
+    return o, m
+
+
+def run_tdm(sc):
+    import gym_macm.envs.combat as combat  # reference code
+    from gym_macm.settings import combatSettings
+    import bots
+
+    combat.combatSettings = combatSettings          # missing import (combat.py:65)
+    N = sum(sc["n_agents"])
+    rng = np.random.default_rng(2000 + sc["seed"])
+    recorded = {}
+    actors = None
+    if sc["policy"] == "combat":
+        def make_actor(i):
+            def actor(o):
+                a = bots.combat(o)
+                recorded[i] = np.asarray(a)
+                return a
+            return actor
+        actors, i = [], 0
+        for n in sc["n_agents"]:
+            actors.append([make_actor(i + j) for j in range(n)])
+            i += n
+    random.seed(sc["seed"])
+    env = combat.TDM(render=False, n_agents=list(sc["n_agents"]), actors=actors)
+    st = env.settings
+    env.cooldown_atk = st.cooldown_atk              # combat.py:150
+    env.cooldown_mov_penalty = st.cooldown_mov_penalty  # :151
+    env.time_limit = st.time_limit                  # :173
+    ag = env.agents
+    out = dict(team=np.array([a.team for a in ag], np.int32),
+               init_pos=np.array([[a.body.position.x, a.body.position.y] for a in ag], np.float32),
+               init_angle=np.array([np.float32(a.body.angle) for a in ag], np.float32))
+    out["init_obs"], out["init_mask"] = tdm_slots(env.obs, ag, N)
+    rec = {k: [] for k in ("actions", "obs", "mask", "health", "alive", "done", "winner", "pos", "angle",
+                           "cd_atk", "cd_mov", "time_passed", "listener")}
+    lst = env.framework.raycastListener
+    for t in range(sc["steps"]):
+        a = np.zeros((N, 4), np.uint8)
+        if sc["policy"] == "random":
+            r = np.concatenate([rng.integers(0, 3, size=(N, 3)), (rng.random((N, 1)) < 0.3)], axis=1)
+            actions = {x.id: r[i] for i, x in enumerate(ag) if x.alive}
+            for i, x in enumerate(ag):
+                if x.alive:
+                    a[i] = r[i]
+            env.step(actions)
+        else:
+            recorded.clear()
+            env.step()
+            for i, v in recorded.items():
+                a[i] = v
+        rec["actions"].append(a)
+        o, m = tdm_slots(env.obs, ag, N)
+        rec["obs"].append(o)
+        rec["mask"].append(m)
+        rec["health"].append(np.array([x.health for x in ag], np.float64))
+        rec["alive"].append(np.array([x.alive for x in ag], np.uint8))
+        rec["done"].append(bool(env.done))
+        rec["winner"].append(-1 if env.winner is None else int(env.winner))
+        rec["pos"].append(np.array([[x.body.position.x, x.body.position.y] for x in ag], np.float32))
+        rec["angle"].append(np.array([np.float32(x.body.angle) for x in ag], np.float32))
+        rec["cd_atk"].append(np.array([x.cooldown_atk for x in ag], np.float64))
+        rec["cd_mov"].append(np.array([x.cooldown_mov_penalty for x in ag], np.float64))
+        rec["time_passed"].append(env.time_passed)
+        hit_body = ag.index(lst.fixture.body.userData) if lst.fixture is not None else -1
+        rec["listener"].append(np.array([int(lst.hit), hit_body], np.int32))
+        if env.done:
+            break
+    for k, v in rec.items():
+        out[k] = np.array(v) if k in ("done", "winner", "time_passed") else np.stack(v)
+    meta = dict(name=sc["name"], seed=sc["seed"], n_agents=sc["n_agents"], N=N, steps=len(rec["done"]),
+                policy=sc["policy"], note=TDM_NOTE,
+                settings=dict(hz=st.hz, time_limit=st.time_limit, cooldown_atk=st.cooldown_atk,
+                              cooldown_mov_penalty=st.cooldown_mov_penalty, world_width=env.world_width,
+                              world_height=env.world_height))
+    out["meta"] = np.array(json.dumps(meta))
+    return out
+
+
 def main():
     gym_stub.install()
     box2d_facade.install()
@@ -142,6 +254,15 @@ def main():
         np.savez_compressed(path, **out)
         print(f"{sc['name']}: {os.path.getsize(path)} bytes, collisions={int((out['reward'] < 0).sum())}, "
               f"positive={int((out['reward'] > 0).sum())}, done_steps={int(out['done'].sum())}")
+    for sc in TDM_SCENARIOS:
+        if names and sc["name"] not in names:
+            continue
+        out = run_tdm(sc)
+        path = os.path.join(HERE, sc["name"] + ".npz")
+        np.savez_compressed(path, **out)
+        print(f"{sc['name']}: {os.path.getsize(path)} bytes, steps={len(out['done'])}, "
+              f"deaths={int((out['alive'][-1] == 0).sum())}, winner={int(out['winner'][-1])}, "
+              f"hits={int((np.diff(out['health'], axis=0) < 0).sum())}")
 
 
 if __name__ == "__main__":

@@ -11,8 +11,35 @@ from gym_macm.settings import flockSettings, to_config
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def names():
+def _all():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+def names():
+    """Flock goldens (mvmnt.py)."""
+    return [n for n in _all() if not n.startswith("tdm_")]
+
+
+def tdm_names():
+    """TDM goldens (combat.py)."""
+    return [n for n in _all() if n.startswith("tdm_")]
+
+
+def tdm_config(g, obs_f64=True):
+    from gym_macm._abi import tdm_config_from_defaults
+    m = g["meta"]
+    c = tdm_config_from_defaults()
+    sizes = m["n_agents"]
+    c.n_teams = len(sizes)
+    for t in range(4):
+        c.team_size[t] = sizes[t] if t < len(sizes) else 0
+    c.n_agents = sum(sizes)
+    c.obs_f64 = 1 if obs_f64 else 0
+    st = m["settings"]
+    assert (st["hz"], st["time_limit"], st["cooldown_atk"], st["cooldown_mov_penalty"]) == (
+        c.hz, c.time_limit, c.cooldown_atk, c.cooldown_mov_penalty)
+    assert (st["world_width"], st["world_height"]) == (c.world_width, c.world_height)
+    return c
 
 
 def load(name):

@@ -40,3 +40,24 @@ def f32_obs_mismatch(gpu_obs, oracle_obs64):
 
 def oracle_for(cfg, tidx, E, seed, env_offset=0):
     return OracleFlock(cfg, tidx, E, seed, env_offset)
+
+
+def combat_bot(obs, mask):
+    """The reference's scripted TDM actor (test_scripts/bots.py:3-16), vectorised over
+    the fixed-slot obs [E, N, N-1, 4] (r, t, p, is_ally) + mask: attack the closest
+    enemy (first minimal r in list order), turning toward it, walking forward when
+    it is within pi/5, attacking when r < 3; idle without enemies. Rows of dead
+    agents are idle (they are not stepped)."""
+    E, N = obs.shape[0], obs.shape[1]
+    enemy = mask.astype(bool) & (obs[..., 3] == 0)
+    r = np.where(enemy, obs[..., 0], np.inf)
+    k = np.argmin(r, axis=-1)  # first index of the minimum == strict '<' scan
+    has = enemy.any(axis=-1)
+    sel = np.take_along_axis(obs, k[..., None, None].repeat(4, -1), axis=2)[..., 0, :]
+    a = np.ones((E, N, 4), np.uint8)
+    a[..., 3] = 0
+    t = sel[..., 1]
+    a[..., 0] = np.where(has, (np.abs(t) < np.pi / 5).astype(np.uint8) + 1, 1)
+    a[..., 2] = np.where(has, (np.sign(t) + 1).astype(np.uint8), 1)
+    a[..., 3] = np.where(has, (sel[..., 0] < 3).astype(np.uint8), 0)
+    return a

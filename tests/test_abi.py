@@ -36,11 +36,28 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_abi.MacmOutputs) == 5 * 8
     assert ctypes.sizeof(_abi.MacmState) == 11 * 8
     assert ctypes.sizeof(_abi.MacmWorldInfo) == 8 * 4
+    assert ctypes.sizeof(_abi.MacmTdmConfig) == 12 * 4 + 12 * 8 + 4 * 4
+    assert ctypes.sizeof(_abi.MacmTdmOutputs) == 6 * 8
+    assert ctypes.sizeof(_abi.MacmTdmState) == 17 * 8
+
+
+def test_tdm_defaults_match_python_mirror():
+    L = _abi.lib()
+    c = _abi.MacmTdmConfig()
+    assert L.macm_tdm_config_default(ctypes.byref(c)) == 0
+    assert bytes(c) == bytes(_abi.tdm_config_from_defaults())
+    c.team_size[0] = 40
+    c.team_size[1] = 40
+    c.n_agents = 80
+    h = ctypes.c_void_p()
+    assert L.macm_tdm_create(ctypes.byref(c), 4, 0, ctypes.byref(h)) == -4
+    c.n_agents = 79
+    assert L.macm_tdm_create(ctypes.byref(c), 4, 0, ctypes.byref(h)) == -1
 
 
 def test_version_and_defaults_without_gpu():
     L = _abi.lib()
-    assert L.macm_abi_version() == 1
+    assert L.macm_abi_version() == 2
     assert b"gfx950" in L.macm_version()
     c = _abi.MacmConfig()
     assert L.macm_config_default(ctypes.byref(c)) == 0

@@ -22,4 +22,11 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
 stop_if_crash $? rocprof
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python bench.py --env tdm --steps 300 --warmup 30 > "$OUT/bench_tdm.json" 2> "$OUT/bench_tdm.err"
+stop_if_crash $? bench_tdm
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof_tdm" -o run -- \
+  python3 "$GRAFT_REPO_ROOT/bench.py" --env tdm --steps 200 --warmup 20 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof_tdm_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof_tdm.err"
+stop_if_crash $? rocprof_tdm
 echo ALLDONE | tee -a "$GRAFT_REPO_ROOT/$OUT/status.txt"

@@ -2,6 +2,8 @@
 that bench.py reads for `roofline.traffic`.
 
     python tools/pmc_summary.py gpurun_out/<dir> --envs 4096 --agents 64 -o profiles/pmc_flock_step.json
+    python tools/pmc_summary.py gpurun_out/<dir> --kernel "env_step_w64<1, float>" --agents 32 \
+        -o profiles/pmc_tdm_step.json
 
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE
 and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
@@ -28,7 +30,7 @@ def kernel_means(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="flock_step_w64<float>")
+    ap.add_argument("--kernel", default="env_step_w64<0, float>")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--agents", type=int, default=64)
     ap.add_argument("-o", "--out", default="")
