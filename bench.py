@@ -37,13 +37,14 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_agents, seed, budget_s=15.0):
-    """Time the CPU oracle on this host (OpenMP over envs) on a bounded sample."""
+def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096):
+    """Time the CPU oracle on this host (OpenMP over envs) on a bounded sample of the
+    same workload: the same E envs x N agents, as many steps as fit the budget."""
     from oracle import OracleFlock
     from gym_macm.settings import flockSettings, to_config
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    E = max(4 * threads, 64)
+    E = n_envs
     cfg = to_config(flockSettings(), n_agents, 1, obs_f64=True)
     orc = OracleFlock(cfg, None, E, seed)
     rng = np.random.default_rng(seed + 1)
@@ -54,7 +55,7 @@ def cpu_baseline(n_agents, seed, budget_s=15.0):
     for a in pre[:3]:
         orc.step_raw(a, bufs, threads)
     per_step = (time.perf_counter() - t0) / 3
-    steps = int(max(10, min(3000, budget_s / max(per_step, 1e-6))))
+    steps = int(max(5, budget_s / max(per_step, 1e-6)))
     acts = [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(16)]
     t0 = time.perf_counter()
     for s in range(steps):
@@ -73,13 +74,14 @@ def b_alg_tdm(n_agents):
     return 80 + 4 + 50 + (n_agents - 1) * 16 + (n_agents - 1) + 9
 
 
-def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0):
-    """Time the CPU TDM oracle (oracle/tdm_oracle.c, OpenMP over envs) on a bounded sample."""
+def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0, n_envs=4096):
+    """Time the CPU TDM oracle (oracle/tdm_oracle.c, OpenMP over envs) on a bounded
+    sample of the same workload (same E envs, as many steps as fit the budget)."""
     from oracle import OracleTDM
     from gym_macm.tdm_world import tdm_config
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    E = max(4 * threads, 64)
+    E = n_envs
     N = sum(team_sizes)
     orc = OracleTDM(tdm_config(team_sizes, obs_f64=True), E, seed)
     rng = np.random.default_rng(seed + 1)
@@ -88,7 +90,7 @@ def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0):
     for a in acts[:3]:
         orc.step(a, threads)
     per_step = (time.perf_counter() - t0) / 3
-    steps = int(max(10, min(3000, budget_s / max(per_step, 1e-6))))
+    steps = int(max(5, budget_s / max(per_step, 1e-6)))
     t0 = time.perf_counter()
     for s in range(steps):
         orc.step(acts[s % 16], threads)
@@ -259,9 +261,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
             if args.env == "flock":
-                out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget)
+                out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget, E)
             else:
-                out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget)
+                out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget, E)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

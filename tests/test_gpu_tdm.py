@@ -49,13 +49,21 @@ def random_actions(rng, E, N, p_attack=0.5):
     return a
 
 
+def check_obs(w, o_obs, o_mask, ctx):
+    if w.cfg.obs_f64:
+        for e in range(w.E):
+            assert tdm_obs_close(w.obs[e].cpu().numpy(), o_obs[e], o_mask[e]), f"obs {ctx} env {e}"
+    else:
+        f32_obs_mismatch(w.obs.cpu().numpy(), o_obs)
+
+
 def check_rollout(w, orc, steps, policy, state_every=1):
     E, N = w.E, w.N
     assert_tdm_state_equal(w.get_state(), orc.get_state(), "reset")
     w.observe()
     o_obs, o_mask = orc.observe()
     np.testing.assert_array_equal(w.mask.cpu().numpy(), o_mask)
-    f32_obs_mismatch(w.obs.cpu().numpy(), o_obs)
+    check_obs(w, o_obs, o_mask, "reset")
     for t in range(steps):
         a = policy(o_obs, o_mask)
         w.step(torch.from_numpy(a).cuda())
@@ -66,11 +74,7 @@ def check_rollout(w, orc, steps, policy, state_every=1):
         np.testing.assert_array_equal(w.done.cpu().numpy(), r["done"], err_msg=f"done step {t}")
         np.testing.assert_array_equal(w.winner.cpu().numpy(), r["winner"], err_msg=f"winner step {t}")
         np.testing.assert_array_equal(w.mask.cpu().numpy(), r["mask"], err_msg=f"mask step {t}")
-        if w.cfg.obs_f64:
-            for e in range(E):
-                assert tdm_obs_close(w.obs[e].cpu().numpy(), r["obs"][e], r["mask"][e]), f"obs step {t} env {e}"
-        else:
-            f32_obs_mismatch(w.obs.cpu().numpy(), r["obs"])
+        check_obs(w, r["obs"], r["mask"], f"step {t}")
         if (t + 1) % state_every == 0 or t == steps - 1:
             assert_tdm_state_equal(w.get_state(), orc.get_state(), f"step {t}")
     assert w.status() == 0
