@@ -122,3 +122,57 @@ def to_config(s: fwSettings, n_agents: int, n_targets: int, obs_f64: bool = Fals
     c.friction = float(getattr(fx, "friction", 0.3))
     c.linear_damping = float(s.bodySettings.get("linearDamping", 0.0))
     return c
+
+
+class combatSettings(fwSettings):
+    """reference settings.py:149-177. The reference ignores kwargs here; like
+    flockSettings they are applied."""
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        self.render = False
+        self.record = False
+        self.record_dir = "../imgs/"
+        self.verbose_display = True
+        self.start_spread = 20
+        self.start_point = [0, 0]
+        self.agent_rotation_speed = 0.8 * (2 * np.pi)
+        self.agent_force = 20
+        self.time_limit = 60
+        self.cooldown_atk = 1
+        self.cooldown_mov_penalty = 0.5
+        self.bodySettings = {"fixtures": CircleFixture(0.5, 1, 0.3), "linearDamping": 5,
+                             "fixedRotation": True}
+        for kw in kwargs:
+            setattr(self, kw, kwargs[kw])
+
+
+def to_tdm_config(s: combatSettings, n_agents, obs_f64=False, fresh_raycast=False, decay_mov_penalty=False,
+                  world_width=30.0, world_height=30.0):
+    """Flatten combatSettings + TDM/Agent constants (combat.py:13-29,76-77) into macm_tdm_config."""
+    sizes = [int(n) for n in n_agents]
+    if not 1 <= len(sizes) <= 4:
+        raise ValueError("TDM supports 1 to 4 teams")
+    c = _abi.tdm_config_from_defaults()
+    c.n_teams = len(sizes)
+    for t in range(4):
+        c.team_size[t] = sizes[t] if t < len(sizes) else 0
+    c.n_agents = sum(sizes)
+    c.velocity_iterations = int(s.velocityIterations)
+    c.position_iterations = int(s.positionIterations)
+    c.warm_starting = 1 if s.enableWarmStarting else 0
+    c.obs_f64 = 1 if obs_f64 else 0
+    c.fresh_raycast = 1 if fresh_raycast else 0
+    c.decay_mov_penalty = 1 if decay_mov_penalty else 0
+    c.hz = float(s.hz)
+    c.world_width = float(world_width)
+    c.world_height = float(world_height)
+    c.agent_rotation_speed = float(s.agent_rotation_speed)
+    c.agent_force = float(s.agent_force)
+    c.time_limit = float(s.time_limit)
+    c.cooldown_atk = float(s.cooldown_atk)
+    c.cooldown_mov_penalty = float(s.cooldown_mov_penalty)
+    fx = s.bodySettings["fixtures"]
+    c.radius, c.density, c.friction = float(fx.radius), float(fx.density), float(fx.friction)
+    c.linear_damping = float(s.bodySettings["linearDamping"])
+    return c

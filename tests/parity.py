@@ -61,3 +61,19 @@ def combat_bot(obs, mask):
     a[..., 2] = np.where(has, (np.sign(t) + 1).astype(np.uint8), 1)
     a[..., 3] = np.where(has, (sel[..., 0] < 3).astype(np.uint8), 0)
     return a
+
+
+def combat_bot_dict(obs):
+    """bots.combat (test_scripts/bots.py:3-16) on one agent's reference-format obs
+    dict, for driving the drop-in TDM through its `actors` hook."""
+    enemies = [a for a in obs["agents"] if a["type"] == 0]
+    if not enemies:
+        return np.array([1, 1, 1, 0])
+    closest = enemies[0]
+    for a in enemies:
+        if a["position"][0] < closest["position"][0]:
+            closest = a
+    rotation = np.sign(closest["position"][1]) + 1
+    forward = int(np.abs(closest["position"][1]) < (np.pi / 5)) + 1
+    attack = int(closest["position"][0] < 3)
+    return np.array([forward, 1, rotation, attack])

@@ -169,3 +169,56 @@ def test_tdm_counters_and_latching_done():
     c = w.counters()
     assert c[1] == attacks and c[2] == deaths and deaths > 0
     assert (w.winner.cpu().numpy() >= 0).sum() > 0
+
+
+def _slots(obs, env):
+    """Reference-format obs dict -> fixed slots (as tests/golden/make_golden.tdm_slots)."""
+    N = len(env.agents)
+    o = np.zeros((N, N - 1, 4))
+    m = np.zeros((N, N - 1), np.uint8)
+    for i, ag in enumerate(env.agents):
+        if ag.id not in obs:
+            continue
+        others = [j for j in range(N) if j != i and env.agents[j].alive]
+        for j, d in zip(others, obs[ag.id]["agents"]):
+            k = j if j < i else j - 1
+            o[i, k, :3] = d["position"]
+            o[i, k, 3] = d["type"]
+            m[i, k] = 1
+    return o, m
+
+
+@pytest.mark.parametrize("name", goldens.tdm_names())
+def test_dropin_tdm_matches_reference_goldens(name):
+    """The drop-in dict API (gym_macm.envs.TDM over the HIP world) reproduces the
+    reference env's own rollouts: random.seed -> spawn, actor hook or action dicts,
+    obs dicts, health, deaths, done and winner."""
+    import random
+    from gym_macm.envs import TDM
+    from parity import combat_bot_dict
+    g = goldens.load(name)
+    m = g["meta"]
+    random.seed(m["seed"])
+    actors = None
+    if m["policy"] == "combat":
+        actors = [[combat_bot_dict] * n for n in m["n_agents"]]
+    env = TDM(render=False, n_agents=m["n_agents"], actors=actors, device="cuda:0")
+    o, msk = _slots(env.obs, env)
+    np.testing.assert_array_equal(msk, g["init_mask"])
+    assert tdm_obs_close(o, g["init_obs"], g["init_mask"])
+    for t in range(m["steps"]):
+        if actors is None:
+            acts = {ag.id: g["actions"][t][k].astype(np.int64) for k, ag in enumerate(env.agents) if ag.alive}
+            obs = env.step(acts)
+        else:
+            obs = env.step()
+        o, msk = _slots(obs, env)
+        np.testing.assert_array_equal(msk, g["mask"][t], err_msg=f"mask step {t}")
+        assert tdm_obs_close(o, g["obs"][t], g["mask"][t]), f"obs step {t}"
+        np.testing.assert_array_equal([ag.health for ag in env.agents], g["health"][t], err_msg=f"health {t}")
+        assert [ag.alive for ag in env.agents] == list(g["alive"][t].astype(bool)), f"alive step {t}"
+        assert env.done == bool(g["done"][t]), f"done step {t}"
+        assert (env.winner if env.winner is not None else -1) == int(g["winner"][t]), f"winner step {t}"
+        assert env.time_passed == g["time_passed"][t]
+        assert sorted(obs) == sorted(ag.id for ag in env.agents if ag.alive)
+    assert sum(env.n_alive) == int(g["alive"][-1].sum())
