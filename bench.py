@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--env", choices=("flock", "tdm"), default="flock",
                     help="flock: cm-flock-v0 (the metric); tdm: cm-tdm-v0 (config 4, --teams)")
     ap.add_argument("--teams", default="16,16", help="TDM team sizes (config 4: 16,16)")
+    ap.add_argument("--policy", choices=("random", "bots"), default="random",
+                    help="random: pre-generated uniform actions (the metric); bots: closed loop with the "
+                         "device bots.flock / bots.combat kernels inside the timed region")
     ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
     if args.traffic_json is None:
@@ -173,6 +176,22 @@ def main():
     sh = stream.cuda_stream
     step = world_h.step_raw
     base = acts.data_ptr()
+    if args.policy == "bots":
+        # closed loop: every step reads the actions the previous step's bot kernel wrote
+        from gym_macm import bots
+        a_loop = acts[0].clone()
+        if args.env == "flock":
+            def policy():
+                bots.flock_actions(world_h.obs, out=a_loop)
+        else:
+            def policy():
+                bots.combat_actions(world_h.obs, world_h.mask, out=a_loop)
+        loop_ptr = a_loop.data_ptr()
+        policy()
+
+        def step(_ptr, sh_):  # noqa: F811
+            world_h.step_raw(loop_ptr, sh_)
+            policy()
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}")
     for w in range(W):
         step(base + w * stride, sh)
@@ -220,13 +239,16 @@ def main():
             metric = json.load(f)["metric"]
         if args.env == "tdm":
             metric = "agent·steps/sec, cm-tdm-v0 (config 4)"
-            workload = (f"cm-tdm-v0 n_agents={teams} x {E} envs per GPU, uniform random actions "
-                        f"(MultiDiscrete[3,3,3,2]) pre-generated on device, from reset (seed {args.seed:#x}); "
-                        f"agent-steps count every agent slot")
+            workload = (f"cm-tdm-v0 n_agents={teams} x {E} envs per GPU, " + (
+                "uniform random actions (MultiDiscrete[3,3,3,2]) pre-generated on device" if args.policy == "random"
+                else "closed loop with the device bots.combat kernel (timed)") +
+                f", from reset (seed {args.seed:#x}); agent-steps count every agent slot")
         else:
             workload = (f"cm-flock-v0 n_agents=[{N}]{f' targets=i//{N // args.flocks}' if args.flocks > 1 else ''} "
-                        f"x {E} envs per GPU, uniform random discrete actions "
-                        f"(MultiDiscrete[3,3,3]) pre-generated on device, from reset (seed {args.seed:#x})")
+                        f"x {E} envs per GPU, " + (
+                            "uniform random discrete actions (MultiDiscrete[3,3,3]) pre-generated on device"
+                            if args.policy == "random" else "closed loop with the device bots.flock kernel (timed)") +
+                        f", from reset (seed {args.seed:#x})")
         out = {
             "metric": metric,
             "value": value,

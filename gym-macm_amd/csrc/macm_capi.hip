@@ -35,6 +35,9 @@ hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const
                                const TdmBuffers& TB, int cur, void* obs, bool obs_f64, hipStream_t s);
 hipError_t launch_tdm_observe_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s);
+hipError_t launch_bots_flock(const void* obs, bool obs_f64, int od, long long rows, uint8_t* act, hipStream_t s);
+hipError_t launch_bots_combat(const void* obs, const uint8_t* mask, bool obs_f64, int N, long long rows,
+                              uint8_t* act, hipStream_t s);
 hipError_t wg_configure(int N, int tcap);
 int wg_block(int N);
 int wg_lds_bytes(int N, int tcap);
@@ -763,6 +766,24 @@ int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream) {
   unsigned long long acc[4] = {0, 0, 0, 0};
   for (size_t i = 0; i < h.size(); ++i) acc[i & 3] += h[i];
   for (int i = 0; i < 4; ++i) out[i] = (int64_t)acc[i];
+  return MACM_OK;
+}
+
+// ============================ scripted actors ===============================
+
+int macm_bots_flock(const void* obs, int32_t obs_f64, int32_t obs_dim, int64_t rows, uint8_t* actions,
+                    void* stream) {
+  if (!obs || !actions || rows < 0) return fail(MACM_E_INVALID, "obs/actions NULL or rows < 0");
+  if (obs_dim != 4 && obs_dim != 6) return fail(MACM_E_INVALID, "obs_dim must be 4 (polar) or 6 (cartesian)");
+  HIP_TRY(launch_bots_flock(obs, obs_f64 != 0, obs_dim, rows, actions, (hipStream_t)stream));
+  return MACM_OK;
+}
+
+int macm_bots_combat(const void* obs, const uint8_t* mask, int32_t obs_f64, int32_t n_agents, int64_t rows,
+                     uint8_t* actions, void* stream) {
+  if (!obs || !mask || !actions || rows < 0) return fail(MACM_E_INVALID, "obs/mask/actions NULL or rows < 0");
+  if (n_agents < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2");
+  HIP_TRY(launch_bots_combat(obs, mask, obs_f64 != 0, n_agents, rows, actions, (hipStream_t)stream));
   return MACM_OK;
 }
 

@@ -331,6 +331,22 @@ int macm_tdm_status(macm_tdm* w, int32_t* status_or, void* stream);
 /* out[0] alive agent-steps, out[1] melee attacks, out[2] deaths, out[3] env-steps with done. */
 int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream);
 
+/* ---- scripted actors on the device (test_scripts/bots.py) ------------------
+ * Read an observation tensor written by a step and write the next actions, so a
+ * closed-loop rollout stays in HBM. Device pointers; asynchronous on `stream`.
+ * With float64 obs the decisions equal the reference bots' on the same obs.
+ */
+
+/* bots.flock (bots.py:37-61) on Flock obs [rows, obs_dim] (4 polar, 6 cartesian);
+ * actions [rows, 3] uint8. rows = E * N. */
+int macm_bots_flock(const void* obs, int32_t obs_f64, int32_t obs_dim, int64_t rows, uint8_t* actions,
+                    void* stream);
+
+/* bots.combat (bots.py:3-16) on TDM obs [rows, N-1, 4] + mask [rows, N-1];
+ * actions [rows, 4] uint8 (rows of dead agents get the idle action). rows = E * N. */
+int macm_bots_combat(const void* obs, const uint8_t* mask, int32_t obs_f64, int32_t n_agents, int64_t rows,
+                     uint8_t* actions, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

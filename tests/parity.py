@@ -77,3 +77,23 @@ def combat_bot_dict(obs):
     forward = int(np.abs(closest["position"][1]) < (np.pi / 5)) + 1
     attack = int(closest["position"][0] < 3)
     return np.array([forward, 1, rotation, attack])
+
+
+def flock_bot(obs):
+    """bots.flock (test_scripts/bots.py:37-61), vectorised over Flock obs [..., 4|6]:
+    idle within r < 1 of the target, else turn toward it (sign(t) + 1) and walk
+    forward when |t| < pi/4 (cartesian: sign(sin t) + 1, forward when cos t > cos(pi/4))."""
+    od = obs.shape[-1]
+    h = od // 2
+    r = obs[..., h]
+    a = np.ones(obs.shape[:-1] + (3,), np.uint8)
+    if od == 6:
+        rot = np.sign(obs[..., h + 2]) + 1
+        fwd = (obs[..., h + 1] > np.cos(np.pi / 4)).astype(np.uint8) + 1
+    else:
+        rot = np.sign(obs[..., h + 1]) + 1
+        fwd = (np.abs(obs[..., h + 1]) < (np.pi / 4)).astype(np.uint8) + 1
+    far = ~(r < 1)
+    a[..., 0] = np.where(far, fwd, 1)
+    a[..., 2] = np.where(far, rot.astype(np.uint8), 1)
+    return a

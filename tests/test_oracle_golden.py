@@ -52,3 +52,18 @@ def test_golden_obs_f32_exact():
             bad += int((a != b).sum())
             total += a.size
     assert bad <= total * 1e-5, (bad, total)
+
+
+def test_vectorised_flock_bot_matches_recorded_reference_actions():
+    """tests/parity.flock_bot (the model of the device bots.flock kernel) reproduces
+    every action the reference's bots.flock chose in the goldens."""
+    from parity import flock_bot
+    n = 0
+    for name in goldens.names():
+        g = goldens.load(name)
+        if g["meta"]["policy"] != "bots":
+            continue
+        obs = np.concatenate([g["init_obs"][None], g["obs"][:-1]])
+        np.testing.assert_array_equal(flock_bot(obs), g["actions"], err_msg=name)
+        n += g["actions"].shape[0] * g["actions"].shape[1]
+    assert n > 5000
