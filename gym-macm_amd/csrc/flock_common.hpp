@@ -105,4 +105,15 @@ __host__ __device__ inline int tdm_team_of(const TdmParams& T, int i) {
   return t;
 }
 
+// Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).
+constexpr int kMtStride = 640;  // words per env: 624 state words, [624] = position
+
+struct PoseDraw {
+  int mode;  // kFlock / kTdm
+  int n_agents;
+  double spread, start_x, start_y;  // Flock (flockSettings start_spread / start_point)
+  double half_width, height;        // TDM (world_width / 2, world_height)
+  TdmParams TP;                     // TDM team boundaries
+};
+
 }  // namespace macm

@@ -982,8 +982,10 @@ __global__ __launch_bounds__(W) void env_step_w64(StepParams P, WorldBuffers B, 
 // and the initial observation (Flock.obs, mvmnt.py:79).
 template <typename OT>
 __global__ __launch_bounds__(W) void flock_init_w64(StepParams P, WorldBuffers B, int cur,
-                                                    OT* __restrict__ obs, int32_t* __restrict__ nbr_out) {
+                                                    OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
+                                                    const uint8_t* __restrict__ mask) {
   const int e = blockIdx.x;
+  if (mask && !mask[e]) return;  // reset_envs: only the masked envs
   const int lane = threadIdx.x;
   const int N = P.n_agents;
   const int C = P.max_contacts;
@@ -1082,8 +1084,9 @@ __global__ __launch_bounds__(W) void flock_observe_w64(StepParams P, WorldBuffer
 // the initial observation (self.obs = self.get_obs(), combat.py:102).
 template <typename OT>
 __global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
-                                                  int cur, OT* __restrict__ obs) {
+                                                  int cur, OT* __restrict__ obs, const uint8_t* __restrict__ mask) {
   const int e = blockIdx.x;
+  if (mask && !mask[e]) return;  // reset_envs: only the masked envs
   const int lane = threadIdx.x;
   const int N = P.n_agents;
   const int C = P.max_contacts;
@@ -1194,12 +1197,13 @@ hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const
 }
 
 hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
-                               const TdmBuffers& TB, int cur, void* obs, bool obs_f64, hipStream_t s) {
+                               const TdmBuffers& TB, int cur, void* obs, bool obs_f64, const uint8_t* mask,
+                               hipStream_t s) {
   dim3 grid(P.n_envs), block(W);
   if (obs_f64)
-    hipLaunchKernelGGL(tdm_init_w64<double>, grid, block, 0, s, P, B, TP, TB, cur, (double*)obs);
+    hipLaunchKernelGGL(tdm_init_w64<double>, grid, block, 0, s, P, B, TP, TB, cur, (double*)obs, mask);
   else
-    hipLaunchKernelGGL(tdm_init_w64<float>, grid, block, 0, s, P, B, TP, TB, cur, (float*)obs);
+    hipLaunchKernelGGL(tdm_init_w64<float>, grid, block, 0, s, P, B, TP, TB, cur, (float*)obs, mask);
   return hipGetLastError();
 }
 
@@ -1214,12 +1218,12 @@ hipError_t launch_tdm_observe_w64(const StepParams& P, const WorldBuffers& B, co
 }
 
 hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
-                           int32_t* nbr, hipStream_t s) {
+                           int32_t* nbr, const uint8_t* mask, hipStream_t s) {
   dim3 grid(P.n_envs), block(W);
   if (obs_f64)
-    hipLaunchKernelGGL(flock_init_w64<double>, grid, block, 0, s, P, B, cur, (double*)obs, nbr);
+    hipLaunchKernelGGL(flock_init_w64<double>, grid, block, 0, s, P, B, cur, (double*)obs, nbr, mask);
   else
-    hipLaunchKernelGGL(flock_init_w64<float>, grid, block, 0, s, P, B, cur, (float*)obs, nbr);
+    hipLaunchKernelGGL(flock_init_w64<float>, grid, block, 0, s, P, B, cur, (float*)obs, nbr, mask);
   return hipGetLastError();
 }
 

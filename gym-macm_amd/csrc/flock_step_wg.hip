@@ -699,10 +699,12 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
 // overlapping pairs, descending), zeroed dynamics, initial observation.
 template <typename OT>
 __global__ __launch_bounds__(1024) void flock_init_wg(StepParams P, WorldBuffers B, int cur, OT* __restrict__ obs,
-                                                      int32_t* __restrict__ nbr_out) {
+                                                      int32_t* __restrict__ nbr_out,
+                                                      const uint8_t* __restrict__ mask) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
   const int e = blockIdx.x, tid = threadIdx.x, N = P.n_agents, C = P.max_contacts;
+  if (mask && !mask[e]) return;  // reset_envs: only the masked envs (mask is not written here)
   const bool act = tid < N;
   const size_t ag = (size_t)e * N + tid;
   Rec* s_rec = (Rec*)lds;
@@ -841,14 +843,14 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   return hipGetLastError();
 }
 
-hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr,
+hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr, const uint8_t* mask,
                           hipStream_t s) {
   const int lds = wg_init_lds_bytes(P.n_agents);
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
   if (obs_f64)
-    hipLaunchKernelGGL(flock_init_wg<double>, grid, block, lds, s, P, B, cur, (double*)obs, nbr);
+    hipLaunchKernelGGL(flock_init_wg<double>, grid, block, lds, s, P, B, cur, (double*)obs, nbr, mask);
   else
-    hipLaunchKernelGGL(flock_init_wg<float>, grid, block, lds, s, P, B, cur, (float*)obs, nbr);
+    hipLaunchKernelGGL(flock_init_wg<float>, grid, block, lds, s, P, B, cur, (float*)obs, nbr, mask);
   return hipGetLastError();
 }
 

@@ -18,21 +18,24 @@ namespace macm {
 hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                            bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
 hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
-                           int32_t* nbr, hipStream_t s);
+                           int32_t* nbr, const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
                               hipStream_t s);
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
                           hipStream_t s);
 hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr,
-                          hipStream_t s);
+                          const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_wg(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
                              hipStream_t s);
 hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
                                uint8_t* done, hipStream_t s);
 hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
-                               const TdmBuffers& TB, int cur, void* obs, bool obs_f64, hipStream_t s);
+                               const TdmBuffers& TB, int cur, void* obs, bool obs_f64, const uint8_t* mask,
+                               hipStream_t s);
+hipError_t launch_draw_poses(const uint8_t* mask, uint32_t* mt, const PoseDraw& D, int n_envs, float2* pos,
+                             float* angle, hipStream_t s);
 hipError_t launch_tdm_observe_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s);
 hipError_t launch_bots_flock(const void* obs, bool obs_f64, int od, long long rows, uint8_t* act, hipStream_t s);
@@ -55,6 +58,9 @@ struct macm_world {
   int tcap;   // touching-contact capacity per env
   std::vector<int32_t> tidx;
   std::vector<void*> allocs;
+  uint32_t* mt = nullptr;     // [E][kMtStride] per-env MT19937 streams (valid after reset)
+  uint8_t* rmask = nullptr;   // [E] reset mask scratch
+  bool mt_valid = false;
 };
 
 struct macm_tdm {
@@ -67,6 +73,9 @@ struct macm_tdm {
   int device;
   std::vector<int> team;  // agent -> team
   std::vector<void*> allocs;
+  uint32_t* mt = nullptr;
+  uint8_t* rmask = nullptr;
+  bool mt_valid = false;
 };
 
 static thread_local std::string g_last_error;
@@ -143,11 +152,18 @@ void free_world(macm_world* w) {
   w->allocs.clear();
 }
 
-hipError_t launch_init(macm_world* w, const macm_outputs* out, hipStream_t s) {
+hipError_t launch_init(macm_world* w, const macm_outputs* out, const uint8_t* mask, hipStream_t s) {
   void* obs = out ? out->obs : nullptr;
   int32_t* nbr = out ? out->nbr_id : nullptr;
-  if (w->wave) return launch_init_w64(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, s);
-  return launch_init_wg(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, s);
+  if (w->wave) return launch_init_w64(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, mask, s);
+  return launch_init_wg(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, mask, s);
+}
+
+// Host generator state -> the env's slot of the device stream buffer.
+void save_stream(std::vector<uint32_t>& host, int e, const PyMT19937& r) {
+  uint32_t* d = host.data() + (size_t)e * kMtStride;
+  memcpy(d, r.state(), sizeof(uint32_t) * PyMT19937::kWords);
+  d[PyMT19937::kWords] = (uint32_t)r.index();
 }
 
 }  // namespace
@@ -270,7 +286,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
 #ifdef MACM_STAMPS
       || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 16))
 #endif
-      || (!w->wave && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap)))
+      || (!w->wave && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap))) ||
+      (rc = dalloc(w, &w->mt, (size_t)n_envs * kMtStride)) || (rc = dalloc(w, &w->rmask, (size_t)n_envs))
   ) {
     free_world(w);
     delete w;
@@ -328,6 +345,7 @@ int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const mac
   const int E = w->P.n_envs, N = w->P.n_agents, T = w->P.n_targets;
   std::vector<float2> pos((size_t)E * N), tg((size_t)E * T);
   std::vector<float> ang((size_t)E * N);
+  std::vector<uint32_t> mts((size_t)E * kMtStride);
   for (int e = 0; e < E; ++e) {
     PyMT19937 r(seed + (uint64_t)(env_offset + e));
     for (int t = 0; t < T; ++t) {  // mvmnt.py:46-52
@@ -342,13 +360,16 @@ int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const mac
       pos[(size_t)e * N + i] = make_float2((float)x, (float)y);
       ang[(size_t)e * N + i] = (float)a;
     }
+    save_stream(mts, e, r);
   }
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemcpyAsync(w->B.pos, pos.data(), pos.size() * sizeof(float2), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w->B.angle, ang.data(), ang.size() * sizeof(float), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w->B.targets, tg.data(), tg.size() * sizeof(float2), hipMemcpyHostToDevice, s));
   w->cur = 0;
-  HIP_TRY(launch_init(w, out, s));
+  HIP_TRY(hipMemcpyAsync(w->mt, mts.data(), mts.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  w->mt_valid = true;
+  HIP_TRY(launch_init(w, out, nullptr, s));
   // host vectors are read by the async copies: wait before they go out of scope
   HIP_TRY(hipStreamSynchronize(s));
   return MACM_OK;
@@ -364,8 +385,36 @@ int macm_world_place(macm_world* w, const void* pos, const void* angle, const vo
   HIP_TRY(hipMemcpyAsync(w->B.angle, angle, EN * sizeof(float), hipMemcpyDefault, s));
   HIP_TRY(hipMemcpyAsync(w->B.targets, targets, ET * sizeof(float2), hipMemcpyDefault, s));
   w->cur = 0;
-  HIP_TRY(launch_init(w, out, s));
+  w->mt_valid = false;  // poses came from the caller's generator
+  HIP_TRY(launch_init(w, out, nullptr, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+static int fill_reset_mask(uint8_t* rmask, const uint8_t* env_mask, int E, hipStream_t s) {
+  // a private copy: the init kernels clear the done flags a caller may pass as the mask
+  if (env_mask) HIP_TRY(hipMemcpyAsync(rmask, env_mask, (size_t)E, hipMemcpyDefault, s));
+  else HIP_TRY(hipMemsetAsync(rmask, 1, (size_t)E, s));
+  return MACM_OK;
+}
+
+int macm_world_reset_envs(macm_world* w, const uint8_t* env_mask, const macm_outputs* out, void* stream) {
+  if (!w) return fail(MACM_E_INVALID, "world is NULL");
+  if (!w->mt_valid)
+    return fail(MACM_E_INVALID, "no per-env random streams: the world was placed, not reset (macm_world_reset)");
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = fill_reset_mask(w->rmask, env_mask, w->P.n_envs, s);
+  if (rc) return rc;
+  PoseDraw D;
+  memset(&D, 0, sizeof(D));
+  D.mode = kFlock;
+  D.n_agents = w->P.n_agents;
+  D.spread = w->cfg.start_spread;
+  D.start_x = w->cfg.start_point[0];
+  D.start_y = w->cfg.start_point[1];
+  HIP_TRY(launch_draw_poses(w->rmask, w->mt, D, w->P.n_envs, w->B.pos, w->B.angle, s));
+  HIP_TRY(launch_init(w, out, w->rmask, s));
   return MACM_OK;
 }
 
@@ -589,7 +638,8 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
       (rc = dalloc(A, &B.time_passed, E)) || (rc = dalloc(A, &B.done, E)) || (rc = dalloc(A, &B.status, E)) ||
       (rc = dalloc(A, &B.env_counters, E * 4)) || (rc = dalloc(A, &TB.health, EN)) ||
       (rc = dalloc(A, &TB.cd_atk, EN)) || (rc = dalloc(A, &TB.cd_mov, EN)) || (rc = dalloc(A, &TB.alive, EN)) ||
-      (rc = dalloc(A, &TB.listener, E)) || (rc = dalloc(A, &TB.winner, E))) {
+      (rc = dalloc(A, &TB.listener, E)) || (rc = dalloc(A, &TB.winner, E)) ||
+      (rc = dalloc(A, &w->mt, E * kMtStride)) || (rc = dalloc(A, &w->rmask, E))) {
     free_tdm(w);
     delete w;
     return rc;
@@ -629,7 +679,8 @@ static TdmBuffers tdm_with_outputs(const macm_tdm* w, const macm_tdm_outputs* ou
 static int tdm_init(macm_tdm* w, const macm_tdm_outputs* out, hipStream_t s) {
   w->cur = 0;
   const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0, s));
+  HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
+                              nullptr, s));
   if (out && out->done) HIP_TRY(hipMemsetAsync(out->done, 0, (size_t)w->P.n_envs, s));
   return MACM_OK;
 }
@@ -641,6 +692,7 @@ int macm_tdm_reset(macm_tdm* w, uint64_t seed, int64_t env_offset, const macm_td
   const int E = w->P.n_envs, N = w->P.n_agents;
   std::vector<float2> pos((size_t)E * N);
   std::vector<float> ang((size_t)E * N);
+  std::vector<uint32_t> mts((size_t)E * kMtStride);
   for (int e = 0; e < E; ++e) {
     PyMT19937 r(seed + (uint64_t)(env_offset + e));
     for (int i = 0; i < N; ++i) {  // combat.py:80-95
@@ -650,10 +702,13 @@ int macm_tdm_reset(macm_tdm* w, uint64_t seed, int64_t env_offset, const macm_td
       pos[(size_t)e * N + i] = make_float2((float)x, (float)y);
       ang[(size_t)e * N + i] = (float)a;
     }
+    save_stream(mts, e, r);
   }
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemcpyAsync(w->B.pos, pos.data(), pos.size() * sizeof(float2), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w->B.angle, ang.data(), ang.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(w->mt, mts.data(), mts.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  w->mt_valid = true;
   int rc = tdm_init(w, out, s);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));  // host vectors feed the async copies
@@ -667,9 +722,32 @@ int macm_tdm_place(macm_tdm* w, const void* pos, const void* angle, const macm_t
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemcpyAsync(w->B.pos, pos, EN * sizeof(float2), hipMemcpyDefault, s));
   HIP_TRY(hipMemcpyAsync(w->B.angle, angle, EN * sizeof(float), hipMemcpyDefault, s));
+  w->mt_valid = false;  // poses came from the caller's generator
   int rc = tdm_init(w, out, s);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
+  return MACM_OK;
+}
+
+int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_outputs* out, void* stream) {
+  if (!w) return fail(MACM_E_INVALID, "tdm is NULL");
+  if (!w->mt_valid)
+    return fail(MACM_E_INVALID, "no per-env random streams: the world was placed, not reset (macm_tdm_reset)");
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = fill_reset_mask(w->rmask, env_mask, w->P.n_envs, s);
+  if (rc) return rc;
+  PoseDraw D;
+  memset(&D, 0, sizeof(D));
+  D.mode = kTdm;
+  D.n_agents = w->P.n_agents;
+  D.half_width = w->cfg.world_width / 2;
+  D.height = w->cfg.world_height;
+  D.TP = w->TP;
+  HIP_TRY(launch_draw_poses(w->rmask, w->mt, D, w->P.n_envs, w->B.pos, w->B.angle, s));
+  const TdmBuffers TB = tdm_with_outputs(w, out);
+  HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
+                              w->rmask, s));
   return MACM_OK;
 }
 

@@ -34,6 +34,12 @@ class PyMT19937 {
   // random.uniform(a, b) = a + (b - a) * random()
   double uniform(double a, double b) { return a + (b - a) * random(); }
 
+  // Generator state (624 words + position), as the device-side stream continues it
+  // (csrc/env_reset.hip).
+  static constexpr int kWords = 624;
+  const uint32_t* state() const { return mt_; }
+  int index() const { return idx_; }
+
  private:
   static constexpr int kN = 624, kM = 397;
   uint32_t mt_[kN];

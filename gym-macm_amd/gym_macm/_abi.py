@@ -167,6 +167,7 @@ SIGNATURES = {
     "macm_world_info_get": (c_int, [c_void_p, POINTER(MacmWorldInfo)]),
     "macm_world_reset": (c_int, [c_void_p, c_uint64, c_int64, POINTER(MacmOutputs), c_void_p]),
     "macm_world_place": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(MacmOutputs), c_void_p]),
+    "macm_world_reset_envs": (c_int, [c_void_p, c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_step": (c_int, [c_void_p, c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_observe": (c_int, [c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_get_state": (c_int, [c_void_p, POINTER(MacmState), c_void_p]),
@@ -179,6 +180,7 @@ SIGNATURES = {
     "macm_tdm_destroy": (c_int, [c_void_p]),
     "macm_tdm_reset": (c_int, [c_void_p, c_uint64, c_int64, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_place": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_reset_envs": (c_int, [c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_step": (c_int, [c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_observe": (c_int, [c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_get_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),

@@ -103,6 +103,20 @@ class TdmWorld:
                                          self._stream()), "macm_tdm_place")
         return self.outputs()
 
+    def reset_envs(self, mask=None):
+        """New episodes in the masked envs ([E] uint8/bool on this device, e.g.
+        ``self.done``; None = all), continuing each env's random stream."""
+        ptr = None
+        if mask is not None:
+            if mask.dtype == torch.bool:
+                mask = mask.to(torch.uint8)
+            if mask.device != self.device or tuple(mask.shape) != (self.E,) or mask.dtype != torch.uint8:
+                raise ValueError(f"mask must be a uint8/bool tensor [{self.E}] on {self.device}")
+            ptr = _ptr(mask.contiguous())
+        _abi.check(self.L.macm_tdm_reset_envs(self.h, ptr, ctypes.byref(self._out), self._stream()),
+                   "macm_tdm_reset_envs")
+        return self.outputs()
+
     def step(self, actions: torch.Tensor):
         """actions: uint8 [E, N, 4] (forward, lateral, rotation, attack) on this device."""
         if actions.device != self.device or not actions.is_contiguous():

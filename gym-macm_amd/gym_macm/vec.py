@@ -8,6 +8,8 @@ launch per step, with actions and outputs as device tensors:
     obs, nbr_id, reward, done = env.step(actions)  # actions uint8 [E, N, 3] on the GPU
 
 Env e is the reference env constructed after ``random.seed(seed + env_offset + e)``;
+each env keeps that stream on the device, so ``reset_envs(mask)`` / ``autoreset=True``
+start new episodes exactly as the env's own ``reset()`` would draw them.
 shard a job over GPUs by giving each rank its contiguous ``env_offset``.
 Settings keyword arguments are the reference's (flockSettings, settings.py:110-146).
 Returned tensors are views of buffers reused by the next call.
@@ -23,7 +25,7 @@ from gym_macm.world import World
 
 class FlockVec(object):
     def __init__(self, num_envs, n_agents=(10,), targets=None, seed=0, env_offset=0, device=None,
-                 obs_dtype=torch.float32, max_contacts=0, **kwargs):
+                 obs_dtype=torch.float32, max_contacts=0, autoreset=False, **kwargs):
         self.settings = flockSettings(**kwargs)
         self.num_envs = int(num_envs)
         self.n_agents = list(n_agents) if not isinstance(n_agents, int) else [n_agents]
@@ -36,6 +38,7 @@ class FlockVec(object):
         self.N = N
         self.seed = int(seed)
         self.env_offset = int(env_offset)
+        self.autoreset = bool(autoreset)
         self.obs, self.nbr_id = self.world.reset(self.seed, self.env_offset)
 
     @property
@@ -49,7 +52,18 @@ class FlockVec(object):
         return self.obs, self.nbr_id
 
     def step(self, actions):
-        return self.world.step(actions)
+        """One step of every env. With ``autoreset``, envs whose episode ended in this
+        step start their next episode right away (reset_envs on the done flags, on
+        the device): the returned done marks them and obs already holds the new
+        episode's initial observation for those envs."""
+        out = self.world.step(actions)
+        if self.autoreset:
+            self.world.reset_envs(self.world.done)
+        return out
+
+    def reset_envs(self, mask=None):
+        """New episodes in the masked envs (see World.reset_envs)."""
+        return self.world.reset_envs(mask)
 
     def observe(self):
         return self.world.observe()

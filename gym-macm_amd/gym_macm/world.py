@@ -96,6 +96,21 @@ class World:
         self.done.zero_()
         return self.obs, self.nbr_id
 
+    def reset_envs(self, mask=None):
+        """New episodes in the envs where `mask` (uint8/bool tensor [E] on this device,
+        e.g. ``self.done``; None = all) is set, continuing each env's random stream
+        (macm_world_reset_envs). Asynchronous; writes the new initial obs for those envs."""
+        ptr = None
+        if mask is not None:
+            if mask.dtype == torch.bool:
+                mask = mask.to(torch.uint8)
+            if mask.device != self.device or tuple(mask.shape) != (self.E,) or mask.dtype != torch.uint8:
+                raise ValueError(f"mask must be a uint8/bool tensor [{self.E}] on {self.device}")
+            ptr = _ptr(mask.contiguous())
+        _abi.check(self.L.macm_world_reset_envs(self.h, ptr, ctypes.byref(self._out_obs), self._stream()),
+                   "macm_world_reset_envs")
+        return self.obs, self.nbr_id
+
     # -- hot path ------------------------------------------------------------
     def step(self, actions: torch.Tensor):
         """actions: discrete uint8/int8 [E,N,3] or continuous float32 [E,N,2], on this device."""

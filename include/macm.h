@@ -264,6 +264,18 @@ int macm_world_place(macm_world* w, const void* pos, const void* angle, const vo
                      const macm_outputs* out, void* stream);
 
 /*
+ * Start a new episode in the envs selected by env_mask (device or host uint8 [E],
+ * nonzero = reset; NULL = all), e.g. the done flags of the last step. Each env
+ * continues the CPython MT19937 stream macm_world_reset seeded it with, drawing
+ * the next agent poses exactly as the reference's reset() draws them from the
+ * global `random` (mvmnt.py:224-233, targets kept); velocities, sleep clocks,
+ * contacts, time and done restart. The new episodes' initial obs are written into
+ * `out` for the reset envs only. Asynchronous on `stream` (no host round trip).
+ * Fails with MACM_E_INVALID after macm_world_place (no device streams).
+ */
+int macm_world_reset_envs(macm_world* w, const uint8_t* env_mask, const macm_outputs* out, void* stream);
+
+/*
  * One env.step for all E envs.
  *   actions: device pointer. Discrete: uint8/int8 [E, N, 3] in {0,1,2}
  *   (MultiDiscrete([3,3,3]), mvmnt.py:143-145). Continuous: float32 [E, N, 2] in [-1,1].
@@ -313,6 +325,13 @@ int macm_tdm_reset(macm_tdm* w, uint64_t seed, int64_t env_offset, const macm_td
 
 /* As reset with caller-drawn poses: pos [E, N, 2] float32, angle [E, N] float32. */
 int macm_tdm_place(macm_tdm* w, const void* pos, const void* angle, const macm_tdm_outputs* out, void* stream);
+
+/*
+ * As macm_world_reset_envs for TDM: the masked envs draw new spawn poses from
+ * their streams (combat.py:234-245 draw order), every agent revived with
+ * init_health, zero cooldowns, a fresh listener, winner -1.
+ */
+int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_outputs* out, void* stream);
 
 /*
  * One TDM.step for all E envs (combat.py:104-184). actions: device uint8

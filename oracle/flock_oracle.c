@@ -38,6 +38,7 @@ typedef struct {
   double time_passed;
   int done;
   int step_count;
+  pyrandom rng;   /* the env's `random` stream, continued by fo_reset_envs */
 } fo_env;
 
 typedef struct fo_batch {
@@ -71,10 +72,28 @@ static void body_def(const macm_config* c, b2l_body_def* d, float x, float y, fl
   d->restitution = 0.0f;
 }
 
+static void env_agents(fo_batch* b, fo_env* e) {
+  const macm_config* c = &b->cfg;
+  pyrandom* r = &e->rng;
+  /* mvmnt.py:60-76 */
+  for (int i = 0; i < b->N; ++i) {
+    double x = c->start_spread * (pyrandom_random(r) - 0.5) + c->start_point[0];
+    double y = c->start_spread * (pyrandom_random(r) - 0.5) + c->start_point[1];
+    double angle = pyrandom_uniform(r, -1, 1) * M_PI;
+    b2l_body_def d;
+    body_def(c, &d, (float)x, (float)y, (float)angle);
+    b2l_create_body(e->w, &d);
+  }
+  e->time_passed = 0.0;
+  e->done = 0;
+  e->step_count = 0;
+}
+
 static void env_init(fo_batch* b, fo_env* e, uint64_t seed) {
   const macm_config* c = &b->cfg;
-  pyrandom r;
-  pyrandom_seed(&r, seed);
+  pyrandom* rp = &e->rng;
+  pyrandom_seed(rp, seed);
+  pyrandom r = *rp; /* targets drawn from the stream, then agents (env_agents) */
   e->w = new_world();
   e->targets = (float*)malloc(sizeof(float) * 2 * (size_t)b->T);
   /* mvmnt.py:46-52 */
@@ -84,18 +103,21 @@ static void env_init(fo_batch* b, fo_env* e, uint64_t seed) {
     e->targets[2 * t + 0] = (float)(rand_dist * cos(rand_angle));
     e->targets[2 * t + 1] = (float)(rand_dist * sin(rand_angle));
   }
-  /* mvmnt.py:60-76 */
-  for (int i = 0; i < b->N; ++i) {
-    double x = c->start_spread * (pyrandom_random(&r) - 0.5) + c->start_point[0];
-    double y = c->start_spread * (pyrandom_random(&r) - 0.5) + c->start_point[1];
-    double angle = pyrandom_uniform(&r, -1, 1) * M_PI;
-    b2l_body_def d;
-    body_def(c, &d, (float)x, (float)y, (float)angle);
-    b2l_create_body(e->w, &d);
+  *rp = r;
+  env_agents(b, e);
+}
+
+/* The working reset (gym_macm/envs/mvmnt.py Flock.reset in this build; the
+ * reference's raises at mvmnt.py:227): next agent poses from the env's stream,
+ * targets kept, a fresh world. */
+void fo_reset_envs(fo_batch* b, const uint8_t* mask) {
+  for (int e = 0; e < b->E; ++e) {
+    if (mask && !mask[e]) continue;
+    fo_env* en = &b->envs[e];
+    b2l_world_free(en->w);
+    en->w = new_world();
+    env_agents(b, en);
   }
-  e->time_passed = 0.0;
-  e->done = 0;
-  e->step_count = 0;
 }
 
 fo_batch* fo_create(const macm_config* cfg, const int32_t* targets_idx, int n_envs, uint64_t seed,

@@ -89,6 +89,8 @@ def lib():
                            P(c_int32), c_int]),
         "to_get_extras": (None, [c_void_p, P(c_double), P(c_double), P(c_int32)]),
         "to_world": (c_void_p, [c_void_p, c_int]),
+        "to_reset_envs": (None, [c_void_p, c_void_p]),
+        "fo_reset_envs": (None, [c_void_p, c_void_p]),
         "to_get_state": (None, [c_void_p] + [c_void_p] * 13 + [c_int] + [c_void_p] * 4),
         "to_set_state": (None, [c_void_p] + [c_void_p] * 13 + [c_int] + [c_void_p] * 4),
     }
@@ -129,6 +131,12 @@ class OracleFlock:
         if h:
             self.L.fo_free(h)
             self.h = None
+
+    def reset_envs(self, mask=None):
+        """This build's working Flock.reset for the masked envs (next poses from each
+        env's stream, targets kept, fresh world)."""
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self.L.fo_reset_envs(self.h, None if m is None else m.ctypes.data)
 
     def observe(self):
         obs = np.zeros((self.E, self.N, self.OD), np.float64)
@@ -278,6 +286,10 @@ class OracleTDM:
         self.L.to_step(self.h, a.ctypes.data, _p(obs, c_double), _p(mask, c_uint8), _p(health, c_double),
                        _p(alive, c_uint8), _p(done, c_uint8), _p(winner, c_int32), n_threads)
         return dict(obs=obs, mask=mask, health=health, alive=alive, done=done, winner=winner)
+
+    def reset_envs(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self.L.to_reset_envs(self.h, None if m is None else m.ctypes.data)
 
     def extras(self):
         E, N = self.E, self.N

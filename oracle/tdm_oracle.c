@@ -38,6 +38,7 @@ typedef struct {
   double time_passed;
   int done, winner;
   int step_count;
+  pyrandom rng;          /* the env's `random` stream, continued by to_reset_envs */
 } to_env;
 
 typedef struct to_batch {
@@ -50,6 +51,35 @@ typedef struct to_batch {
 
 static inline double sgn(double x) { return (x > 0) - (x < 0); }
 static inline double wrap(double t) { return fabs(t) > M_PI ? t - sgn(t) * 2 * M_PI : t; }
+
+/* combat.py:78-101: a new world, bodies at poses drawn from the env's stream. */
+static void env_spawn(const to_batch* b, to_env* en) {
+  const macm_tdm_config* cfg = &b->cfg;
+  const int N = b->N;
+  en->w = b2l_world_new(0.0f, 0.0f, 1);
+  for (int i = 0; i < N; ++i) { /* combat.py:80-95 */
+    double x = pyrandom_random(&en->rng) * (b->team[i] + cfg->world_width / 2);
+    double y = pyrandom_random(&en->rng) * cfg->world_height;
+    double angle = pyrandom_uniform(&en->rng, -1, 1) * M_PI;
+    b2l_body_def d;
+    memset(&d, 0, sizeof(d));
+    d.x = (float)x; d.y = (float)y; d.angle = (float)angle;
+    d.linear_damping = cfg->linear_damping; d.fixed_rotation = 1; d.allow_sleep = 1;
+    d.radius = cfg->radius; d.density = cfg->density; d.friction = cfg->friction;
+    b2l_create_body(en->w, &d);
+    en->health[i] = cfg->init_health;
+    en->cd_atk[i] = 0.0;
+    en->cd_mov[i] = 0.0;
+    en->alive[i] = 1;
+  }
+  for (int t = 0; t < cfg->n_teams; ++t) en->n_alive[t] = cfg->team_size[t];
+  en->listener_hit = 0;
+  en->listener_body = -1;
+  en->winner = -1;
+  en->done = 0;
+  en->time_passed = 0.0;
+  en->step_count = 0;
+}
 
 to_batch* to_create(const macm_tdm_config* cfg, int n_envs, uint64_t seed, int64_t env_offset) {
   if (!cfg || n_envs <= 0 || cfg->n_teams < 1 || cfg->n_teams > 4) return NULL;
@@ -66,32 +96,26 @@ to_batch* to_create(const macm_tdm_config* cfg, int n_envs, uint64_t seed, int64
   b->envs = (to_env*)calloc((size_t)n_envs, sizeof(to_env));
   for (int e = 0; e < n_envs; ++e) {
     to_env* en = &b->envs[e];
-    pyrandom r;
-    pyrandom_seed(&r, seed + (uint64_t)(env_offset + e));
-    en->w = b2l_world_new(0.0f, 0.0f, 1);
+    pyrandom_seed(&en->rng, seed + (uint64_t)(env_offset + e));
     en->health = (double*)calloc((size_t)N, sizeof(double));
     en->cd_atk = (double*)calloc((size_t)N, sizeof(double));
     en->cd_mov = (double*)calloc((size_t)N, sizeof(double));
     en->alive = (uint8_t*)calloc((size_t)N, 1);
-    for (int i = 0; i < N; ++i) { /* combat.py:80-95 */
-      double x = pyrandom_random(&r) * (b->team[i] + cfg->world_width / 2);
-      double y = pyrandom_random(&r) * cfg->world_height;
-      double angle = pyrandom_uniform(&r, -1, 1) * M_PI;
-      b2l_body_def d;
-      memset(&d, 0, sizeof(d));
-      d.x = (float)x; d.y = (float)y; d.angle = (float)angle;
-      d.linear_damping = cfg->linear_damping; d.fixed_rotation = 1; d.allow_sleep = 1;
-      d.radius = cfg->radius; d.density = cfg->density; d.friction = cfg->friction;
-      b2l_create_body(en->w, &d);
-      en->health[i] = cfg->init_health;
-      en->alive[i] = 1;
-    }
-    for (int t = 0; t < cfg->n_teams; ++t) en->n_alive[t] = cfg->team_size[t];
-    en->listener_hit = 0;
-    en->listener_body = -1;
-    en->winner = -1;
+    env_spawn(b, en);
   }
   return b;
+}
+
+/* This build's working reset (the reference's, combat.py:234-245, leaves dead
+ * bodies inactive): next spawn poses from the env's stream, a fresh world, every
+ * agent alive with init_health and zero cooldowns, a fresh listener. */
+void to_reset_envs(to_batch* b, const uint8_t* mask) {
+  for (int e = 0; e < b->E; ++e) {
+    if (mask && !mask[e]) continue;
+    to_env* en = &b->envs[e];
+    b2l_world_free(en->w);
+    env_spawn(b, en);
+  }
 }
 
 void to_free(to_batch* b) {
