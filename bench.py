@@ -227,13 +227,15 @@ def main():
     if rank == 0:
         b_alg = B_ALG if args.env == "flock" else b_alg_tdm(N)
         achieved_gbs = b_alg * E * N / (kernel_ms * 1e-3) / 1e9
+        ncap = 32 if N <= 32 else 64
         if args.env == "tdm":
-            kname = "env_step_w64<1, float>"
+            kname = f"env_step_w64<1, {ncap}, float>"
         else:
-            kname = "env_step_w64<0, float>" if N <= 64 else "flock_step_wg<float>"
+            kname = f"env_step_w64<0, {ncap}, float>" if N <= 64 else "flock_step_wg<float>"
         traffic = None
         tj = load_traffic(args.traffic_json)
-        if tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname:
+        if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
+                and tj.get("policy", "random") == args.policy):
             traffic = tj.get("hbm_bytes_per_launch")
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]

@@ -105,6 +105,21 @@ __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// v_writelane_b32 with a compile-time lane (an inline constant: with an SGPR value
+// the lane select cannot be a second SGPR on gfx9): lane J of v receives x.
+template <int J>
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(J));
+}
+
+typedef float fvec2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fvec2 mk2(float a, float b) {
+  fvec2 v;
+  v.x = a;
+  v.y = b;
+  return v;
+}
+
 // One agent's record for the all-pairs sweep: read by LDS broadcast (2 x ds_read_b128).
 struct __align__(32) PairRec {
   float4 fn;  // fat AABB after SynchronizeFixtures
@@ -189,6 +204,47 @@ __device__ __forceinline__ void tdm_obs_rows(OT* __restrict__ obs, uint8_t* __re
   }
 }
 
+struct SweepState {
+  uint32_t ov_lo, ov_hi;  // partner row of this lane's agent (written by lane j = row owner)
+  float best;             // nearest other agent: squared distance
+  int bj;                 //                      and index
+};
+
+// One record of the all-pairs sweep, unrolled at compile time over J < NCAP (lanes
+// >= N hold dummies that overlap nothing and are infinitely far). Row J of the
+// symmetric overlap matrix is the ballot of the AABB test and goes to lane J by
+// v_writelane; the AABB / distance differences run as packed float2 ops, each lane
+// of which is the same IEEE operation as the scalar form.
+template <int J, int NCAP, bool NN>
+__device__ __forceinline__ void sweep_step(const PairRec* s_pj, const PairRec q, fvec2 fn_lo, fvec2 fn_hi,
+                                           fvec2 cme, unsigned long long valid, int lane, SweepState& st) {
+  PairRec qn;
+  if constexpr (J + 1 < NCAP) qn = s_pj[J + 1];  // next record in flight while this one is tested
+  // b2TestOverlap(fn, fj) separates iff one of (fj.lo - fn.hi, fn.lo - fj.hi) > 0;
+  // for finite AABBs (and the +-inf dummies) that is max(...) > 0
+  const fvec2 a = mk2(q.fn.x, q.fn.y) - fn_hi;
+  const fvec2 b = fn_lo - mk2(q.fn.z, q.fn.w);
+  const float sepv = fmaxf(fmaxf(a.x, a.y), fmaxf(b.x, b.y));
+  const unsigned long long row = __ballot(!(sepv > 0.0f)) & valid;
+  writelane<J>(st.ov_lo, (uint32_t)row);
+  writelane<J>(st.ov_hi, (uint32_t)(row >> 32));
+  if constexpr (NN) {
+    const fvec2 d = mk2(q.c.x, q.c.y) - cme;  // other.position - agent.position
+    const fvec2 dd = d * d;
+    const float d2 = dd.x + dd.y;             // b2DistanceSquared(other, agent)
+    if (d2 < st.best && lane != J) {          // strict '<': lowest index wins ties (mvmnt.py:194)
+      st.best = d2;
+      st.bj = J;
+    }
+    // materialise the running minimum here: otherwise the compiler sinks all the
+    // distance work past the sweep and spills every record's position
+    asm volatile("" : "+v"(st.best), "+v"(st.bj));
+  }
+  // keep the scheduler from hoisting every record's LDS read (register pressure)
+  if constexpr ((J & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+  if constexpr (J + 1 < NCAP) sweep_step<J + 1, NCAP, NN>(s_pj, qn, fn_lo, fn_hi, cme, valid, lane, st);
+}
+
 // New-pair compaction in descending (a, b) order: lane a owns the bitmask of
 // partners b > a. Returns the total count; writes at most C entries.
 __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newmask, uint32_t* ocab,
@@ -217,8 +273,10 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
 // MODE kFlock: Flock.step. MODE kTdm: TDM.step (combat.py:104-184) — the same
 // physics with alive masks, plus melee ray casts, health, deaths and the full
 // relative observation; `TP`/`TB` are unused for Flock.
-template <int MODE, typename OT>
-__global__ __launch_bounds__(W) void env_step_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
+// waves_per_eu(4): <= 128 VGPRs, so the 16 envs per CU of a 4096-env launch are
+// resident together (the unrolled sweep would otherwise hoist every LDS record).
+template <int MODE, int NCAP, typename OT>
+__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_step_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
                                                   int cur, const void* __restrict__ actions,
                                                   OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
                                                   float* __restrict__ rew_out,
@@ -365,8 +423,11 @@ __global__ __launch_bounds__(W) void env_step_w64(StepParams P, WorldBuffers B, 
       double force = P.force;
       // Agent.force = _force * (1 - percent_mov_penalty * int(cooldown_mov_penalty > 0))   combat.py:46-49
       if constexpr (kT) force = P.force * (1.0 - TP.percent_mov_penalty * (double)(cdm > 0.0));
-      const double fx = (cos(ad) * k0 + cos(ad + M_PI / 2) * k1) * cc * force;
-      const double fy = (sin(ad) * k0 + sin(ad + M_PI / 2) * k1) * cc * force;
+      double s0, c0, s1, c1;  // np.cos / np.sin of angle and angle + pi/2 (one reduction each)
+      sincos(ad, &s0, &c0);
+      sincos(ad + M_PI / 2, &s1, &c1);
+      const double fx = (c0 * k0 + c1 * k1) * cc * force;
+      const double fy = (s0 * k0 + s1 * k1) * cc * force;
       Fx = (float)fx;  // ApplyForce: b2Vec2(float32) accumulated onto m_force = 0
       Fy = (float)fy;
       if constexpr (kT) {  // melee (combat.py:141-155)
@@ -793,36 +854,21 @@ __global__ __launch_bounds__(W) void env_step_w64(StepParams P, WorldBuffers B, 
   //   FindNewContacts creates        Ov(F_t) \ Ov(F_{t-1})
   // Overlap is symmetric, so the ballot of ovn at iteration j is agent j's
   // partner row; lane j keeps it. Agent j's record arrives by LDS broadcast.
+  // The sweep is fully unrolled over NCAP >= N records (lanes >= N hold dummies
+  // that overlap nothing and are infinitely far), so j is a compile-time constant:
+  // row j goes to lane j by v_writelane, and the AABB / distance differences run
+  // as packed float2 ops (each lane-wise result is the same IEEE op as scalar).
   const unsigned long long valid = livem;
-  unsigned long long myov = 0ull;
-  float best = __builtin_inff();
-  int bj = lane == 0 ? 1 : 0;
-  const int N4 = (N + 3) & ~3;
-  for (int j0 = 0; j0 < N4; j0 += 4) {
-    PairRec q[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) q[u] = s_pj[j0 + u];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = j0 + u;
-      const float4 fj = q[u].fn;
-      // b2TestOverlap(fn, fj) separates iff one of (fj.lo - fn.hi, fn.lo - fj.hi) > 0;
-      // for finite AABBs (and the +-inf dummies) that is max(...) > 0, all on VALU
-      const float sepv = fmaxf(fmaxf(fj.x - fn.z, fj.y - fn.w), fmaxf(fn.x - fj.z, fn.y - fj.w));
-      const unsigned long long row = __ballot(!(sepv > 0.0f)) & valid;
-      const bool self = lane == j;
-      myov = self ? row : myov;
-      if constexpr (!kT) {
-        const float dx = q[u].c.x - cx, dy = q[u].c.y - cy;  // other.position - agent.position
-        const float d2 = dx * dx + dy * dy;                 // b2DistanceSquared(other, agent)
-        const float d2o = self ? __builtin_inff() : d2;
-        if (d2o < best) {  // strict '<': lowest index wins ties (mvmnt.py:194)
-          best = d2o;
-          bj = j;
-        }
-      }
-    }
-  }
+  SweepState sw;
+  sw.ov_lo = 0u;
+  sw.ov_hi = 0u;
+  sw.best = __builtin_inff();
+  sw.bj = lane == 0 ? 1 : 0;
+  sweep_step<0, NCAP, !kT>(s_pj, s_pj[0], mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), valid, lane, sw);
+  const float best = sw.best;
+  const int bj = sw.bj;
+  const uint32_t ov_lo = sw.ov_lo, ov_hi = sw.ov_hi;
+  unsigned long long myov = ((unsigned long long)ov_hi << 32) | ov_lo;
   myov &= ~(1ull << lane);
   const unsigned long long oldm = (unsigned long long)s_oldm[2 * lane] | ((unsigned long long)s_oldm[2 * lane + 1] << 32);
   const bool coll = act && ((myov | oldm) != 0ull);
@@ -1174,12 +1220,22 @@ hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, 
   dim3 grid(P.n_envs), block(W);
   const TdmParams TP{};
   const TdmBuffers TB{};
-  if (obs_f64)
-    hipLaunchKernelGGL((env_step_w64<kFlock, double>), grid, block, 0, s, P, B, TP, TB, cur, actions, (double*)obs,
-                       nbr, rew, coll, done);
-  else
-    hipLaunchKernelGGL((env_step_w64<kFlock, float>), grid, block, 0, s, P, B, TP, TB, cur, actions, (float*)obs,
-                       nbr, rew, coll, done);
+  const bool small = P.n_agents <= 32;
+  if (obs_f64) {
+    if (small)
+      hipLaunchKernelGGL((env_step_w64<kFlock, 32, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (double*)obs, nbr, rew, coll, done);
+    else
+      hipLaunchKernelGGL((env_step_w64<kFlock, 64, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (double*)obs, nbr, rew, coll, done);
+  } else {
+    if (small)
+      hipLaunchKernelGGL((env_step_w64<kFlock, 32, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (float*)obs, nbr, rew, coll, done);
+    else
+      hipLaunchKernelGGL((env_step_w64<kFlock, 64, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (float*)obs, nbr, rew, coll, done);
+  }
   return hipGetLastError();
 }
 
@@ -1187,12 +1243,22 @@ hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const
                                const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
                                uint8_t* done, hipStream_t s) {
   dim3 grid(P.n_envs), block(W);
-  if (obs_f64)
-    hipLaunchKernelGGL((env_step_w64<kTdm, double>), grid, block, 0, s, P, B, TP, TB, cur, actions, (double*)obs,
-                       nullptr, nullptr, nullptr, done);
-  else
-    hipLaunchKernelGGL((env_step_w64<kTdm, float>), grid, block, 0, s, P, B, TP, TB, cur, actions, (float*)obs,
-                       nullptr, nullptr, nullptr, done);
+  const bool small = P.n_agents <= 32;
+  if (obs_f64) {
+    if (small)
+      hipLaunchKernelGGL((env_step_w64<kTdm, 32, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (double*)obs, nullptr, nullptr, nullptr, done);
+    else
+      hipLaunchKernelGGL((env_step_w64<kTdm, 64, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (double*)obs, nullptr, nullptr, nullptr, done);
+  } else {
+    if (small)
+      hipLaunchKernelGGL((env_step_w64<kTdm, 32, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (float*)obs, nullptr, nullptr, nullptr, done);
+    else
+      hipLaunchKernelGGL((env_step_w64<kTdm, 64, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (float*)obs, nullptr, nullptr, nullptr, done);
+  }
   return hipGetLastError();
 }
 

@@ -2,7 +2,7 @@
 that bench.py reads for `roofline.traffic`.
 
     python tools/pmc_summary.py gpurun_out/<dir> --envs 4096 --agents 64 -o profiles/pmc_flock_step.json
-    python tools/pmc_summary.py gpurun_out/<dir> --kernel "env_step_w64<1, float>" --agents 32 \
+    python tools/pmc_summary.py gpurun_out/<dir> --kernel "env_step_w64<1, 32, float>" --agents 32 \
         -o profiles/pmc_tdm_step.json
 
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE
@@ -30,7 +30,8 @@ def kernel_means(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="env_step_w64<0, float>")
+    ap.add_argument("--kernel", default="env_step_w64<0, 64, float>")
+    ap.add_argument("--policy", default="random")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--agents", type=int, default=64)
     ap.add_argument("-o", "--out", default="")
@@ -44,7 +45,7 @@ def main():
     write_b = res["WRITE_SIZE"] * 1024.0
     agents = a.envs * a.agents
     out = {
-        "kernel": a.kernel, "envs": a.envs, "agents": a.agents,
+        "kernel": a.kernel, "envs": a.envs, "agents": a.agents, "policy": a.policy,
         "fetch_size_kib": res["FETCH_SIZE"], "write_size_kib": res["WRITE_SIZE"],
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "hbm_bytes_per_agent_step": (2.0 * fetch_b + write_b) / agents,
