@@ -176,28 +176,33 @@ __device__ __forceinline__ void store4(OT* o, double a, double b, double c, doub
 // agent j = k < i ? k : k + 1, holding (r, t, p, is_ally) with rel = other - agent
 // (float32), r = sqrt(b2DistanceSquared), t = atan2(rel) - angle_i and
 // p = angle_j - angle_i each wrapped once; mask = both alive, masked slots zero.
-// Lane k writes slot k of row i, so each row is one contiguous store.
+// The wave is split into 64/gs groups of gs >= N-1 lanes (gs a power of two); each
+// group writes one row per pass (lane k -> slot k, one contiguous store per row), so
+// at N = 32 two rows go per pass and no f64 atan2 lane idles.
 template <typename OT>
 __device__ __forceinline__ void tdm_obs_rows(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
                                              unsigned long long livem, const TdmParams& TP, const float* sx,
                                              const float* sy, const float* sa) {
-  for (int i = 0; i < N; ++i) {
-    const float xi = sx[i], yi = sy[i], ai = sa[i];
-    const bool li = (livem >> i) & 1ull;
-    const int ti = tdm_team_of(TP, i);
-    if (lane < N - 1) {
-      const int j = lane < i ? lane : lane + 1;
-      const bool m = li && ((livem >> j) & 1ull);
+  const int S = N - 1;
+  int lg = 6;  // log2(gs)
+  while (lg > 0 && (1 << (lg - 1)) >= S) --lg;
+  const int ng = 64 >> lg, g = lane >> lg, k = lane & ((1 << lg) - 1);
+  for (int i0 = 0; i0 < N; i0 += ng) {
+    const int i = i0 + g;
+    if (i < N && k < S) {
+      const int j = k < i ? k : k + 1;
+      const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
       double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
       if (m) {
-        const float rx = sx[j] - xi, ry = sy[j] - yi;  // other.position - agent.position
-        const float d2 = rx * rx + ry * ry;           // b2DistanceSquared(other, agent)
+        const float ai = sa[i];
+        const float rx = sx[j] - sx[i], ry = sy[j] - sy[i];  // other.position - agent.position
+        const float d2 = rx * rx + ry * ry;                 // b2DistanceSquared(other, agent)
         r = sqrt((double)d2);
         t = wrap_pi(atan2((double)ry, (double)rx) - (double)ai);
         p = wrap_pi((double)sa[j] - (double)ai);
-        ty = tdm_team_of(TP, j) == ti ? 1.0 : 0.0;
+        ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
       }
-      const size_t slot = (size_t)i * (N - 1) + lane;
+      const size_t slot = (size_t)i * S + k;
       if (obs) store4<OT>(obs + slot * 4, r, t, p, ty);
       if (mask) mask[slot] = m ? 1 : 0;
     }
