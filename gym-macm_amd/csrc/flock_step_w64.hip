@@ -209,6 +209,68 @@ __device__ __forceinline__ void tdm_obs_rows(OT* __restrict__ obs, uint8_t* __re
   }
 }
 
+// b2ContactSolver, one circle contact (fixedRotation: no angular terms). Shared by
+// the LDS path and the single-contact register path, so both round identically.
+__device__ __forceinline__ void warm_start_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
+                                                   float ny, float ln, float ltg, float mA, float mB) {
+  const float tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
+  const float Px = ln * nx + ltg * tx, Py = ln * ny + ltg * ty;
+  vAx = vAx - mA * Px;
+  vAy = vAy - mA * Py;
+  vBx = vBx + mB * Px;
+  vBy = vBy + mB * Py;
+}
+
+__device__ __forceinline__ void solve_velocity_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
+                                                       float ny, float& ln, float& ltg, float mA, float mB,
+                                                       float kmass, float friction) {
+  const float tx = ny, ty = -nx;
+  {  // tangent first
+    const float dvx = vBx - vAx, dvy = vBy - vAy;
+    const float vt = dvx * tx + dvy * ty;
+    float lambda = kmass * (-vt);
+    const float maxf = friction * ln;
+    const float ni = bclamp(ltg + lambda, -maxf, maxf);
+    lambda = ni - ltg;
+    ltg = ni;
+    const float Px = lambda * tx, Py = lambda * ty;
+    vAx = vAx - mA * Px;
+    vAy = vAy - mA * Py;
+    vBx = vBx + mB * Px;
+    vBy = vBy + mB * Py;
+  }
+  {  // normal
+    const float dvx = vBx - vAx, dvy = vBy - vAy;
+    const float vn = dvx * nx + dvy * ny;
+    float lambda = -kmass * (vn - 0.0f);  // velocityBias == 0 (restitution 0)
+    const float ni = bmax(ln + lambda, 0.0f);
+    lambda = ni - ln;
+    ln = ni;
+    const float Px = lambda * nx, Py = lambda * ny;
+    vAx = vAx - mA * Px;
+    vAy = vAy - mA * Py;
+    vBx = vBx + mB * Px;
+    vBy = vBy + mB * Py;
+  }
+}
+
+// b2PositionSolverManifold + one SolvePositionConstraints contact; returns sep.
+__device__ __forceinline__ float solve_position_contact(float& cAx, float& cAy, float& cBx, float& cBy,
+                                                        float radius, float mA, float mB) {
+  float nx = cBx - cAx, ny = cBy - cAy;
+  normalize(nx, ny);
+  const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - radius - radius;
+  const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+  const float K = mA + mB;
+  const float imp = K > 0.0f ? -Cc / K : 0.0f;
+  const float Px = imp * nx, Py = imp * ny;
+  cAx = cAx - mA * Px;
+  cAy = cAy - mA * Py;
+  cBx = cBx + mB * Px;
+  cBy = cBy + mB * Py;
+  return sep;
+}
+
 struct SweepState {
   uint32_t ov_lo, ov_hi;  // partner row of this lane's agent (written by lane j = row owner)
   float best;             // nearest other agent: squared distance
@@ -677,21 +739,39 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   const float friction = P.friction;
 
   // ---- warm start + velocity iterations, one lane per island ---------------
+  // A single-contact island (the common case) runs entirely in registers; larger
+  // islands go through LDS in Box2D's order.
   for (int I = lane; I < nisl; I += W) {
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
+    if (c1 - c0 == 1) {
+      const int t = s_ord[c0];
+      const uint32_t ab = s_tab[t];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      const float nx = s_tnx[t], ny = s_tny[t];
+      float ln = s_tln[t], ltg = s_tlt[t];
+      float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+      if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB);
+      for (int it = 0; it < P.vel_iters; ++it)
+        solve_velocity_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB, kmass, friction);
+      s_vx[a] = vAx;
+      s_vy[a] = vAy;
+      s_vx[b] = vBx;
+      s_vy[b] = vBy;
+      s_tln[t] = ln;
+      s_tlt[t] = ltg;
+      continue;
+    }
     if (P.warm_starting) {
       for (int k = c0; k < c1; ++k) {
         const int t = s_ord[k];
         const uint32_t ab = s_tab[t];
         const int a = ab & 0xffffu, b = ab >> 16;
-        const float nx = s_tnx[t], ny = s_tny[t];
-        const float tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
-        const float ln = s_tln[t], ltg = s_tlt[t];
-        const float Px = ln * nx + ltg * tx, Py = ln * ny + ltg * ty;
-        s_vx[a] = s_vx[a] - mA * Px;
-        s_vy[a] = s_vy[a] - mA * Py;
-        s_vx[b] = s_vx[b] + mB * Px;
-        s_vy[b] = s_vy[b] + mB * Py;
+        float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+        warm_start_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], s_tln[t], s_tlt[t], mA, mB);
+        s_vx[a] = vAx;
+        s_vy[a] = vAy;
+        s_vx[b] = vBx;
+        s_vy[b] = vBy;
       }
     }
     for (int it = 0; it < P.vel_iters; ++it) {
@@ -699,37 +779,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         const int t = s_ord[k];
         const uint32_t ab = s_tab[t];
         const int a = ab & 0xffffu, b = ab >> 16;
-        const float nx = s_tnx[t], ny = s_tny[t];
-        const float tx = ny, ty = -nx;
         float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
         float ln = s_tln[t], ltg = s_tlt[t];
-        {  // tangent first
-          const float dvx = vBx - vAx, dvy = vBy - vAy;
-          const float vt = dvx * tx + dvy * ty;
-          float lambda = kmass * (-vt);
-          const float maxf = friction * ln;
-          const float ni = bclamp(ltg + lambda, -maxf, maxf);
-          lambda = ni - ltg;
-          ltg = ni;
-          const float Px = lambda * tx, Py = lambda * ty;
-          vAx = vAx - mA * Px;
-          vAy = vAy - mA * Py;
-          vBx = vBx + mB * Px;
-          vBy = vBy + mB * Py;
-        }
-        {  // normal
-          const float dvx = vBx - vAx, dvy = vBy - vAy;
-          const float vn = dvx * nx + dvy * ny;
-          float lambda = -kmass * (vn - 0.0f);  // velocityBias == 0 (restitution 0)
-          const float ni = bmax(ln + lambda, 0.0f);
-          lambda = ni - ln;
-          ln = ni;
-          const float Px = lambda * nx, Py = lambda * ny;
-          vAx = vAx - mA * Px;
-          vAy = vAy - mA * Py;
-          vBx = vBx + mB * Px;
-          vBy = vBy + mB * Py;
-        }
+        solve_velocity_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], ln, ltg, mA, mB, kmass, friction);
         s_vx[a] = vAx;
         s_vy[a] = vAy;
         s_vx[b] = vBx;
@@ -765,25 +817,33 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   for (int I = lane; I < nisl; I += W) {
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
     int solved = 0;
+    if (c1 - c0 == 1) {  // single contact: registers
+      const uint32_t ab = s_tab[s_ord[c0]];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      float cAx = s_cx[a], cAy = s_cy[a], cBx = s_cx[b], cBy = s_cy[b];
+      for (int it = 0; it < P.pos_iters; ++it) {
+        const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+        const float min_sep = bmin(0.0f, sep);
+        if (min_sep >= -3.0f * kLinearSlop) {
+          solved = 1;
+          break;
+        }
+      }
+      s_cx[a] = cAx;
+      s_cy[a] = cAy;
+      s_cx[b] = cBx;
+      s_cy[b] = cBy;
+      s_isolved[I] = (uint8_t)solved;
+      continue;
+    }
     for (int it = 0; it < P.pos_iters; ++it) {
       float min_sep = 0.0f;
       for (int k = c0; k < c1; ++k) {
-        const int t = s_ord[k];
-        const uint32_t ab = s_tab[t];
+        const uint32_t ab = s_tab[s_ord[k]];
         const int a = ab & 0xffffu, b = ab >> 16;
         float cAx = s_cx[a], cAy = s_cy[a], cBx = s_cx[b], cBy = s_cy[b];
-        float nx = cBx - cAx, ny = cBy - cAy;
-        normalize(nx, ny);
-        const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - P.radius - P.radius;
+        const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
         min_sep = bmin(min_sep, sep);
-        const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-        const float K = mA + mB;
-        const float imp = K > 0.0f ? -Cc / K : 0.0f;
-        const float Px = imp * nx, Py = imp * ny;
-        cAx = cAx - mA * Px;
-        cAy = cAy - mA * Py;
-        cBx = cBx + mB * Px;
-        cBy = cBy + mB * Py;
         s_cx[a] = cAx;
         s_cy[a] = cAy;
         s_cx[b] = cBx;
