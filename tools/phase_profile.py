@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--spread", type=float, default=20.0)
+    ap.add_argument("--policy", choices=("random", "bots"), default="random")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     L = _abi.lib()
@@ -46,7 +47,11 @@ def main():
     buf = np.zeros((E, 16), np.uint64)
     deltas, stats, walls = [], [], []
     for s in range(args.warmup + args.steps):
-        a = torch.randint(0, 3, (E, N, 3), dtype=torch.uint8, device="cuda:0", generator=gen)
+        if args.policy == "bots":
+            from gym_macm.bots import flock_actions
+            a = flock_actions(vec.obs)
+        else:
+            a = torch.randint(0, 3, (E, N, 3), dtype=torch.uint8, device="cuda:0", generator=gen)
         if s >= args.warmup:
             torch.cuda.synchronize()
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,7 +69,7 @@ def main():
     d = np.concatenate(deltas)  # [steps*E, 13]
     st = np.concatenate(stats)
     total = d.sum(axis=1)
-    out = {"envs": E, "agents": N, "spread": args.spread, "kernel_ms_stamped": float(np.mean(walls)),
+    out = {"envs": E, "agents": N, "spread": args.spread, "policy": args.policy, "kernel_ms_stamped": float(np.mean(walls)),
            "wave_cycles_mean": float(total.mean()), "wave_cycles_p95": float(np.percentile(total, 95)),
            "wave_cycles_max": float(total.max()), "phases": {}}
     for k, name in enumerate(PHASES):
