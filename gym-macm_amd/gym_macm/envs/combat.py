@@ -59,10 +59,12 @@ class _BodyView(object):
 
 
 class Agent(object):
-    """reference combat.py:13-54; health, alive and cooldowns mirror the device state
-    after every step."""
+    """reference combat.py:13-54; health and alive mirror the device state after every
+    step, the cooldowns are read from it on access."""
 
-    def __init__(self, ID, team=0, actor=None):
+    def __init__(self, ID, team=0, actor=None, env=None, index=0):
+        self._env = env
+        self._k = index
         self.init_health = 1
         self.team = team
         self.id = ID
@@ -74,9 +76,15 @@ class Agent(object):
         self.percent_mov_penalty = 0.2
         self.health = self.init_health
         self.alive = True
-        self.cooldown_atk = 0
-        self.cooldown_mov_penalty = 0
         self.body = None
+
+    @property
+    def cooldown_atk(self):
+        return float(self._env._host_state()["cd_atk"][0, self._k]) if self._env else 0
+
+    @property
+    def cooldown_mov_penalty(self):
+        return float(self._env._host_state()["cd_mov"][0, self._k]) if self._env else 0
 
     @property
     def color(self):
@@ -113,7 +121,7 @@ class TDM(object):
         pos, ang = self._draw_poses()
         for i in range(len(self.n_agents)):
             for j in range(self.n_agents[i]):
-                agent = Agent(team=i, ID=str(i) + str(j))
+                agent = Agent(team=i, ID=str(i) + str(j), env=self, index=len(self.agents))
                 if actors:
                     agent.actor = actors[i][j]
                 if colors:
@@ -123,7 +131,10 @@ class TDM(object):
         cfg = to_tdm_config(self.settings, self.n_agents, obs_f64=True, fresh_raycast=fresh_raycast,
                             decay_mov_penalty=decay_mov_penalty, world_width=self.world_width,
                             world_height=self.world_height)
-        self.world = TdmWorld(cfg, 1, device=device)
+        # one env: outputs and actions in pinned host memory (zero-copy views)
+        self.world = TdmWorld(cfg, 1, device=device, host_outputs=True)
+        self._act = torch.ones((1, N, 4), dtype=torch.uint8, pin_memory=True)
+        self._act_np = self._act.numpy()
         self._cache = None
         self.world.place(pos[None], ang[None])
         self.n_alive = self.n_agents.copy()
@@ -151,17 +162,19 @@ class TDM(object):
             self._cache = self.world.get_state()
         return self._cache
 
+    def _sync(self):
+        torch.cuda.current_stream(self.world.device).synchronize()
+
     def _sync_agents(self):
-        s = self._host_state()
+        health = self.world.health[0].numpy()
+        alive = self.world.alive[0].numpy()
         for k, agent in enumerate(self.agents):
-            agent.health = float(s["health"][0, k])
-            agent.alive = bool(s["alive"][0, k])
-            agent.cooldown_atk = float(s["cd_atk"][0, k])
-            agent.cooldown_mov_penalty = float(s["cd_mov"][0, k])
+            agent.health = float(health[k])
+            agent.alive = bool(alive[k])
 
     def _obs_dict(self):
-        obs = self.world.obs[0].cpu().numpy()
-        mask = self.world.mask[0].cpu().numpy()
+        obs = self.world.obs[0].numpy()  # pinned host outputs: views, copied per entry below
+        mask = self.world.mask[0].numpy()
         self._sync_agents()
         out = {}
         N = self._N
@@ -187,12 +200,11 @@ class TDM(object):
                     continue
                 actions[agent.id] = agent.actor(self.obs[agent.id])
         assert self.action_space.contains(actions)
-        a = np.ones((1, self._N, 4), np.uint8)
-        a[..., 3] = 0
+        a = self._act_np
         for k, agent in enumerate(self.agents):
-            if agent.alive:
-                a[0, k] = np.asarray(actions[agent.id])
-        self.world.step(torch.from_numpy(a).to(self.world.device))
+            a[0, k] = actions[agent.id] if agent.alive else (1, 1, 1, 0)
+        self.world.step(self._act)
+        self._sync()
         self._cache = None
         alive_before = [agent.alive for agent in self.agents]
         self.obs = self._obs_dict()
@@ -204,8 +216,8 @@ class TDM(object):
         if died:
             self.create_space()
         self.time_passed += (1 / self.settings.hz)
-        self.done = bool(self.world.done[0].item())
-        w = int(self.world.winner[0].item())
+        self.done = bool(self.world.done[0])
+        w = int(self.world.winner[0])
         self.winner = None if w < 0 else w
         return self.obs
 
@@ -229,6 +241,7 @@ class TDM(object):
 
     def get_obs(self):
         self.world.observe()
+        self._sync()
         return self._obs_dict()
 
     def reset(self):

@@ -136,7 +136,13 @@ class Flock(object):
             self.agents.append(agent)
         self.targets = [Vec2(*tg[t]) for t in range(self.n_targets)]
         cfg = to_config(s, N, self.n_targets, obs_f64=True)
-        self.world = World(cfg, np.asarray(self.targets_idx, np.int32), 1, device=device)
+        # one env: outputs (and actions) in pinned host memory, read as zero-copy views
+        self.world = World(cfg, np.asarray(self.targets_idx, np.int32), 1, device=device, host_outputs=True)
+        if s.action_mode == "discrete":
+            self._act = torch.ones((1, N, 3), dtype=torch.uint8, pin_memory=True)
+        else:
+            self._act = torch.zeros((1, N, 2), dtype=torch.float32, pin_memory=True)
+        self._act_np = self._act.numpy()
         self._N = N
         self._cache = None
         obs, nbr = self.world.place(pos[None], ang[None], tg[None])
@@ -150,9 +156,12 @@ class Flock(object):
             self._cache = self.world.get_state()
         return self._cache
 
+    def _sync(self):
+        torch.cuda.current_stream(self.world.device).synchronize()
+
     def _obs_dict(self, obs_t, nbr_t):
-        obs = obs_t[0].cpu().numpy()
-        nbr = nbr_t[0].cpu().numpy()
+        obs = obs_t[0].numpy()  # pinned host output: a view, copied per node below
+        nbr = nbr_t[0].numpy()
         N = self._N
         half = obs.shape[1] // 2
         out = {}
@@ -173,20 +182,14 @@ class Flock(object):
             for agent in self.agents:
                 actions[agent.id] = agent.actor({agent.id: self.obs[agent.id]})
         assert self.action_space.contains(actions)
-        N = self._N
-        if self.settings.action_mode == "discrete":
-            a = np.empty((1, N, 3), np.uint8)
-            for agent in self.agents:
-                a[0, agent.id] = np.asarray(actions[agent.id])
-        else:
-            a = np.empty((1, N, 2), np.float32)
-            for agent in self.agents:
-                a[0, agent.id] = np.asarray(actions[agent.id], np.float32)
-        at = torch.from_numpy(a).to(self.world.device)
-        obs_t, nbr_t, rew_t, _ = self.world.step(at)
+        a = self._act_np
+        for agent in self.agents:
+            a[0, agent.id] = actions[agent.id]
+        obs_t, nbr_t, rew_t, _ = self.world.step(self._act)
+        self._sync()
         self._cache = None
-        obs = obs_t[0].cpu().numpy()
-        rew = rew_t[0].cpu().numpy()
+        obs = obs_t[0].numpy()
+        rew = rew_t[0].numpy()
         half = obs.shape[1] // 2
         rewards = {}
         for agent in self.agents:
@@ -219,6 +222,7 @@ class Flock(object):
 
     def get_obs(self):
         obs, nbr = self.world.observe()
+        self._sync()
         return self._obs_dict(obs, nbr)
 
     def reset(self):

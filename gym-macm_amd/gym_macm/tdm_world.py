@@ -42,7 +42,7 @@ class TdmWorld:
     """E independent TDM envs of one configuration on one GPU. Output tensors are
     owned by this object and overwritten by every call."""
 
-    def __init__(self, cfg: _abi.MacmTdmConfig, n_envs: int = 1, device=None):
+    def __init__(self, cfg: _abi.MacmTdmConfig, n_envs: int = 1, device=None, host_outputs: bool = False):
         self.L = _abi.lib()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
@@ -61,13 +61,17 @@ class TdmWorld:
         self.h = h
         odt = torch.float64 if cfg.obs_f64 else torch.float32
         E, N = self.E, self.N
-        kw = dict(device=device)
+        # host_outputs: pinned host outputs written by the kernels (zero-copy dict API)
+        self.host_outputs = bool(host_outputs)
+        kw = dict(pin_memory=True) if self.host_outputs else dict(device=device)
         self.obs = torch.empty((E, N, N - 1, 4), dtype=odt, **kw)
         self.mask = torch.empty((E, N, N - 1), dtype=torch.uint8, **kw)
         self.health = torch.empty((E, N), dtype=torch.float64, **kw)
         self.alive = torch.empty((E, N), dtype=torch.uint8, **kw)
         self.done = torch.zeros((E,), dtype=torch.uint8, **kw)
         self.winner = torch.full((E,), -1, dtype=torch.int32, **kw)
+        if self.host_outputs:
+            self.done.zero_()
         self._out = _abi.MacmTdmOutputs(_ptr(self.obs), _ptr(self.mask), _ptr(self.health), _ptr(self.alive),
                                         _ptr(self.done), _ptr(self.winner))
         team = []
@@ -119,8 +123,10 @@ class TdmWorld:
 
     def step(self, actions: torch.Tensor):
         """actions: uint8 [E, N, 4] (forward, lateral, rotation, attack) on this device."""
-        if actions.device != self.device or not actions.is_contiguous():
-            raise ValueError("actions must be a contiguous tensor on the world's device")
+        pinned_ok = self.host_outputs and actions.device.type == "cpu" and actions.is_pinned()
+        if (actions.device != self.device and not pinned_ok) or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous tensor on the world's device (or pinned host "
+                             "memory with host_outputs)")
         if actions.dtype not in (torch.uint8, torch.int8) or tuple(actions.shape) != (self.E, self.N, 4):
             raise ValueError(f"TDM actions must be uint8 [{self.E},{self.N},4]")
         _abi.check(self.L.macm_tdm_step(self.h, _ptr(actions), ctypes.byref(self._out), self._stream()),

@@ -27,7 +27,7 @@ class World:
     """
 
     def __init__(self, cfg: _abi.MacmConfig, targets_idx=None, n_envs: int = 1, device=None,
-                 max_contacts: int = 0):
+                 max_contacts: int = 0, host_outputs: bool = False):
         self.L = _abi.lib()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
@@ -56,7 +56,10 @@ class World:
         self.OD = info.obs_dim
         self.C = info.max_contacts
         odt = torch.float64 if cfg.obs_f64 else torch.float32
-        kw = dict(device=device)
+        # host_outputs: outputs live in pinned host memory that the kernels write over
+        # the bus (zero-copy views for the small-E dict API; actions may be pinned too)
+        self.host_outputs = bool(host_outputs)
+        kw = dict(pin_memory=True) if self.host_outputs else dict(device=device)
         self.obs = torch.empty((self.E, self.N, self.OD), dtype=odt, **kw)
         self.nbr_id = torch.empty((self.E, self.N), dtype=torch.int32, **kw)
         self.reward = torch.empty((self.E, self.N), dtype=torch.float32, **kw)
@@ -114,8 +117,10 @@ class World:
     # -- hot path ------------------------------------------------------------
     def step(self, actions: torch.Tensor):
         """actions: discrete uint8/int8 [E,N,3] or continuous float32 [E,N,2], on this device."""
-        if actions.device != self.device or not actions.is_contiguous():
-            raise ValueError("actions must be a contiguous tensor on the world's device")
+        pinned_ok = self.host_outputs and actions.device.type == "cpu" and actions.is_pinned()
+        if (actions.device != self.device and not pinned_ok) or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous tensor on the world's device (or pinned host "
+                             "memory with host_outputs)")
         if self.cfg.action_mode == _abi.ACTION_DISCRETE:
             if actions.dtype not in (torch.uint8, torch.int8) or tuple(actions.shape) != (self.E, self.N, 3):
                 raise ValueError(f"discrete actions must be uint8/int8 [{self.E},{self.N},3]")

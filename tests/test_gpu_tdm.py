@@ -222,3 +222,22 @@ def test_dropin_tdm_matches_reference_goldens(name):
         assert env.time_passed == g["time_passed"][t]
         assert sorted(obs) == sorted(ag.id for ag in env.agents if ag.alive)
     assert sum(env.n_alive) == int(g["alive"][-1].sum())
+
+
+def test_host_outputs_equal_device_outputs():
+    """The zero-copy pinned-host outputs (dict API) hold the same values as device outputs."""
+    E, teams = 4, [6, 6]
+    wd = TdmWorld(tdm_config(teams, world_width=8.0, world_height=8.0), E, device="cuda:0")
+    wh = TdmWorld(tdm_config(teams, world_width=8.0, world_height=8.0), E, device="cuda:0", host_outputs=True)
+    wd.reset(3)
+    wh.reset(3)
+    rng = np.random.default_rng(0)
+    act_h = torch.empty((E, 12, 4), dtype=torch.uint8, pin_memory=True)
+    for t in range(60):
+        a = random_actions(rng, E, 12)
+        wd.step(torch.from_numpy(a).cuda())
+        act_h.numpy()[:] = a
+        wh.step(act_h)
+        torch.cuda.synchronize()
+        for x, y in zip(wd.outputs(), wh.outputs()):
+            np.testing.assert_array_equal(x.cpu().numpy(), y.numpy(), err_msg=f"step {t}")
