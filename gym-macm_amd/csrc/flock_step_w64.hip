@@ -299,13 +299,19 @@ __device__ __forceinline__ void sweep_step(const PairRec* s_pj, const PairRec q,
     const fvec2 d = mk2(q.c.x, q.c.y) - cme;  // other.position - agent.position
     const fvec2 dd = d * d;
     const float d2 = dd.x + dd.y;             // b2DistanceSquared(other, agent)
-    if (d2 < st.best && lane != J) {          // strict '<': lowest index wins ties (mvmnt.py:194)
-      st.best = d2;
-      st.bj = J;
-    }
-    // materialise the running minimum here: otherwise the compiler sinks all the
-    // distance work past the sweep and spills every record's position
-    asm volatile("" : "+v"(st.best), "+v"(st.bj));
+    // strict '<': lowest index wins ties (mvmnt.py:194); lane J (self) is cleared
+    // from the compare mask on the scalar unit. The asm also materialises the
+    // running minimum here (otherwise the compiler sinks the distance work past the
+    // sweep and spills every record's position).
+    asm volatile(
+        "v_cmp_lt_f32 vcc, %2, %0\n\t"
+        "s_bitset0_b64 vcc, %3\n\t"
+        "v_cndmask_b32 %0, %0, %2, vcc\n\t"
+        "v_cndmask_b32_e64 %1, %1, %3, vcc"
+        : "+v"(st.best), "+v"(st.bj)
+        : "v"(d2), "i"(J)
+        : "vcc");
+    (void)lane;
   }
   // keep the scheduler from hoisting every record's LDS read (register pressure)
   if constexpr ((J & 7) == 7) __builtin_amdgcn_sched_barrier(0);
