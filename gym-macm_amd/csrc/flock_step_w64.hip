@@ -509,8 +509,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
             attacking = true;
             // point2 = point1 + (range*cos(angle), range*sin(angle)): b2Vec2 + tuple is a
             // float32 add of the float32-converted tuple
-            ray_x = p.x + (float)(TP.melee_range * cos(ad));
-            ray_y = p.y + (float)(TP.melee_range * sin(ad));
+            ray_x = p.x + (float)(TP.melee_range * c0);  // c0 = cos(angle), s0 = sin(angle)
+            ray_y = p.y + (float)(TP.melee_range * s0);
             cda = TP.cooldown_atk;
             cdm = TP.cooldown_mov_penalty;
           }
