@@ -30,14 +30,25 @@ def rand_actions(rng, E, N):
     return rng.integers(0, 3, size=(E, N, 3)).astype(np.uint8)
 
 
-def check_rollout(vec, orc, steps, rng, state_every=1, actions_fn=None):
+def obs_check(gpu_obs, oracle_obs64, obs_f64, ctx):
+    """f32 obs: the oracle's f64 values rounded to f32 (<= 1 ulp, see parity.py);
+    f64 obs: within a few f64 ulp (goldens.obs_close)."""
+    if not obs_f64:
+        return f32_obs_mismatch(gpu_obs, oracle_obs64)
+    od = gpu_obs.shape[-1]
+    for e in range(gpu_obs.shape[0]):
+        assert goldens.obs_close(gpu_obs[e], oracle_obs64[e], od), f"obs {ctx} env {e}"
+    return 0
+
+
+def check_rollout(vec, orc, steps, rng, state_every=1, actions_fn=None, obs_f64=False):
     E, N = vec.num_envs, vec.N
     C = vec.world.C
     assert_state_equal(vec.get_state(), orc.get_state(C), "reset")
     vec.observe()
     o0, n0 = orc.observe()
     np.testing.assert_array_equal(vec.nbr_id.cpu().numpy(), n0)
-    f32_obs_mismatch(vec.obs.cpu().numpy(), o0)
+    obs_check(vec.obs.cpu().numpy(), o0, obs_f64, "reset")
     ulp_total = 0
     for t in range(steps):
         a = actions_fn(t) if actions_fn else rand_actions(rng, E, N)
@@ -47,7 +58,7 @@ def check_rollout(vec, orc, steps, rng, state_every=1, actions_fn=None):
         np.testing.assert_array_equal(nbr.cpu().numpy(), r["nbr_id"], err_msg=f"nbr step {t}")
         np.testing.assert_array_equal(done.cpu().numpy(), r["done"], err_msg=f"done step {t}")
         np.testing.assert_array_equal(vec.world.collided.cpu().numpy(), r["collided"], err_msg=f"coll step {t}")
-        ulp_total += f32_obs_mismatch(obs.cpu().numpy(), r["obs"])
+        ulp_total += obs_check(obs.cpu().numpy(), r["obs"], obs_f64, f"step {t}")
         if (t + 1) % state_every == 0 or t == steps - 1:
             assert_state_equal(vec.get_state(), orc.get_state(C), f"step {t}")
     assert vec.status() == 0
