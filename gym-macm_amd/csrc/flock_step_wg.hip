@@ -22,6 +22,22 @@ namespace wg {
 
 constexpr int W = 64;
 
+// Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
+// block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
+// --kernel wg). The product library compiles these to nothing.
+#ifdef MACM_STAMPS
+#define WSTAMP(k)                                                       \
+  do {                                                                  \
+    __builtin_amdgcn_s_waitcnt(0);                                      \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();         \
+    if (tid == 0) B.stamps[(size_t)e * 16 + (k)] = _t;                  \
+  } while (0)
+#else
+#define WSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
@@ -212,6 +228,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
   for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0;
   if (tid < 8) s_misc[tid] = 0;
   int status = 0;
+  WSTAMP(0);
 
   // ---- actions -> angle, force (mvmnt.py:97-129) ---------------------------------
   float Fx = 0.0f, Fy = 0.0f;
@@ -241,6 +258,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     Fy = 0.0f + Fy;
   }
   __syncthreads();
+  WSTAMP(1);
 
   // ---- Collide: ordered compaction of the touching contacts -----------------------
   const float rr = (P.radius + P.radius) * (P.radius + P.radius);
@@ -274,6 +292,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     T = tcap;
   }
   __syncthreads();
+  WSTAMP(2);
 
   // ---- CSR touching edges, each body's segment in list (= Box2D edge) order ---------
   // 16-bit counters packed in 32-bit LDS words
@@ -325,6 +344,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     }
   }
   __syncthreads();
+  WSTAMP(3);
 
   // ---- island DFS in Box2D order, serial on thread 0 ----------------------------------
   // Seeds: bodies with touching edges, highest index first (reverse creation order).
@@ -370,6 +390,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     s_misc[0] = nisl;
   }
   __syncthreads();
+  WSTAMP(4);
   const int nisl = s_misc[0];
   const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
 
@@ -411,6 +432,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     if (k < nord) s_ct[k] = stage[r];
   }
   __syncthreads();
+  WSTAMP(5);
 
   const float mA = P.inv_mass, mB = P.inv_mass;
   const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
@@ -472,6 +494,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     }
   }
   __syncthreads();
+  WSTAMP(6);
   for (int k = tid; k < nord; k += BS) {  // StoreImpulses, back in list order
     const Contact c = s_ct[k];
     g_lam[s_ord[k]] = make_float2(c.ln, c.lt);
@@ -525,6 +548,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     }
     s_isolv[I] = (uint8_t)solved;
   }
+  WSTAMP(7);
   // ---- sleep clock + island sleep decision --------------------------------------------------------
   float ns = 0.0f;
   if (act) {
@@ -542,6 +566,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     for (int k = b0; k < b1; ++k) s_flag[s_ibod[k]] = sl;
   }
   __syncthreads();
+  WSTAMP(8);
 
   // ---- SynchronizeFixtures ----------------------------------------------------------------------
   float4 fn = fo;
@@ -572,6 +597,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     s_rec[tid] = r0;
   }
   __syncthreads();
+  WSTAMP(9);
 
   // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour ----------------------------
   //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t); new contacts = Ov(F_t) \ Ov(F_{t-1})
@@ -595,6 +621,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
       if (j > tid && ovn && !overlap(fo, r.fo)) ++newcnt;
     }
   }
+  WSTAMP(10);
   // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs ------------------------
   uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
   float2* ocimp = B.cimp[nxt] + (size_t)e * C;
@@ -647,6 +674,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     total = C;
   }
 
+  WSTAMP(11);
   // ---- rewards + obs -----------------------------------------------------------------------------
   float rew = 0.0f;
   if (act) {
@@ -693,6 +721,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     ec[2] += (unsigned long long)npos;
     ec[3] += (unsigned long long)dn;
   }
+  WSTAMP(12);
 }
 
 // Reset for the workgroup variant: fat AABBs, first FindNewContacts list (all
@@ -729,6 +758,7 @@ __global__ __launch_bounds__(1024) void flock_init_wg(StepParams P, WorldBuffers
     s_rec[tid] = r0;
   }
   __syncthreads();
+  WSTAMP(9);
   int cnt = 0;
   float best = __builtin_inff();
   int bj = tid == 0 ? 1 : 0;

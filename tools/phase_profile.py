@@ -25,6 +25,10 @@ from gym_macm.vec import FlockVec  # noqa: E402
 PHASES = ["actions", "collide", "adjacency", "dfs+integrate+normals", "velocity_solve", "integrate_pos",
           "position_solve+sleepclk", "sleep_decision", "sync_fixtures", "pairs+nearest", "list_build",
           "reward+obs+writeback", "bookkeeping"]
+# flock_step_wg (N > 64): WSTAMP(0..12) in csrc/flock_step_wg.hip
+PHASES_WG = ["loads+actions", "collide", "csr+sort", "dfs", "integrate+records", "velocity_solve",
+             "impulses+integrate+position", "sleep", "sync_fixtures", "pairs+nearest", "list_build",
+             "reward+obs+writeback"]
 
 
 def main():
@@ -67,15 +71,24 @@ def main():
             deltas.append(np.diff(t, axis=1))
             stats.append(buf[:, 14:].copy())
     d = np.concatenate(deltas)  # [steps*E, 13]
+    phases = PHASES if N <= 64 else PHASES_WG
+    if N > 64:
+        d = d[:, :12]
     st = np.concatenate(stats)
     total = d.sum(axis=1)
     out = {"envs": E, "agents": N, "spread": args.spread, "policy": args.policy, "kernel_ms_stamped": float(np.mean(walls)),
            "wave_cycles_mean": float(total.mean()), "wave_cycles_p95": float(np.percentile(total, 95)),
            "wave_cycles_max": float(total.max()), "phases": {}}
-    for k, name in enumerate(PHASES):
+    for k, name in enumerate(phases):
         col = d[:, k]
         out["phases"][name] = {"mean": float(col.mean()), "p95": float(np.percentile(col, 95)),
                                "max": float(col.max()), "share": float(col.sum() / total.sum())}
+    if N > 64:  # the workgroup kernel records no size statistics
+        print(json.dumps(out, indent=1))
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(out, f, indent=1)
+        return
     T = (st[:, 0] & 0xFFFF).astype(np.int64)
     nisl = ((st[:, 0] >> 16) & 0xFFFF).astype(np.int64)
     M = (st[:, 0] >> 32).astype(np.int64)
