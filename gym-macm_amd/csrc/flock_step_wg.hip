@@ -48,6 +48,10 @@ __device__ __forceinline__ bool overlap(float4 a, float4 b) {  // b2TestOverlap
   if (d2x > 0.0f || d2y > 0.0f) return false;
   return true;
 }
+// max of the four AABB separations; > 0 iff b2TestOverlap(a, b) is false (finite boxes)
+__device__ __forceinline__ float sep_max(float4 a, float4 b) {
+  return fmaxf(fmaxf(b.x - a.z, b.y - a.w), fmaxf(a.x - b.z, a.y - b.w));
+}
 __device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Normalize
   const float len = sqrtf(x * x + y * y);
   if (len < kEps) return;
@@ -346,11 +350,13 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
   __syncthreads();
   WSTAMP(3);
 
+  // ---- island DFS in Box2D order ------------------------------------------------------
+  const bool par_dfs = 2 * T >= 4 * N;
   // ---- island DFS in Box2D order, serial on thread 0 ----------------------------------
   // Seeds: bodies with touching edges, highest index first (reverse creation order).
   // A body is "visited" once its s_todo bit is cleared; a contact once bit 31 of its
   // s_tab entry is set (b < 32768, so the bit is free).
-  if (tid == 0) {
+  if (!par_dfs && tid == 0) {
     int nord = 0, nisl = 0, nb = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
       const unsigned long long m = s_todo[w];
@@ -388,6 +394,74 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
     s_ic[nisl] = (uint16_t)nord;
     s_ib[nisl] = (uint16_t)nb;
     s_misc[0] = nisl;
+  }
+  // Dense worlds (average touching degree >= 4): the DFS on wave 0.
+  // Seeds: bodies with touching edges, highest index first (reverse creation order).
+  // A body is "visited" once its s_todo bit is cleared; a contact once bit 31 of its
+  // s_tab entry is set (b < 32768, so the bit is free). The edges of a popped body
+  // are taken together, one lane per edge: within one body's edge loop Box2D's
+  // decisions are independent (every edge has its own contact and its own other
+  // body), so ballot ranks in edge order reproduce its appends and pushes exactly.
+  if (par_dfs && tid < W) {
+    const int lane = tid;
+    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int nord = 0, nisl = 0, nb = 0;
+    for (int w = (N + 63) / 64 - 1; w >= 0;) {
+      const unsigned long long m = s_todo[w];
+      if (m == 0ull) {
+        --w;
+        continue;
+      }
+      const int sd = w * 64 + 63 - __clzll(m);
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        s_todo[w] = m & ~(1ull << (sd & 63));
+        s_ic[nisl] = (uint16_t)nord;
+        s_ib[nisl] = (uint16_t)nb;
+        s_stk[0] = (uint16_t)sd;
+      }
+      int sp = 1;
+      __builtin_amdgcn_wave_barrier();
+      while (sp > 0) {
+        const int bdy = s_stk[--sp];
+        if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
+        ++nb;
+        const int e0 = s_off[bdy], e1 = s_off[bdy + 1];
+        for (int q0 = e0; q0 < e1; q0 += W) {
+          const int q = q0 + lane;
+          bool newc = false, push = false;
+          int t = 0, o = 0;
+          uint32_t ab = 0u;
+          if (q < e1) {
+            t = s_adj[q];
+            ab = s_tab[t];
+            newc = !(ab & 0x80000000u);
+          }
+          const unsigned long long mc = __ballot(newc);
+          if (newc) {
+            s_tab[t] = ab | 0x80000000u;
+            s_ord[nord + __popcll(mc & lt)] = (uint16_t)t;
+            const int a = ab & 0xffffu, bb = ab >> 16;
+            o = (a == bdy) ? bb : a;
+            push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
+          }
+          nord += __popcll(mc);
+          const unsigned long long mp = __ballot(push);
+          if (push) {
+            atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
+            s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
+          }
+          sp += __popcll(mp);
+          __builtin_amdgcn_wave_barrier();  // stack / marks visible before the next read
+        }
+      }
+      ++nisl;
+    }
+    if (lane == 0) {
+      s_ic[nisl] = (uint16_t)nord;
+      s_ib[nisl] = (uint16_t)nb;
+      s_misc[0] = nisl;
+    }
   }
   __syncthreads();
   WSTAMP(4);
@@ -606,19 +680,20 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
   float best = __builtin_inff();
   int bj = tid == 0 ? 1 : 0;
   if (act) {
+#pragma unroll 4
     for (int j = 0; j < N; ++j) {
       const Rec r = s_rec[j];
-      const bool ovn = overlap(fn, r.fn);
+      // b2TestOverlap as one VALU test: separated iff max(lo_j - hi_i, lo_i - hi_j) > 0
+      const bool ovn = !(sep_max(fn, r.fn) > 0.0f);
       const float dx = r.c.x - cx, dy = r.c.y - cy;
       const float d2 = dx * dx + dy * dy;
-      if (j != tid) {
-        coll |= ovn;
-        if (d2 < best) {
-          best = d2;
-          bj = j;
-        }
+      const bool other = j != tid;
+      coll |= other && ovn;
+      if (other && d2 < best) {
+        best = d2;
+        bj = j;
       }
-      if (j > tid && ovn && !overlap(fo, r.fo)) ++newcnt;
+      if (j > tid && ovn && sep_max(fo, r.fo) > 0.0f) ++newcnt;
     }
   }
   WSTAMP(10);
