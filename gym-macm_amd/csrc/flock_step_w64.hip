@@ -198,7 +198,7 @@ __device__ __forceinline__ void tdm_obs_rows(OT* __restrict__ obs, uint8_t* __re
         const float rx = sx[j] - sx[i], ry = sy[j] - sy[i];  // other.position - agent.position
         const float d2 = rx * rx + ry * ry;                 // b2DistanceSquared(other, agent)
         r = sqrt((double)d2);
-        t = wrap_pi(atan2((double)ry, (double)rx) - (double)ai);
+        t = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)ai);
         p = wrap_pi((double)sa[j] - (double)ai);
         ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
       }
