@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "../../include/macm.h"
+#include "macm_math.h"
 
 namespace macm {
 
@@ -105,44 +106,22 @@ __host__ __device__ inline int tdm_team_of(const TdmParams& T, int i) {
   return t;
 }
 
-// atan2 for the TDM observation rows (combat.py:221). fdlibm's
-// atan reduction (e_atan2.c / s_atan.c) with the quotient folded into one division:
-// a = min(|x|,|y|) / max(|x|,|y|) is reduced by the selected (c_a*a - c_b)/(c_d*a + c_c)
-// without forming a (the 7/16 and 11/16 thresholds scale max exactly), an
-// 11-term Horner polynomial in FMA, then the octant/quadrant fix-ups with the split
-// constants (hi + lo). Measured against glibc atan2 on 2e7 float32-valued inputs:
-// <= 1 ulp, and identical after the observation's "- angle" and float32 rounding
-// (tools/atan2_check.c). About half the instructions of the general library atan2.
-// Used where atan2 is per pair (TDM: N-1 per agent, 39.8 -> 39.3 us/step at C4);
-// the Flock obs' two atan2 per agent stay on the library (A/B: 28.24 vs 28.37 us).
-__device__ __forceinline__ double obs_atan2(double y, double x) {
-  const double ax = fabs(x), ay = fabs(y);
-  const bool swap = ay > ax;
-  const double mx = swap ? ay : ax, mn = swap ? ax : ay;
-  const bool r0 = mn < 0.4375 * mx;   // id -1: atan(a) directly
-  const bool r1 = !r0 && mn < 0.6875 * mx;  // id 0: atan(1/2) + atan((2a-1)/(2+a)); else id 1: pi/4 + ...
-  const double ca = r1 ? 2.0 : 1.0, cb = r0 ? 0.0 : 1.0, cd = r0 ? 0.0 : 1.0;
-  const double xr = fma(ca, mn, -(cb * mx)) / fma(cd, mn, ca * mx);
-  const double z = xr * xr;
-  double p = 1.62858201153657823623e-02;
-  p = fma(p, z, -3.65315727442169155270e-02);
-  p = fma(p, z, 4.97687799461593236017e-02);
-  p = fma(p, z, -5.83357013379057348645e-02);
-  p = fma(p, z, 6.66107313738753120669e-02);
-  p = fma(p, z, -7.69187620504482999495e-02);
-  p = fma(p, z, 9.09088713343650656196e-02);
-  p = fma(p, z, -1.11111104054623557880e-01);
-  p = fma(p, z, 1.42857142725034663711e-01);
-  p = fma(p, z, -1.99999999998764832476e-01);
-  p = fma(p, z, 3.33333333333329318027e-01);
-  const double sz = z * p;
-  const double hi = r1 ? 4.63647609000806093515e-01 : 7.85398163397448278999e-01;
-  const double lo = r1 ? 2.26987774529616870924e-17 : 3.06161699786838301793e-17;
-  double r = r0 ? fma(-xr, sz, xr) : hi - (fma(xr, sz, -lo) - xr);
-  if (swap) r = (1.57079632679489655800e+00 - r) + 6.12323399573676603587e-17;
-  if (x < 0.0) r = (3.1415926535897931160e+00 - r) + 1.2246467991473531772e-16;
-  if (mx == 0.0) r = signbit(x) ? 3.1415926535897931160e+00 : 0.0;
-  return copysign(r, y);
+// sin/cos of the action angle and of angle + pi/2 (mvmnt.py:113-116, combat.py:147):
+// macm_action_trig (macm_math.h; its derived float32 forces and ray offsets equal glibc's
+// for every float32 angle |a| < 2^19, tools/trig_check.c) in that range, the device libm
+// beyond it (|angle| >= 2^19 only arises from injected state: the step wraps into [-pi, pi]).
+__device__ __forceinline__ void act_trig(float a, double* s0, double* c0, double* s1, double* c1) {
+#ifdef MACM_LIB_TRIG
+  sincos((double)a, s0, c0);
+  sincos((double)a + M_PI / 2, s1, c1);
+#else
+  if (fabsf(a) < 524288.0f) {
+    macm_action_trig(a, s0, c0, s1, c1);
+  } else {
+    sincos((double)a, s0, c0);
+    sincos((double)a + M_PI / 2, s1, c1);
+  }
+#endif
 }
 
 // Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).

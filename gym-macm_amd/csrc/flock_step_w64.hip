@@ -497,8 +497,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       // Agent.force = _force * (1 - percent_mov_penalty * int(cooldown_mov_penalty > 0))   combat.py:46-49
       if constexpr (kT) force = P.force * (1.0 - TP.percent_mov_penalty * (double)(cdm > 0.0));
       double s0, c0, s1, c1;  // np.cos / np.sin of angle and angle + pi/2 (one reduction each)
-      sincos(ad, &s0, &c0);
-      sincos(ad + M_PI / 2, &s1, &c1);
+      act_trig(af, &s0, &c0, &s1, &c1);
       const double fx = (c0 * k0 + c1 * k1) * cc * force;
       const double fy = (s0 * k0 + s1 * k1) * cc * force;
       Fx = (float)fx;  // ApplyForce: b2Vec2(float32) accumulated onto m_force = 0

@@ -247,8 +247,10 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
       ang = af;
       const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
       const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
-      Fx = (float)((cos(ad) * k0 + cos(ad + M_PI / 2) * k1) * cc * P.force);
-      Fy = (float)((sin(ad) * k0 + sin(ad + M_PI / 2) * k1) * cc * P.force);
+      double s0, c0, s1, c1;
+      act_trig(af, &s0, &c0, &s1, &c1);
+      Fx = (float)((c0 * k0 + c1 * k1) * cc * P.force);
+      Fy = (float)((s0 * k0 + s1 * k1) * cc * P.force);
     } else {
       float x = ax, y = ay;
       if ((x * x + y * y) > 1.0f) {
