@@ -66,6 +66,19 @@ struct WorldBuffers {
   unsigned long long* env_counters;  // [E, 4] per-env accumulators (see macm_world_counters)
   unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
   float2* scratch;               // [E, tcap] list-order impulses (workgroup kernel only)
+  // Workgroup path, split step (flock_step_wg_a -> flock_solve_wg -> flock_step_wg_c), per env:
+  float4* x_cst;                 // [E, tcap] island-ordered touching contacts (ab bits, nx, ny, 0)
+  float2* x_cimp;                // [E, tcap] their impulses (normal, tangent), island order
+  uint16_t* x_ord;               // [E, tcap] island order -> touching (list) rank
+  uint16_t* x_ic;                // [E, IS]   island contact ranges (IS = N/2 + 2)
+  uint16_t* x_ib;                // [E, IS]   island body ranges
+  uint16_t* x_ibod;              // [E, N]    island bodies
+  int32_t* x_nisl;               // [E]
+  float2* x_vmid;                // [E, N]    velocities after integration (solver input)
+  float2* x_cout;                // [E, N]    positions after the position solve
+  float2* x_vout;                // [E, N]    velocities after the solve (max-translation clamped)
+  uint8_t* x_deg;                // [E, N]    body has touching edges
+  uint8_t* x_isolv;              // [E, IS]   island position-solved
 };
 
 // Env modes of the wave-per-env kernel: same physics, different env layer.

@@ -62,7 +62,7 @@ __device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Norm
 __device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
 __device__ __forceinline__ double wrap_pi(double t) { return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t; }
 
-struct __align__(8) Rec {  // per-agent record for the pair sweep (40 B)
+struct __align__(16) Rec {  // per-agent record for the pair sweep (48 B with float4 alignment)
   float4 fn;               // new fat AABB
   float4 fo;               // old fat AABB
   float2 c;                // final position
@@ -114,7 +114,7 @@ __host__ __device__ inline WgLayout wg_layout(int N, int tcap) {
   L.region = o;
   const int part1 = align16(4 * tcap) + align16(2 * 2 * tcap);  // tab + adj
   const int part2 = align16(20 * tcap);                         // contacts (20 B)
-  const int part3 = align16(40 * N);                            // pair records (40 B)
+  const int part3 = align16((int)sizeof(wg::Rec) * N);          // pair records
   L.tab = L.region;
   L.adj = L.region + align16(4 * tcap);
   L.cont = L.region;
@@ -918,6 +918,823 @@ __global__ __launch_bounds__(1024) void flock_observe_wg(StepParams P, WorldBuff
   }
 }
 
+// ==== split step for large N =========================================================================
+// The fused kernel above keeps one env's whole world in LDS (up to ~134 KB at N = 1024), so a CU
+// holds one env, and while that env's single Gauss-Seidel lane walks a dense island the rest of
+// the CU idles. The split step runs the same algorithm as three launches:
+//   A  flock_step_wg_a : actions, Collide, CSR edges, island DFS, velocity integration, and the
+//                        island-ordered contact records written to HBM (x_cst / x_cimp).
+//   B  flock_solve_wg  : one wave per env, LDS = positions + velocities only (16 B per body):
+//                        warm start, velocity iterations, StoreImpulses, position integration,
+//                        position iterations. Contacts stream from HBM two records ahead
+//                        (islands of >= 3 contacts; smaller islands stay in registers).
+//   C  flock_step_wg_c : sleep, SynchronizeFixtures, pair sweep, next contact list, rewards, obs,
+//                        write-back.
+// Every arithmetic operation and its order are those of the fused kernel.
+
+struct WgLayoutA {
+  int c, deg, csr_off, todo, ord, ib, ibod, stk, ic, scan, misc, tab, adj, total;
+};
+__host__ __device__ inline WgLayoutA wg_layout_a(int N, int tcap) {
+  WgLayoutA L;
+  int o = 0;
+  auto take = [&](int bytes) {
+    int r = o;
+    o = align16(o + bytes);
+    return r;
+  };
+  L.c = take(8 * N);
+  L.deg = take(2 * (N + 2));
+  L.csr_off = take(2 * (N + 1));
+  L.todo = take(8 * ((N + 63) / 64));
+  L.ord = take(2 * tcap);
+  L.ib = take(2 * (N / 2 + 2));
+  L.ibod = take(2 * N);
+  L.stk = take(2 * N);
+  L.ic = take(2 * (N / 2 + 2));
+  L.scan = take(4 * 32);
+  L.misc = take(4 * 8);
+  L.tab = take(4 * tcap);
+  L.adj = take(4 * tcap);
+  L.total = o;
+  return L;
+}
+
+struct WgLayoutC {
+  int slp, flags, oldc, scan, misc, recs, total;
+};
+__host__ __device__ inline WgLayoutC wg_layout_c(int N) {
+  WgLayoutC L;
+  int o = 0;
+  auto take = [&](int bytes) {
+    int r = o;
+    o = align16(o + bytes);
+    return r;
+  };
+  L.slp = take(4 * N);
+  L.flags = take(N);
+  L.oldc = take(4 * ((N + 31) / 32));
+  L.scan = take(4 * 32);
+  L.misc = take(4 * 8);
+  L.recs = take((int)sizeof(wg::Rec) * N);
+  L.total = o;
+  return L;
+}
+
+__host__ __device__ inline int wg_isl_stride(int N) { return N / 2 + 2; }
+
+__global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffers B, int cur, int tcap,
+                                                        const void* __restrict__ actions) {
+  using namespace wg;
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int BS = blockDim.x;
+  const int N = P.n_agents;
+  const int C = P.max_contacts;
+  const bool act = tid < N;
+  const size_t ag = (size_t)e * N + tid;
+  const WgLayoutA L = wg_layout_a(N, tcap);
+  float2* s_c = (float2*)(lds + L.c);
+  uint16_t* s_deg = (uint16_t*)(lds + L.deg);
+  uint16_t* s_off = (uint16_t*)(lds + L.csr_off);
+  unsigned long long* s_todo = (unsigned long long*)(lds + L.todo);
+  uint16_t* s_ord = (uint16_t*)(lds + L.ord);
+  uint16_t* s_ib = (uint16_t*)(lds + L.ib);
+  uint16_t* s_ibod = (uint16_t*)(lds + L.ibod);
+  uint16_t* s_stk = (uint16_t*)(lds + L.stk);
+  uint16_t* s_ic = (uint16_t*)(lds + L.ic);
+  int* s_scan = (int*)(lds + L.scan);
+  int* s_misc = (int*)(lds + L.misc);
+  uint32_t* s_tab = (uint32_t*)(lds + L.tab);
+  uint16_t* s_adj = (uint16_t*)(lds + L.adj);
+  float2* g_lam = B.scratch + (size_t)e * tcap;
+
+  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
+  const float2* cimp = B.cimp[cur] + (size_t)e * C;
+  const int step_count = B.step_count[e];
+  const int M = B.ccount[cur][e];
+  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f);
+  float ang = 0.0f;
+  int a0 = 1, a1 = 1, a2 = 1;
+  float ax = 0.0f, ay = 0.0f;
+  if (act) {
+    p = B.pos[ag];
+    v = B.vel[ag];
+    ang = B.angle[ag];
+    if (P.action_mode == MACM_ACTION_DISCRETE) {
+      const uint8_t* a = (const uint8_t*)actions + ag * 3;
+      a0 = a[0]; a1 = a[1]; a2 = a[2];
+    } else {
+      const float2 c = ((const float2*)actions)[ag];
+      ax = c.x; ay = c.y;
+    }
+    s_c[tid] = p;
+  }
+  for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0;
+  if (tid < 8) s_misc[tid] = 0;
+  int status = 0;
+
+  // ---- actions -> angle, force (mvmnt.py:97-129) ---------------------------------
+  float Fx = 0.0f, Fy = 0.0f;
+  if (act) {
+    if (P.action_mode == MACM_ACTION_DISCRETE) {
+      float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
+      double ad = (double)af;
+      if (fabs(ad) > M_PI) {
+        af = (float)(ad - sgn(ad) * (2.0 * M_PI));
+        ad = (double)af;
+      }
+      ang = af;
+      const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
+      const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
+      double s0, c0, s1, c1;
+      act_trig(af, &s0, &c0, &s1, &c1);
+      Fx = (float)((c0 * k0 + c1 * k1) * cc * P.force);
+      Fy = (float)((s0 * k0 + s1 * k1) * cc * P.force);
+    } else {
+      float x = ax, y = ay;
+      if ((x * x + y * y) > 1.0f) {
+        x = sqrtf(x * x / (x * x + y * y));
+        y = sqrtf(y * y / (x * x + y * y));
+      }
+      Fx = x * P.force_f32;
+      Fy = y * P.force_f32;
+    }
+    Fx = 0.0f + Fx;
+    Fy = 0.0f + Fy;
+    B.angle[ag] = ang;  // kernel C reads it for the observation
+  }
+  __syncthreads();
+
+  // ---- Collide: ordered compaction of the touching contacts -----------------------
+  const float rr = (P.radius + P.radius) * (P.radius + P.radius);
+  const float dt_ratio = step_count > 0 ? P.inv_dt * P.dt : 0.0f;
+  int T = 0;
+  for (int k0 = 0; k0 < M; k0 += BS) {
+    const int k = k0 + tid;
+    bool touch = false;
+    uint32_t ab = 0u;
+    float2 lam = make_float2(0.0f, 0.0f);
+    if (k < M) {
+      ab = cab[k];
+      lam = cimp[k];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      const float2 pa = s_c[a], pb = s_c[b];
+      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
+      touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+    }
+    int pos;
+    const int n = block_scan_excl(touch ? 1 : 0, pos, s_scan);
+    if (touch && T + pos < tcap) {
+      s_tab[T + pos] = ab;
+      g_lam[T + pos] = P.warm_starting ? make_float2(dt_ratio * lam.x, dt_ratio * lam.y) : make_float2(0.0f, 0.0f);
+    }
+    T += n;
+  }
+  if (T > tcap) {
+    status |= MACM_ST_TOUCH_OVERFLOW;
+    T = tcap;
+  }
+  __syncthreads();
+
+  // ---- CSR touching edges, each body's segment in list (= Box2D edge) order ---------
+#define DEG_WORD(i) ((unsigned int*)(s_deg + ((i) & ~1)))
+#define DEG_INC(i) (((i) & 1) ? 0x10000u : 1u)
+#define DEG_GET(w, i) (((i) & 1) ? ((w) >> 16) : ((w) & 0xffffu))
+  for (int t = tid; t < T; t += BS) {
+    const uint32_t ab = s_tab[t];
+    const int a = ab & 0xffffu, b = ab >> 16;
+    atomicAdd(DEG_WORD(a), DEG_INC(a));
+    atomicAdd(DEG_WORD(b), DEG_INC(b));
+  }
+  __syncthreads();
+  const int deg = act ? (int)s_deg[tid] : 0;
+  {
+    int off;
+    block_scan_excl(deg, off, s_scan);
+    if (act) s_off[tid] = (uint16_t)off;
+    if (tid == 0) s_off[N] = (uint16_t)(2 * T);
+    const unsigned long long m = __ballot(act && deg > 0);
+    if ((tid & (W - 1)) == 0 && tid / W < (N + 63) / 64) s_todo[tid / W] = m;
+  }
+  __syncthreads();
+  if (act) s_deg[tid] = s_off[tid];
+  __syncthreads();
+  for (int t = tid; t < T; t += BS) {
+    const uint32_t ab = s_tab[t];
+    const int a = ab & 0xffffu, b = ab >> 16;
+    const unsigned wa = atomicAdd(DEG_WORD(a), DEG_INC(a));
+    const unsigned wb = atomicAdd(DEG_WORD(b), DEG_INC(b));
+    s_adj[DEG_GET(wa, a)] = (uint16_t)t;
+    s_adj[DEG_GET(wb, b)] = (uint16_t)t;
+  }
+#undef DEG_WORD
+#undef DEG_INC
+#undef DEG_GET
+  __syncthreads();
+  if (act && deg > 1) {
+    const int o0 = s_off[tid];
+    for (int x = o0 + 1; x < o0 + deg; ++x) {
+      const uint16_t key = s_adj[x];
+      int y = x - 1;
+      while (y >= o0 && s_adj[y] > key) {
+        s_adj[y + 1] = s_adj[y];
+        --y;
+      }
+      s_adj[y + 1] = key;
+    }
+  }
+  __syncthreads();
+
+  // ---- island DFS in Box2D order (as in flock_step_wg) ---------------------------------
+  const bool par_dfs = 2 * T >= 4 * N;
+  if (!par_dfs && tid == 0) {
+    int nord = 0, nisl = 0, nb = 0;
+    for (int w = (N + 63) / 64 - 1; w >= 0;) {
+      const unsigned long long m = s_todo[w];
+      if (m == 0ull) {
+        --w;
+        continue;
+      }
+      const int s = w * 64 + 63 - __clzll(m);
+      s_todo[w] = m & ~(1ull << (s & 63));
+      s_ic[nisl] = (uint16_t)nord;
+      s_ib[nisl] = (uint16_t)nb;
+      int sp = 0;
+      s_stk[sp++] = (uint16_t)s;
+      while (sp > 0) {
+        const int b = s_stk[--sp];
+        s_ibod[nb++] = (uint16_t)b;
+        const int e0 = s_off[b], e1 = s_off[b + 1];
+        for (int q = e0; q < e1; ++q) {
+          const int t = s_adj[q];
+          const uint32_t ab = s_tab[t];
+          if (ab & 0x80000000u) continue;
+          s_tab[t] = ab | 0x80000000u;
+          s_ord[nord++] = (uint16_t)t;
+          const int a = ab & 0xffffu, bb = ab >> 16;
+          const int o = (a == b) ? bb : a;
+          const unsigned long long ob = 1ull << (o & 63);
+          const unsigned long long tw = s_todo[o >> 6];
+          if (!(tw & ob)) continue;
+          s_todo[o >> 6] = tw & ~ob;
+          s_stk[sp++] = (uint16_t)o;
+        }
+      }
+      ++nisl;
+    }
+    s_ic[nisl] = (uint16_t)nord;
+    s_ib[nisl] = (uint16_t)nb;
+    s_misc[0] = nisl;
+  }
+  if (par_dfs && tid < W) {
+    const int lane = tid;
+    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int nord = 0, nisl = 0, nb = 0;
+    for (int w = (N + 63) / 64 - 1; w >= 0;) {
+      const unsigned long long m = s_todo[w];
+      if (m == 0ull) {
+        --w;
+        continue;
+      }
+      const int sd = w * 64 + 63 - __clzll(m);
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        s_todo[w] = m & ~(1ull << (sd & 63));
+        s_ic[nisl] = (uint16_t)nord;
+        s_ib[nisl] = (uint16_t)nb;
+        s_stk[0] = (uint16_t)sd;
+      }
+      int sp = 1;
+      __builtin_amdgcn_wave_barrier();
+      while (sp > 0) {
+        const int bdy = s_stk[--sp];
+        if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
+        ++nb;
+        const int e0 = s_off[bdy], e1 = s_off[bdy + 1];
+        for (int q0 = e0; q0 < e1; q0 += W) {
+          const int q = q0 + lane;
+          bool newc = false, push = false;
+          int t = 0, o = 0;
+          uint32_t ab = 0u;
+          if (q < e1) {
+            t = s_adj[q];
+            ab = s_tab[t];
+            newc = !(ab & 0x80000000u);
+          }
+          const unsigned long long mc = __ballot(newc);
+          if (newc) {
+            s_tab[t] = ab | 0x80000000u;
+            s_ord[nord + __popcll(mc & lt)] = (uint16_t)t;
+            const int a = ab & 0xffffu, bb = ab >> 16;
+            o = (a == bdy) ? bb : a;
+            push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
+          }
+          nord += __popcll(mc);
+          const unsigned long long mp = __ballot(push);
+          if (push) {
+            atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
+            s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
+          }
+          sp += __popcll(mp);
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      ++nisl;
+    }
+    if (lane == 0) {
+      s_ic[nisl] = (uint16_t)nord;
+      s_ib[nisl] = (uint16_t)nb;
+      s_misc[0] = nisl;
+    }
+  }
+  __syncthreads();
+  const int nisl = s_misc[0];
+  const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
+
+  // ---- integrate velocities; island-ordered contact records with normals -> HBM --------
+  const int IS = wg_isl_stride(N);
+  if (act) {
+    const float vx = v.x + P.dt * (0.0f + P.inv_mass * Fx);
+    const float vy = v.y + P.dt * (0.0f + P.inv_mass * Fy);
+    B.x_vmid[ag] = make_float2(vx * P.damp, vy * P.damp);
+    B.x_deg[ag] = deg > 0 ? 1 : 0;
+    B.x_ibod[ag] = s_ibod[tid];
+  }
+  float4* xc = B.x_cst + (size_t)e * tcap;
+  float2* xi = B.x_cimp + (size_t)e * tcap;
+  uint16_t* xo = B.x_ord + (size_t)e * tcap;
+  for (int k = tid; k < nord; k += BS) {
+    const int t = s_ord[k];
+    const uint32_t ab = s_tab[t] & 0x7fffffffu;
+    const int a = ab & 0xffffu, b = ab >> 16;
+    const float2 pa = s_c[a], pb = s_c[b];
+    float nx = 1.0f, ny = 0.0f;
+    const float ddx = pa.x - pb.x, ddy = pa.y - pb.y;
+    if (ddx * ddx + ddy * ddy > kEps * kEps) {
+      nx = pb.x - pa.x;
+      ny = pb.y - pa.y;
+      normalize(nx, ny);
+    }
+    xc[k] = make_float4(__uint_as_float(ab), nx, ny, 0.0f);
+    xi[k] = g_lam[t];
+    xo[k] = (uint16_t)t;
+  }
+  for (int q = tid; q <= nisl; q += BS) {
+    B.x_ic[(size_t)e * IS + q] = s_ic[q];
+    B.x_ib[(size_t)e * IS + q] = s_ib[q];
+  }
+  if (tid == 0) {
+    B.x_nisl[e] = nisl;
+    if (status) B.status[e] |= status;
+  }
+}
+
+namespace wg {
+
+// One Gauss-Seidel velocity constraint (b2ContactSolver::SolveVelocityConstraints, one point,
+// fixedRotation bodies): the fused kernel's arithmetic.
+__device__ __forceinline__ void gs_velocity(float2& va, float2& vb, float nx, float ny, float& ln, float& ltg,
+                                            float mA, float mB, float kmass, float friction) {
+  const float tx = ny, ty = -nx;
+  {
+    const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+    const float vt = dvx * tx + dvy * ty;
+    float lambda = kmass * (-vt);
+    const float maxf = friction * ln;
+    const float ni = bclamp(ltg + lambda, -maxf, maxf);
+    lambda = ni - ltg;
+    ltg = ni;
+    const float Px = lambda * tx, Py = lambda * ty;
+    va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+    vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+  }
+  {
+    const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+    const float vn = dvx * nx + dvy * ny;
+    float lambda = -kmass * (vn - 0.0f);
+    const float ni = bmax(ln + lambda, 0.0f);
+    lambda = ni - ln;
+    ln = ni;
+    const float Px = lambda * nx, Py = lambda * ny;
+    va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+    vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+  }
+}
+
+__device__ __forceinline__ void gs_warm(float2& va, float2& vb, float nx, float ny, float ln, float lt, float mA,
+                                        float mB) {
+  const float tx = ny, ty = -nx;
+  const float Px = ln * nx + lt * tx, Py = ln * ny + lt * ty;
+  va.x = va.x - mA * Px;
+  va.y = va.y - mA * Py;
+  vb.x = vb.x + mB * Px;
+  vb.y = vb.y + mB * Py;
+}
+
+// b2PositionSolverManifold + one position-constraint correction; returns the separation.
+__device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radius, float mA, float mB) {
+  float nx = cb.x - ca.x, ny = cb.y - ca.y;
+  normalize(nx, ny);
+  const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
+  const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+  const float K = mA + mB;
+  const float imp = K > 0.0f ? -Cc / K : 0.0f;
+  const float Px = imp * nx, Py = imp * ny;
+  ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
+  cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
+  return sep;
+}
+
+}  // namespace wg
+
+__global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap) {
+  using namespace wg;
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int e = blockIdx.x, lane = threadIdx.x, N = P.n_agents;
+  float2* s_v = (float2*)lds;
+  float2* s_c = s_v + N;
+  const size_t en = (size_t)e * N;
+  const int IS = wg_isl_stride(N);
+  const float4* cst = B.x_cst + (size_t)e * tcap;
+  const uint32_t* cab = (const uint32_t*)cst;  // .x of each record, stride 4 words
+  float2* cimp = B.x_cimp + (size_t)e * tcap;
+  const uint16_t* ic = B.x_ic + (size_t)e * IS;
+  for (int i = lane; i < N; i += W) {
+    s_c[i] = B.pos[en + i];
+    s_v[i] = B.x_vmid[en + i];
+  }
+  const int nisl = B.x_nisl[e];
+  __syncthreads();
+  const float mA = P.inv_mass, mB = P.inv_mass;
+  const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
+  const float friction = P.friction;
+
+  // ---- warm start + velocity iterations, one lane per island ------------------------------------
+  for (int I = lane; I < nisl; I += W) {
+    const int c0 = ic[I], c1 = ic[I + 1];
+    const int len = c1 - c0;
+    if (len <= 2) {  // records and impulses in registers
+      const float4 r0 = cst[c0], r1 = len == 2 ? cst[c0 + 1] : r0;
+      float2 i0 = cimp[c0], i1 = len == 2 ? cimp[c0 + 1] : i0;
+      const uint32_t ab0 = __float_as_uint(r0.x), ab1 = __float_as_uint(r1.x);
+      const int a0 = ab0 & 0xffffu, b0 = ab0 >> 16, a1 = ab1 & 0xffffu, b1 = ab1 >> 16;
+      if (P.warm_starting) {
+        float2 va = s_v[a0], vb = s_v[b0];
+        gs_warm(va, vb, r0.y, r0.z, i0.x, i0.y, mA, mB);
+        s_v[a0] = va;
+        s_v[b0] = vb;
+        if (len == 2) {
+          va = s_v[a1];
+          vb = s_v[b1];
+          gs_warm(va, vb, r1.y, r1.z, i1.x, i1.y, mA, mB);
+          s_v[a1] = va;
+          s_v[b1] = vb;
+        }
+      }
+      for (int it = 0; it < P.vel_iters; ++it) {
+        float2 va = s_v[a0], vb = s_v[b0];
+        gs_velocity(va, vb, r0.y, r0.z, i0.x, i0.y, mA, mB, kmass, friction);
+        s_v[a0] = va;
+        s_v[b0] = vb;
+        if (len == 2) {
+          va = s_v[a1];
+          vb = s_v[b1];
+          gs_velocity(va, vb, r1.y, r1.z, i1.x, i1.y, mA, mB, kmass, friction);
+          s_v[a1] = va;
+          s_v[b1] = vb;
+        }
+      }
+      cimp[c0] = i0;
+      if (len == 2) cimp[c0 + 1] = i1;
+      continue;
+    }
+    if (P.warm_starting) {
+      float4 rn = cst[c0];
+      float2 in = cimp[c0];
+      for (int k = c0; k < c1; ++k) {
+        const float4 r = rn;
+        const float2 im = in;
+        if (k + 1 < c1) {
+          rn = cst[k + 1];
+          in = cimp[k + 1];
+        }
+        const uint32_t ab = __float_as_uint(r.x);
+        const int a = ab & 0xffffu, b = ab >> 16;
+        float2 va = s_v[a], vb = s_v[b];
+        gs_warm(va, vb, r.y, r.z, im.x, im.y, mA, mB);
+        s_v[a] = va;
+        s_v[b] = vb;
+      }
+    }
+    // Velocity passes flattened into one stream of nq = iters * len contact solves. The record
+    // for solve q + 2 is loaded at solve q; with len >= 3 it is a different contact from
+    // solves q and q + 1, so its impulses are final when loaded (their store came one pass
+    // earlier from this lane).
+    const int nq = P.vel_iters * len;
+    int k0 = c0, k1 = c0 + 1, k2 = c0 + 2;
+    float4 r0 = cst[k0], r1 = cst[k1], r2;
+    float2 i0 = cimp[k0], i1 = cimp[k1], i2;
+#define VSTEP(X, Y, Z)                                              \
+  {                                                                 \
+    if (q == nq) break;                                             \
+    k##Z = k##Y + 1 < c1 ? k##Y + 1 : c0;                           \
+    r##Z = cst[k##Z];                                               \
+    i##Z = cimp[k##Z];                                              \
+    const uint32_t ab = __float_as_uint(r##X.x);                    \
+    const int a = ab & 0xffffu, b = ab >> 16;                       \
+    float2 va = s_v[a], vb = s_v[b];                                \
+    gs_velocity(va, vb, r##X.y, r##X.z, i##X.x, i##X.y, mA, mB, kmass, friction); \
+    s_v[a] = va;                                                    \
+    s_v[b] = vb;                                                    \
+    cimp[k##X] = i##X;                                              \
+    ++q;                                                            \
+  }
+    for (int q = 0;;) {
+      VSTEP(0, 1, 2)
+      VSTEP(1, 2, 0)
+      VSTEP(2, 0, 1)
+    }
+#undef VSTEP
+  }
+  __syncthreads();
+
+  // ---- StoreImpulses back in list order; integrate positions ----------------------------------
+  const int nord = nisl > 0 ? (int)ic[nisl] : 0;
+  {
+    const uint16_t* ord = B.x_ord + (size_t)e * tcap;
+    float2* g_lam = B.scratch + (size_t)e * tcap;
+    for (int k = lane; k < nord; k += W) g_lam[ord[k]] = cimp[k];
+  }
+  for (int i = lane; i < N; i += W) {
+    const float2 vv = s_v[i];
+    float vx = vv.x, vy = vv.y;
+    const float tx = P.dt * vx, ty = P.dt * vy;
+    if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
+      const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
+      vx = vx * ratio;
+      vy = vy * ratio;
+    }
+    const float2 c = s_c[i];
+    s_c[i] = make_float2(c.x + P.dt * vx, c.y + P.dt * vy);
+    B.x_vout[en + i] = make_float2(vx, vy);
+  }
+  __syncthreads();
+
+  // ---- position iterations, one lane per island ---------------------------------------------
+  uint8_t* isolv = B.x_isolv + (size_t)e * IS;
+  for (int I = lane; I < nisl; I += W) {
+    const int c0 = ic[I], c1 = ic[I + 1];
+    int solved = 0;
+    uint32_t abn = cab[4 * c0];
+    for (int it = 0; it < P.pos_iters; ++it) {
+      float min_sep = 0.0f;
+      for (int k = c0; k < c1; ++k) {
+        const uint32_t ab = abn;
+        abn = cab[4 * (k + 1 < c1 ? k + 1 : c0)];
+        const int a = ab & 0xffffu, b = ab >> 16;
+        float2 ca = s_c[a], cb = s_c[b];
+        const float sep = gs_position(ca, cb, P.radius, mA, mB);
+        min_sep = bmin(min_sep, sep);
+        s_c[a] = ca;
+        s_c[b] = cb;
+      }
+      if (min_sep >= -3.0f * kLinearSlop) {
+        solved = 1;
+        break;
+      }
+    }
+    isolv[I] = (uint8_t)solved;
+  }
+  __syncthreads();
+  for (int i = lane; i < N; i += W) B.x_cout[en + i] = s_c[i];
+}
+
+template <typename OT>
+__global__ __launch_bounds__(1024) void flock_step_wg_c(StepParams P, WorldBuffers B, int cur, int tcap,
+                                                        OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
+                                                        float* __restrict__ rew_out, uint8_t* __restrict__ coll_out,
+                                                        uint8_t* __restrict__ done_out) {
+  using namespace wg;
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int BS = blockDim.x;
+  const int N = P.n_agents;
+  const int C = P.max_contacts;
+  const bool act = tid < N;
+  const size_t ag = (size_t)e * N + tid;
+  const int nxt = cur ^ 1;
+  const WgLayoutC L = wg_layout_c(N);
+  float* s_slp = (float*)(lds + L.slp);
+  uint8_t* s_flag = (uint8_t*)(lds + L.flags);
+  uint32_t* s_oldc = (uint32_t*)(lds + L.oldc);
+  int* s_scan = (int*)(lds + L.scan);
+  int* s_misc = (int*)(lds + L.misc);
+  Rec* s_rec = (Rec*)(lds + L.recs);
+  const float2* g_lam = B.scratch + (size_t)e * tcap;
+  const int IS = wg_isl_stride(N);
+
+  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
+  const int step_count = B.step_count[e];
+  const int M = B.ccount[cur][e];
+  const int nisl = B.x_nisl[e];
+  float2 p = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
+  float ang = 0.0f, slp = 0.0f, cx = 0.0f, cy = 0.0f, vx = 0.0f, vy = 0.0f;
+  float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  bool hasdeg = false;
+  if (act) {
+    p = B.pos[ag];
+    ang = B.angle[ag];
+    fo = B.fat[ag];
+    slp = B.sleep[ag];
+    const float2 c = B.x_cout[ag], vv = B.x_vout[ag];
+    cx = c.x; cy = c.y; vx = vv.x; vy = vv.y;
+    hasdeg = B.x_deg[ag] != 0;
+    tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
+  }
+  for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
+  if (tid < 8) s_misc[tid] = 0;
+  int status = 0;
+  __syncthreads();
+  for (int k = tid; k < M; k += BS) {  // agents in the old list (world.contacts before the step)
+    const uint32_t ab = cab[k];
+    const int a = ab & 0xffffu, b = ab >> 16;
+    atomicOr(&s_oldc[a >> 5], 1u << (a & 31));
+    atomicOr(&s_oldc[b >> 5], 1u << (b & 31));
+  }
+
+  // ---- sleep clock + island sleep decision --------------------------------------------------------
+  float ns = 0.0f;
+  if (act) {
+    const bool moving = vx * vx + vy * vy > kLinearSleepTol * kLinearSleepTol;
+    ns = moving ? 0.0f : slp + P.dt;
+    s_slp[tid] = ns;
+    s_flag[tid] = (!hasdeg && ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
+  }
+  __syncthreads();
+  {
+    const uint16_t* ib = B.x_ib + (size_t)e * IS;
+    const uint16_t* ibod = B.x_ibod + (size_t)e * N;
+    const uint8_t* isolv = B.x_isolv + (size_t)e * IS;
+    for (int I = tid; I < nisl; I += BS) {
+      const int b0 = ib[I], b1 = ib[I + 1];
+      float mn = 3.402823466e+38f;
+      for (int k = b0; k < b1; ++k) mn = bmin(mn, s_slp[ibod[k]]);
+      const uint8_t sl = (mn >= kTimeToSleep && isolv[I]) ? 1 : 0;
+      for (int k = b0; k < b1; ++k) s_flag[ibod[k]] = sl;
+    }
+  }
+  __syncthreads();
+
+  // ---- SynchronizeFixtures ----------------------------------------------------------------------
+  float4 fn = fo;
+  if (act) {
+    const float r = P.radius;
+    const float c0x = p.x, c0y = p.y;
+    const float lox = bmin(c0x - r, cx - r), loy = bmin(c0y - r, cy - r);
+    const float hix = bmax(c0x + r, cx + r), hiy = bmax(c0y + r, cy + r);
+    const bool contains = fo.x <= lox && fo.y <= loy && hix <= fo.z && hiy <= fo.w;
+    if (!contains) {
+      fn = make_float4(lox - kAabbExtension, loy - kAabbExtension, hix + kAabbExtension, hiy + kAabbExtension);
+      const float dx = kAabbMultiplier * (cx - c0x), dy = kAabbMultiplier * (cy - c0y);
+      if (dx < 0.0f) fn.x += dx; else fn.z += dx;
+      if (dy < 0.0f) fn.y += dy; else fn.w += dy;
+    }
+    if (s_flag[tid]) {
+      vx = 0.0f;
+      vy = 0.0f;
+      ns = 0.0f;
+    }
+    Rec r0;
+    r0.fn = fn;
+    r0.fo = fo;
+    r0.c = make_float2(cx, cy);
+    s_rec[tid] = r0;
+  }
+  __syncthreads();
+
+  // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour ----------------------------
+  bool coll = act && ((s_oldc[tid >> 5] >> (tid & 31)) & 1u);
+  int newcnt = 0;
+  float best = __builtin_inff();
+  int bj = tid == 0 ? 1 : 0;
+  if (act) {
+#pragma unroll 4
+    for (int j = 0; j < N; ++j) {
+      const Rec r = s_rec[j];
+      const bool ovn = !(sep_max(fn, r.fn) > 0.0f);
+      const float dx = r.c.x - cx, dy = r.c.y - cy;
+      const float d2 = dx * dx + dy * dy;
+      const bool other = j != tid;
+      coll |= other && ovn;
+      if (other && d2 < best) {
+        best = d2;
+        bj = j;
+      }
+      if (j > tid && ovn && sep_max(fo, r.fo) > 0.0f) ++newcnt;
+    }
+  }
+  // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs ------------------------
+  uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
+  float2* ocimp = B.cimp[nxt] + (size_t)e * C;
+  int excl;
+  const int nnew = block_scan_excl(newcnt, excl, s_scan);
+  if (act && newcnt > 0) {
+    int w = nnew - excl - newcnt;
+    for (int j = N - 1; j > tid; --j) {
+      const Rec r = s_rec[j];
+      if (overlap(fn, r.fn) && !overlap(fo, r.fo)) {
+        if (w < C) {
+          ocab[w] = (uint32_t)tid | ((uint32_t)j << 16);
+          ocimp[w] = make_float2(0.0f, 0.0f);
+        }
+        ++w;
+      }
+    }
+  }
+  const float rr = (P.radius + P.radius) * (P.radius + P.radius);
+  int kept = 0, Tr = 0;
+  for (int k0 = 0; k0 < M; k0 += BS) {
+    const int k = k0 + tid;
+    bool keep = false, touch = false;
+    uint32_t ab = 0u;
+    if (k < M) {
+      ab = cab[k];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      keep = overlap(s_rec[a].fn, s_rec[b].fn);
+      const float2 pa = B.pos[(size_t)e * N + a], pb = B.pos[(size_t)e * N + b];
+      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
+      touch = !(dx * dx + dy * dy > rr);
+    }
+    int tpos, kpos;
+    const int tn = block_scan_excl(touch ? 1 : 0, tpos, s_scan);
+    const int kn = block_scan_excl(keep ? 1 : 0, kpos, s_scan);
+    if (keep) {
+      const int w = nnew + kept + kpos;
+      const int trank = Tr + tpos;
+      if (w < C) {
+        ocab[w] = ab;
+        ocimp[w] = (touch && trank < tcap) ? g_lam[trank] : make_float2(0.0f, 0.0f);
+      }
+    }
+    Tr += tn;
+    kept += kn;
+  }
+  int total = nnew + kept;
+  if (total > C) {
+    status |= MACM_ST_CONTACT_OVERFLOW;
+    total = C;
+  }
+
+  // ---- rewards + obs -----------------------------------------------------------------------------
+  float rew = 0.0f;
+  if (act) {
+    const float tdx = tg.x - cx, tdy = tg.y - cy;
+    const float td2 = tdx * tdx + tdy * tdy;
+    const double d = sqrt((double)td2);
+    if (coll) rew = -1.0f;
+    else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
+    else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
+    rew_out[ag] = rew;
+    if (coll_out) coll_out[ag] = coll ? 1 : 0;
+    if (nbr_out) nbr_out[ag] = bj;
+    if (obs) {
+      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+      const float2 cb = s_rec[bj].c;
+      write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
+    }
+  }
+  int dummy;
+  const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);
+  const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);
+  if (status) atomicOr(&s_misc[1], status);
+  __syncthreads();
+  if (act) {
+    B.pos[ag] = make_float2(cx, cy);
+    B.vel[ag] = make_float2(vx, vy);
+    B.fat[ag] = fn;
+    B.sleep[ag] = ns;
+  }
+  if (tid == 0) {
+    const int nst = s_misc[1];
+    const double tp = B.time_passed[e] + P.inv_hz;
+    const uint8_t dn = tp > P.time_limit ? 1 : 0;
+    B.time_passed[e] = tp;
+    B.done[e] = dn;
+    if (done_out) done_out[e] = dn;
+    B.step_count[e] = step_count + 1;
+    B.ccount[nxt][e] = total;
+    if (nst) B.status[e] |= nst;
+    unsigned long long* ec = B.env_counters + (size_t)e * 4;
+    ec[0] += (unsigned long long)N;
+    ec[1] += (unsigned long long)ncoll;
+    ec[2] += (unsigned long long)npos;
+    ec[3] += (unsigned long long)dn;
+  }
+}
+
 // ---- launchers -------------------------------------------------------------------------------------
 int wg_block(int N) { return ((N + 63) / 64) * 64; }
 int wg_lds_bytes(int N, int tcap) { return wg_layout(N, tcap).total; }
@@ -933,14 +1750,40 @@ hipError_t wg_configure(int N, int tcap) {
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, step);
   for (const void* f : fi)
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, init);
+  const void* fsplit[] = {(const void*)flock_step_wg_a, (const void*)flock_solve_wg,
+                          (const void*)flock_step_wg_c<float>, (const void*)flock_step_wg_c<double>};
+  const int lsplit[] = {wg_layout_a(N, tcap).total, 16 * N, wg_layout_c(N).total, wg_layout_c(N).total};
+  for (int i = 0; i < 4; ++i)
+    if (e == hipSuccess) e = hipFuncSetAttribute(fsplit[i], hipFuncAttributeMaxDynamicSharedMemorySize, lsplit[i]);
   return e;
+}
+
+// The split step (kernels A, B, C above) unless MACM_WG_FUSED=1 (A/B comparisons).
+static bool wg_use_split() {
+  static const int v = [] {
+    const char* s = getenv("MACM_WG_FUSED");
+    return (s && s[0] == '1') ? 0 : 1;
+  }();
+  return v != 0;
 }
 
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
                           hipStream_t s) {
-  const int lds = wg_lds_bytes(P.n_agents, tcap);
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
+  if (wg_use_split()) {
+    const int N = P.n_agents, lc = wg_layout_c(N).total;
+    hipLaunchKernelGGL(flock_step_wg_a, grid, block, wg_layout_a(N, tcap).total, s, P, B, cur, tcap, actions);
+    hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), 16 * N, s, P, B, tcap);
+    if (obs_f64)
+      hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, s, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
+                         done);
+    else
+      hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, s, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
+                         done);
+    return hipGetLastError();
+  }
+  const int lds = wg_lds_bytes(P.n_agents, tcap);
   if (obs_f64)
     hipLaunchKernelGGL(flock_step_wg<double>, grid, block, lds, s, P, B, cur, tcap, actions, (double*)obs, nbr, rew,
                        coll, done);

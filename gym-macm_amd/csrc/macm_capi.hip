@@ -287,6 +287,15 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 16))
 #endif
       || (!w->wave && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap))) ||
+      (!w->wave && ((rc = dalloc(w, &B.x_cst, (size_t)n_envs * w->tcap)) ||
+                    (rc = dalloc(w, &B.x_cimp, (size_t)n_envs * w->tcap)) ||
+                    (rc = dalloc(w, &B.x_ord, (size_t)n_envs * w->tcap)) ||
+                    (rc = dalloc(w, &B.x_ic, (size_t)n_envs * (N / 2 + 2))) ||
+                    (rc = dalloc(w, &B.x_ib, (size_t)n_envs * (N / 2 + 2))) ||
+                    (rc = dalloc(w, &B.x_ibod, EN)) || (rc = dalloc(w, &B.x_nisl, (size_t)n_envs)) ||
+                    (rc = dalloc(w, &B.x_vmid, EN)) || (rc = dalloc(w, &B.x_cout, EN)) ||
+                    (rc = dalloc(w, &B.x_vout, EN)) || (rc = dalloc(w, &B.x_deg, EN)) ||
+                    (rc = dalloc(w, &B.x_isolv, (size_t)n_envs * (N / 2 + 2))))) ||
       (rc = dalloc(w, &w->mt, (size_t)n_envs * kMtStride)) || (rc = dalloc(w, &w->rmask, (size_t)n_envs))
   ) {
     free_world(w);

@@ -39,13 +39,15 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--spread", type=float, default=20.0)
     ap.add_argument("--policy", choices=("random", "bots"), default="random")
+    ap.add_argument("--flocks", type=int, default=1, help="targets = i * flocks // N (config 3: 4)")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     L = _abi.lib()
     L.macm_debug_stamps.restype = ctypes.c_int
     L.macm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     E, N = args.envs, args.agents
-    vec = FlockVec(E, n_agents=[N], seed=0x6D61636D, device="cuda:0", start_spread=args.spread)
+    targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
+    vec = FlockVec(E, n_agents=[N], targets=targets, seed=0x6D61636D, device="cuda:0", start_spread=args.spread)
     gen = torch.Generator(device="cuda:0")
     gen.manual_seed(1)
     buf = np.zeros((E, 16), np.uint64)
