@@ -151,8 +151,8 @@ __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
 template <typename OT>
 __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float best, float rx, float ry, float tdx,
                                           float tdy, float td2) {
-  const double t0 = wrap_pi(atan2((double)ry, (double)rx) - (double)ang);
-  const double t1 = wrap_pi(atan2((double)tdy, (double)tdx) - (double)ang);
+  const double t0 = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)ang);
+  const double t1 = wrap_pi(obs_atan2((double)tdy, (double)tdx) - (double)ang);
   const double r0 = sqrt((double)best), r1 = sqrt((double)td2);
   if (coord == MACM_COORD_CARTESIAN) {
     o[0] = (OT)r0; o[1] = (OT)cos(t0); o[2] = (OT)sin(t0);
@@ -982,6 +982,8 @@ __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
 }
 
 __host__ __device__ inline int wg_isl_stride(int N) { return N / 2 + 2; }
+// solver LDS: velocities + positions (16 B per body), record/impulse/ab rings, big-island list
+__host__ __device__ inline int wg_solve_lds(int N) { return 16 * N + 2 * 64 * (16 + 8 + 4) + 4 * (64 + 1); }
 
 __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffers B, int cur, int tcap,
                                                         const void* __restrict__ actions) {
@@ -1355,6 +1357,10 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   const int e = blockIdx.x, lane = threadIdx.x, N = P.n_agents;
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
+  float4* s_rr = (float4*)(s_c + N);               // [2][64] record ring (big islands)
+  float2* s_ri = (float2*)(s_rr + 2 * W);          // [2][64] impulse ring
+  uint32_t* s_ra = (uint32_t*)(s_ri + 2 * W);      // [2][64] ab ring (position passes)
+  int* s_big = (int*)(s_ra + 2 * W);               // [W] islands with >= kBig contacts, [W] = count
   const size_t en = (size_t)e * N;
   const int IS = wg_isl_stride(N);
   const float4* cst = B.x_cst + (size_t)e * tcap;
@@ -1366,15 +1372,30 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
     s_v[i] = B.x_vmid[en + i];
   }
   const int nisl = B.x_nisl[e];
+  if (lane == 0) s_big[W] = 0;
   __syncthreads();
+  const int tid = lane;  // for WSTAMP (slots 13..15, diagnostic build)
+  (void)tid;
+  WSTAMP(13);
   const float mA = P.inv_mass, mB = P.inv_mass;
   const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
   const float friction = P.friction;
 
   // ---- warm start + velocity iterations, one lane per island ------------------------------------
+  // Islands of >= kBig contacts (dense worlds: one island of thousands) are set aside for the
+  // chunked path below; the rest run one lane per island.
+  constexpr int kBig = 128;
+  bool len_overflow = false;
   for (int I = lane; I < nisl; I += W) {
     const int c0 = ic[I], c1 = ic[I + 1];
     const int len = c1 - c0;
+    if (len >= kBig) {  // solved below by the whole wave, one island at a time
+      const int slot = atomicAdd(&s_big[W], 1);
+      if (slot < W) s_big[slot] = I;
+      else len_overflow = true;
+    }
+    if (len >= kBig && !len_overflow) continue;
+    len_overflow = false;
     if (len <= 2) {  // records and impulses in registers
       const float4 r0 = cst[c0], r1 = len == 2 ? cst[c0 + 1] : r0;
       float2 i0 = cimp[c0], i1 = len == 2 ? cimp[c0 + 1] : i0;
@@ -1460,6 +1481,73 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   }
   __syncthreads();
 
+  // Big islands, one at a time: the solve stream (warm-start pass, then vel_iters passes) is cut
+  // into chunks of 64 solves. The wave loads chunk c + 2 (one record per lane, coalesced) while
+  // lane 0 solves chunk c out of an LDS ring, and writes chunk c's impulses back after it. A
+  // contact recurs len >= kBig = 2 * 64 solves later, i.e. at least two chunks on, whose loads
+  // are issued after this chunk's write-back.
+  const int nbig = __builtin_amdgcn_readfirstlane(s_big[W] < W ? s_big[W] : W);
+  for (int bi = 0; bi < nbig; ++bi) {
+    const int I = __builtin_amdgcn_readfirstlane(s_big[bi]);
+    const int c0 = __builtin_amdgcn_readfirstlane((int)ic[I]);
+    const int c1 = __builtin_amdgcn_readfirstlane((int)ic[I + 1]);
+    const int len = c1 - c0;
+    const int nw = P.warm_starting ? len : 0;
+    const int ns = nw + P.vel_iters * len;
+    const int nch = (ns + W - 1) / W;
+    // contact of this lane's solve in chunk c: c0 + (64 c + lane) mod len, kept incrementally
+    int kl = c0 + lane % len;
+    float4 vr = cst[kl];
+    float2 vi = cimp[kl];
+    s_rr[lane] = vr;
+    s_ri[lane] = vi;
+    int kl1 = kl + W % len;
+    if (kl1 >= c1) kl1 -= len;
+    if (nch > 1) {
+      vr = cst[kl1];
+      vi = cimp[kl1];
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      const int slot = (c & 1) * W;
+      if (lane == 0) {
+        const int s0 = c * W;
+        const int tn = ns - s0 < W ? ns - s0 : W;
+        for (int t = 0; t < tn; ++t) {
+          const float4 r = s_rr[slot + t];
+          const uint32_t ab = __float_as_uint(r.x);
+          const int a = ab & 0xffffu, b = ab >> 16;
+          float2 va = s_v[a], vb = s_v[b];
+          float2 im = s_ri[slot + t];
+          if (s0 + t < nw) {
+            gs_warm(va, vb, r.y, r.z, im.x, im.y, mA, mB);
+          } else {
+            gs_velocity(va, vb, r.y, r.z, im.x, im.y, mA, mB, kmass, friction);
+            s_ri[slot + t] = im;
+          }
+          s_v[a] = va;
+          s_v[b] = vb;
+        }
+      }
+      __syncthreads();
+      if (c * W + lane < ns) cimp[kl] = s_ri[slot + lane];  // this chunk's impulses back
+      int kl2 = kl1 + W % len;
+      if (kl2 >= c1) kl2 -= len;
+      if (c + 1 < nch) {  // ring <- chunk c + 1 (loaded a chunk ago), then load chunk c + 2
+        s_rr[(W - slot) + lane] = vr;
+        s_ri[(W - slot) + lane] = vi;
+        if (c + 2 < nch) {
+          vr = cst[kl2];
+          vi = cimp[kl2];
+        }
+      }
+      kl = kl1;
+      kl1 = kl2;
+      __syncthreads();
+    }
+  }
+
+  WSTAMP(14);
   // ---- StoreImpulses back in list order; integrate positions ----------------------------------
   const int nord = nisl > 0 ? (int)ic[nisl] : 0;
   {
@@ -1486,6 +1574,11 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   uint8_t* isolv = B.x_isolv + (size_t)e * IS;
   for (int I = lane; I < nisl; I += W) {
     const int c0 = ic[I], c1 = ic[I + 1];
+    if (c1 - c0 >= kBig) {
+      bool listed = false;
+      for (int q = 0; q < nbig; ++q) listed |= s_big[q] == I;
+      if (listed) continue;
+    }
     int solved = 0;
     uint32_t abn = cab[4 * c0];
     for (int it = 0; it < P.pos_iters; ++it) {
@@ -1508,11 +1601,67 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
     isolv[I] = (uint8_t)solved;
   }
   __syncthreads();
+  // Big islands: position passes (read-only records) through the same chunked ring; lane 0
+  // decides the early exit at each pass end.
+  for (int bi = 0; bi < nbig; ++bi) {
+    const int I = __builtin_amdgcn_readfirstlane(s_big[bi]);
+    const int c0 = __builtin_amdgcn_readfirstlane((int)ic[I]);
+    const int c1 = __builtin_amdgcn_readfirstlane((int)ic[I + 1]);
+    const int len = c1 - c0;
+    const int ns = P.pos_iters * len;
+    const int nch = (ns + W - 1) / W;
+    int kl = c0 + lane % len;
+    s_ra[lane] = cab[4 * kl];
+    int kl1 = kl + W % len;
+    if (kl1 >= c1) kl1 -= len;
+    uint32_t va = nch > 1 ? cab[4 * kl1] : 0u;
+    __syncthreads();
+    int solved = 0, done = 0;
+    float min_sep = 0.0f;
+    for (int c = 0; c < nch && !done; ++c) {
+      const int slot = (c & 1) * W;
+      if (lane == 0) {
+        const int s0 = c * W;
+        const int tn = ns - s0 < W ? ns - s0 : W;
+        int j = s0 % len;
+        for (int t = 0; t < tn; ++t) {
+          const uint32_t ab = s_ra[slot + t];
+          const int a = ab & 0xffffu, b = ab >> 16;
+          float2 ca = s_c[a], cb = s_c[b];
+          const float sep = gs_position(ca, cb, P.radius, mA, mB);
+          min_sep = bmin(min_sep, sep);
+          s_c[a] = ca;
+          s_c[b] = cb;
+          if (++j == len) {
+            j = 0;
+            if (min_sep >= -3.0f * kLinearSlop) {
+              solved = 1;
+              done = 1;
+              break;
+            }
+            min_sep = 0.0f;
+          }
+        }
+      }
+      done = __builtin_amdgcn_readfirstlane(done);
+      int kl2 = kl1 + W % len;
+      if (kl2 >= c1) kl2 -= len;
+      if (!done && c + 1 < nch) {
+        s_ra[(W - slot) + lane] = va;
+        if (c + 2 < nch) va = cab[4 * kl2];
+      }
+      kl1 = kl2;
+      __syncthreads();
+    }
+    if (lane == 0) isolv[I] = (uint8_t)solved;
+  }
+  __syncthreads();
+  WSTAMP(15);
   for (int i = lane; i < N; i += W) B.x_cout[en + i] = s_c[i];
 }
 
 template <typename OT>
-__global__ __launch_bounds__(1024) void flock_step_wg_c(StepParams P, WorldBuffers B, int cur, int tcap,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void flock_step_wg_c(StepParams P, WorldBuffers B, int cur, int tcap,
                                                         OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
                                                         float* __restrict__ rew_out, uint8_t* __restrict__ coll_out,
                                                         uint8_t* __restrict__ done_out) {
@@ -1621,7 +1770,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_c(StepParams P, WorldBuffe
   float best = __builtin_inff();
   int bj = tid == 0 ? 1 : 0;
   if (act) {
-#pragma unroll 4
+#pragma unroll 2
     for (int j = 0; j < N; ++j) {
       const Rec r = s_rec[j];
       const bool ovn = !(sep_max(fn, r.fn) > 0.0f);
@@ -1752,7 +1901,7 @@ hipError_t wg_configure(int N, int tcap) {
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, init);
   const void* fsplit[] = {(const void*)flock_step_wg_a, (const void*)flock_solve_wg,
                           (const void*)flock_step_wg_c<float>, (const void*)flock_step_wg_c<double>};
-  const int lsplit[] = {wg_layout_a(N, tcap).total, 16 * N, wg_layout_c(N).total, wg_layout_c(N).total};
+  const int lsplit[] = {wg_layout_a(N, tcap).total, wg_solve_lds(N), wg_layout_c(N).total, wg_layout_c(N).total};
   for (int i = 0; i < 4; ++i)
     if (e == hipSuccess) e = hipFuncSetAttribute(fsplit[i], hipFuncAttributeMaxDynamicSharedMemorySize, lsplit[i]);
   return e;
@@ -1774,7 +1923,7 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   if (wg_use_split()) {
     const int N = P.n_agents, lc = wg_layout_c(N).total;
     hipLaunchKernelGGL(flock_step_wg_a, grid, block, wg_layout_a(N, tcap).total, s, P, B, cur, tcap, actions);
-    hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), 16 * N, s, P, B, tcap);
+    hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
     if (obs_f64)
       hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, s, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
                          done);
