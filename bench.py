@@ -4,7 +4,8 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 One "step" = one env.step of every env on this rank: one HIP launch of
-flock_step_w64 over E envs x N agents (physics + rewards + observations), with
+env_step_w64 over E envs x N agents (physics + rewards + observations; N > 64: the
+workgroup path's three launches), with
 the actions pre-generated on the device (uniform {0,1,2}^3 uint8, the
 MultiDiscrete([3,3,3]) action space) and outputs written to device tensors.
 Weak scaling: every rank runs its own E envs (global env ids rank*E .. rank*E+E-1),
@@ -231,7 +232,9 @@ def main():
         if args.env == "tdm":
             kname = f"env_step_w64<1, {ncap}, float>"
         else:
-            kname = f"env_step_w64<0, {ncap}, float>" if N <= 64 else "flock_step_wg<float>"
+            # N > 64: the workgroup path's three launches per step (split step; kernel_ms covers all)
+            kname = (f"env_step_w64<0, {ncap}, float>" if N <= 64
+                     else "flock_step_wg_a + flock_solve_wg + flock_step_wg_c<float>")
         traffic = None
         tj = load_traffic(args.traffic_json)
         if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
