@@ -106,8 +106,10 @@ MACM_MATH_FN void macm_action_trig(float a, double* s0, double* c0, double* s1, 
 // constants (hi + lo). Measured against glibc atan2 on 2e7 float32-valued inputs:
 // <= 1 ulp, and identical after the observation's "- angle" and float32 rounding
 // (tools/atan2_check.c). About half the instructions of the general library atan2.
-MACM_MATH_FN double obs_atan2(double y, double x) {
-  const double ax = fabs(x), ay = fabs(y);
+// Split in two so that the pair (y, x) / (-y, -x) seen from both agents of a TDM pair shares
+// the reduction and polynomial: obs_atan2_core depends on |x|, |y| only; obs_atan2_finish
+// applies the quadrant from the signs. obs_atan2(y, x) is exactly finish(core(|x|, |y|), y, x).
+MACM_MATH_FN double obs_atan2_core(double ax, double ay) {
   const int swap = ay > ax;
   const double mx = swap ? ay : ax, mn = swap ? ax : ay;
   const int r0 = mn < 0.4375 * mx;         // id -1: atan(a) directly
@@ -131,7 +133,13 @@ MACM_MATH_FN double obs_atan2(double y, double x) {
   const double lo = r1 ? 2.26987774529616870924e-17 : 3.06161699786838301793e-17;
   double r = r0 ? fma(-xr, sz, xr) : hi - (fma(xr, sz, -lo) - xr);
   if (swap) r = (1.57079632679489655800e+00 - r) + 6.12323399573676603587e-17;
+  return r;
+}
+
+MACM_MATH_FN double obs_atan2_finish(double r, double y, double x) {
   if (x < 0.0) r = (3.1415926535897931160e+00 - r) + 1.2246467991473531772e-16;
-  if (mx == 0.0) r = signbit(x) ? 3.1415926535897931160e+00 : 0.0;
+  if (x == 0.0 && y == 0.0) r = signbit(x) ? 3.1415926535897931160e+00 : 0.0;
   return copysign(r, y);
 }
+
+MACM_MATH_FN double obs_atan2(double y, double x) { return obs_atan2_finish(obs_atan2_core(fabs(x), fabs(y)), y, x); }
