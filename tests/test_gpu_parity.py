@@ -226,3 +226,47 @@ def test_c5_dense_1024_agents():
     circles in 400 m^2): one giant island, thousands of touching contacts."""
     vec, orc = make_pair(2, [1024], seed=55)
     check_rollout(vec, orc, 6, np.random.default_rng(5), state_every=2)
+
+
+@pytest.mark.parametrize("vel,pos,warm", [(8, 3, True), (3, 1, True), (1, 0, False), (10, 2, False)])
+def test_dense_relaxing_big_islands(vel, pos, warm):
+    """Dense start that relaxes: islands of hundreds of contacts (the solver's chunked
+    whole-wave path) whose position passes stop early once separated, with the solver
+    settings varied (iterations, no position passes, no warm start)."""
+    kw = dict(start_spread=11, velocityIterations=vel, positionIterations=pos, enableWarmStarting=warm)
+    vec, orc = make_pair(3, [300], seed=300 + vel, **kw)
+    check_rollout(vec, orc, 60, np.random.default_rng(vel), state_every=10)
+
+
+def test_relaxed_lattice_big_island_early_exit():
+    """A 256-body hexagonal cluster at spacing 0.995 (every neighbour pair touching, overlap
+    0.005 < 3 * linearSlop): one island of ~700 contacts whose position passes stop after the
+    first pass, inside the solver's chunked whole-wave path. The state is injected into both
+    the oracle and the HIP world."""
+    E, N = 2, 256
+    vec, orc = make_pair(E, [N], seed=7)
+    C = vec.world.C
+    st = orc.get_state(C)
+    s, h = 0.995, 0.995 * np.sqrt(3.0) / 2.0
+    k, i = np.divmod(np.arange(N), 16)
+    pos = np.stack([(i + 0.5 * (k % 2)) * s - 8.0, k * h - 7.0], -1).astype(np.float32)
+    for e in range(E):
+        p = pos + np.float32(0.3 * e)
+        st["pos"][e] = p
+        st["vel"][e] = 0.0
+        st["sleep"][e] = 0.0
+        r = np.float32(0.5 + 0.1)
+        st["fat"][e] = np.concatenate([p - r, p + r], -1)
+        f = st["fat"][e]
+        pairs = [(a, b) for a in range(N - 1, -1, -1) for b in range(N - 1, a, -1)
+                 if not (f[b, 0] > f[a, 2] or f[b, 1] > f[a, 3] or f[a, 0] > f[b, 2] or f[a, 1] > f[b, 3])]
+        assert len(pairs) <= C
+        st["contact_count"][e] = len(pairs)
+        st["contact_ab"][e] = 0
+        st["contact_ab"][e, :len(pairs)] = [a | (b << 16) for a, b in pairs]
+        st["contact_imp"][e] = 0.0
+    orc.set_state(st)
+    vec.set_state(st)
+    rng = np.random.default_rng(17)
+    check_rollout(vec, orc, 30, rng, state_every=5,
+                  actions_fn=lambda t: np.ones((E, N, 3), np.uint8) if t < 5 else rand_actions(rng, E, N))
