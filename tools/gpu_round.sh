@@ -12,7 +12,7 @@ stop_if_crash() {  # $1 = exit code, $2 = step name; pytest 1 = test failures (n
   echo "$2 rc=$rc" | tee -a "$OUT/status.txt"
 }
 nproc > "$OUT/host.txt"; lscpu | grep -i "model name" >> "$OUT/host.txt"; rocm-smi --showproductname >> "$OUT/host.txt" 2>&1
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 stop_if_crash $? pytest_gpu
 timeout -k 10 180 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1
 stop_if_crash $? smoke
