@@ -137,6 +137,17 @@ __device__ __forceinline__ void act_trig(float a, double* s0, double* c0, double
 #endif
 }
 
+// sqrt((double)x) of a float32 x (b2DistanceSquared), as stored into an OT observation.
+// For float32 outputs the correctly rounded sqrtf (HIP's default lowering) equals
+// (float)sqrt((double)x): double rounding is innocuous for sqrt since 53 >= 2 * 24 + 2
+// (device check over every float32: tools/sqrt_gpu_check.hip). Much cheaper than the f64
+// sequence.
+template <typename OT>
+__device__ __forceinline__ double obs_sqrt(float x) {
+  if constexpr (sizeof(OT) == 4) return (double)sqrtf(x);
+  else return sqrt((double)x);
+}
+
 // Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).
 constexpr int kMtStride = 640;  // words per env: 624 state words, [624] = position
 

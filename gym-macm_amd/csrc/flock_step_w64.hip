@@ -48,11 +48,19 @@ constexpr int TCAP = 256;   // touching contacts per env held in LDS (indices fi
 constexpr int DEG = 16;     // touching contacts per body
 constexpr int ICAP = W / 2; // islands with >= 1 contact (>= 2 bodies each)
 constexpr int RCH = 2;      // list chunks (of 64 entries) cached in registers
+#ifdef MACM_NO_CHAIN_PRIORITY  // A/B knob: no s_setprio around the serial solver chain
+constexpr bool kChainPriority = false;
+#else
+constexpr bool kChainPriority = true;
+#endif
 
 // Diagnostic build only (-DMACM_STAMPS, build/libmacm_hip_stamps.so via `make stamps`):
 // lane 0 records s_memtime at phase boundaries into B.stamps[e][0..13] and per-env
 // sizes into [14..15]. The product library compiles these to nothing.
-#ifdef MACM_STAMPS
+// -DMACM_TIMELINE (with MACM_STAMPS for the buffer): instead of phase stamps, lane 0
+// records only [0] s_memrealtime and [1] s_memtime at entry, [2] HW_ID | XCC_ID << 32,
+// [3] / [4] the same clocks after the last store is issued (tools/timeline.py).
+#if defined(MACM_STAMPS) && !defined(MACM_TIMELINE)
 #define STAMP(k)                                                                    \
   do {                                                                              \
     __builtin_amdgcn_s_waitcnt(0);                                                  \
@@ -105,13 +113,6 @@ __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-// v_writelane_b32 with a compile-time lane (an inline constant: with an SGPR value
-// the lane select cannot be a second SGPR on gfx9): lane J of v receives x.
-template <int J>
-__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(J));
-}
-
 typedef float fvec2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ fvec2 mk2(float a, float b) {
   fvec2 v;
@@ -157,9 +158,11 @@ __device__ __forceinline__ void write_obs_row(OT* o, int coord, double r0, doubl
 template <typename OT>
 __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float best, float rx, float ry, float tdx,
                                           float tdy, float td2) {
-  const double t0 = wrap_pi(atan2((double)ry, (double)rx) - (double)ang);
-  const double t1 = wrap_pi(atan2((double)tdy, (double)tdx) - (double)ang);
-  write_obs_row(o, coord, sqrt((double)best), t0, sqrt((double)td2), t1);
+  // obs_atan2 (macm_math.h): <= 1 ulp from glibc atan2 in f64, identical after "- angle"
+  // and the float32 rounding (tools/atan2_check.c), about half the device libm's work
+  const double t0 = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)ang);
+  const double t1 = wrap_pi(obs_atan2((double)tdy, (double)tdx) - (double)ang);
+  write_obs_row(o, coord, obs_sqrt<OT>(best), t0, obs_sqrt<OT>(td2), t1);
 }
 
 template <typename OT>
@@ -295,10 +298,10 @@ struct SweepState {
 };
 
 // One record of the all-pairs sweep, unrolled at compile time over J < NCAP (lanes
-// >= N hold dummies that overlap nothing and are infinitely far). Row J of the
-// symmetric overlap matrix is the ballot of the AABB test and goes to lane J by
-// v_writelane; the AABB / distance differences run as packed float2 ops, each lane
-// of which is the same IEEE operation as the scalar form.
+// >= N hold dummies that overlap nothing and are infinitely far). Each lane shifts its
+// overlap bit for agent J into its own partner row (add-with-carry, below); the AABB /
+// distance differences run as packed float2 ops, each lane of which is the same IEEE
+// operation as the scalar form.
 template <int J, int NCAP, bool NN>
 __device__ __forceinline__ void sweep_step(const PairRec* s_pj, const PairRec q, fvec2 fn_lo, fvec2 fn_hi,
                                            fvec2 cme, unsigned long long valid, int lane, SweepState& st) {
@@ -309,9 +312,15 @@ __device__ __forceinline__ void sweep_step(const PairRec* s_pj, const PairRec q,
   const fvec2 a = mk2(q.fn.x, q.fn.y) - fn_hi;
   const fvec2 b = fn_lo - mk2(q.fn.z, q.fn.w);
   const float sepv = fmaxf(fmaxf(a.x, a.y), fmaxf(b.x, b.y));
-  const unsigned long long row = __ballot(!(sepv > 0.0f)) & valid;
-  writelane<J>(st.ov_lo, (uint32_t)row);
-  writelane<J>(st.ov_hi, (uint32_t)(row >> 32));
+  // this lane's overlap bit for agent J (= bit J of its own partner row: the test is
+  // symmetric, both orders compare the same four differences) shifted into a per-lane
+  // register by add-with-carry (acc = 2 acc + bit): bit J lands at 31 - (J & 31) and is
+  // bit-reversed after the sweep; the valid mask is applied there
+  (void)valid;
+  if constexpr (J < 32)
+    asm volatile("v_cmp_nlt_f32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(st.ov_lo) : "v"(sepv) : "vcc");
+  else
+    asm volatile("v_cmp_nlt_f32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(st.ov_hi) : "v"(sepv) : "vcc");
   if constexpr (NN) {
     const fvec2 d = mk2(q.c.x, q.c.y) - cme;  // other.position - agent.position
     const fvec2 dd = d * d;
@@ -375,6 +384,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   constexpr bool kT = MODE == kTdm;
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
+#ifdef MACM_TIMELINE
+  const unsigned long long tl_rt0 = __builtin_amdgcn_s_memrealtime(), tl_c0 = __builtin_amdgcn_s_memtime();
+#endif
   const int N = P.n_agents;
   const int C = P.max_contacts;
   // a body that takes part in the physics: every agent (Flock) / alive agents (TDM;
@@ -673,6 +685,14 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   const unsigned long long hasdeg = __ballot(act && deg > 0);
   __syncthreads();
   STAMP(3);
+  // The serial Box2D chain (DFS, Gauss-Seidel, position passes) is a latency chain; the
+  // waves sharing this SIMD run throughput phases (sweep, obs) that can fill its gaps.
+  // Raising the issue priority of a wave that has touching contacts while it walks the
+  // chain (3), and keeping it above the contact-free waves afterwards (1), shortens the
+  // envs with the most contacts, which set the kernel's duration (tools/timeline.py:
+  // waves end at 15.5 us median, 25 us at the latest). Measured -8% per step at the metric
+  // config against no priority; per-island-size or list-size priorities did no better.
+  if (kChainPriority && hasdeg) __builtin_amdgcn_s_setprio(3);
 
   // ---- island DFS in Box2D order (b2World::Solve), serial on lane 0 --------
   // Seeds in body-list order (reverse creation); bodies without touching
@@ -879,6 +899,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     s_isolved[I] = (uint8_t)solved;
   }
 
+  if (kChainPriority && hasdeg) __builtin_amdgcn_s_setprio(1);
   // ---- per-body sleep clock ---------------------------------------------------
   float ns = 0.0f;
   if (act) {
@@ -939,12 +960,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // The old list IS Ov(F_{t-1}), so only the new fat AABBs are tested here:
   //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t)        
   //   FindNewContacts creates        Ov(F_t) \ Ov(F_{t-1})
-  // Overlap is symmetric, so the ballot of ovn at iteration j is agent j's
-  // partner row; lane j keeps it. Agent j's record arrives by LDS broadcast.
-  // The sweep is fully unrolled over NCAP >= N records (lanes >= N hold dummies
-  // that overlap nothing and are infinitely far), so j is a compile-time constant:
-  // row j goes to lane j by v_writelane, and the AABB / distance differences run
-  // as packed float2 ops (each lane-wise result is the same IEEE op as scalar).
+  // Agent j's record arrives by LDS broadcast; each lane accumulates its own partner
+  // row one bit per record (2 VALU: compare into VCC, add-with-carry). The sweep is
+  // fully unrolled over NCAP >= N records (lanes >= N hold dummies that overlap
+  // nothing and are infinitely far), so j is a compile-time constant, and the AABB /
+  // distance differences run as packed float2 ops (each lane-wise result is the same
+  // IEEE op as scalar). The ballot + v_writelane form of the row costs 0.5% more.
   const unsigned long long valid = livem;
   SweepState sw;
   sw.ov_lo = 0u;
@@ -954,8 +975,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   sweep_step<0, NCAP, !kT>(s_pj, s_pj[0], mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), valid, lane, sw);
   const float best = sw.best;
   const int bj = sw.bj;
-  const uint32_t ov_lo = sw.ov_lo, ov_hi = sw.ov_hi;
-  unsigned long long myov = ((unsigned long long)ov_hi << 32) | ov_lo;
+  const uint32_t ov_lo = __builtin_bitreverse32(sw.ov_lo), ov_hi = __builtin_bitreverse32(sw.ov_hi);
+  unsigned long long myov = (((unsigned long long)ov_hi << 32) | ov_lo) & valid;
   myov &= ~(1ull << lane);
   const unsigned long long oldm = (unsigned long long)s_oldm[2 * lane] | ((unsigned long long)s_oldm[2 * lane + 1] << 32);
   const bool coll = act && ((myov | oldm) != 0ull);
@@ -1104,6 +1125,21 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     ec[1] = make_ulonglong2(ctr[2] + c2, ctr[3] + (unsigned long long)dn);
   }
   STAMP(13);
+#ifdef MACM_TIMELINE
+  {
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime(), c1t = __builtin_amdgcn_s_memtime();
+    const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    if (lane == 0) {
+      unsigned long long* st = B.stamps + (size_t)e * 16;
+      st[0] = tl_rt0;
+      st[1] = tl_c0;
+      st[2] = hw | (xcc << 32);
+      st[3] = rt1;
+      st[4] = c1t;
+    }
+  }
+#endif
   STAMP_STAT(14, (unsigned long long)T | ((unsigned long long)nisl << 16) | ((unsigned long long)M << 32));
 #ifdef MACM_STAMPS
   STAMP_STAT(15, (unsigned long long)s_stat_maxisl | ((unsigned long long)total << 32));

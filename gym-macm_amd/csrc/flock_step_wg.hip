@@ -153,7 +153,7 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
                                           float tdy, float td2) {
   const double t0 = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)ang);
   const double t1 = wrap_pi(obs_atan2((double)tdy, (double)tdx) - (double)ang);
-  const double r0 = sqrt((double)best), r1 = sqrt((double)td2);
+  const double r0 = obs_sqrt<OT>(best), r1 = obs_sqrt<OT>(td2);
   if (coord == MACM_COORD_CARTESIAN) {
     o[0] = (OT)r0; o[1] = (OT)cos(t0); o[2] = (OT)sin(t0);
     o[3] = (OT)r1; o[4] = (OT)cos(t1); o[5] = (OT)sin(t1);

@@ -60,6 +60,67 @@ MACM_MATH_FN void macm_sincos(double x, double* sp, double* cp) {
   *cp = co;
 }
 
+// sin/cos of x and of x1 = fl64(x + pi/2) (the reference's `angle + np.pi/2`) from ONE
+// reduction. With P = fl64(pi/2) = pi/2 - c (c = 6.123e-17) and x1 = x + P - err (err the
+// rounding error of the sum, exact by TwoSum), x1 - (q+1) pi/2 = (y0 + y1) - (c + err):
+// the second argument has the same leading remainder y0 (so the same z and the same
+// minimax polynomials) and the correction y1' = y1 - (c + err), a first-order term of both
+// kernels like y1; |err| <= ulp(x1)/2, so this is only accurate for small |x| (|x| < 4:
+// |y1'| < 2^-51; see macm_action_trig_raw). Its quadrant is q + 1. The kernels are then
+// finished twice: ~30 f64 ops instead of a second full evaluation.
+MACM_MATH_FN void macm_sincos_pair(double x, double* s0p, double* c0p, double* s1p, double* c1p) {
+  const double fn = rint(x * 6.36619772367581382433e-01);  // round(x * 2/pi)
+  const int q = (int)fn;
+  const double t1 = fma(-fn, 1.57079632673412561417e+00, x);  // exact
+  const double w2 = fn * 6.07710050630396597660e-11;            // exact
+  const double r2 = t1 - w2;
+  const double e2 = (t1 - r2) - w2;
+  const double tail = fma(-fn, 2.02226624879595063154e-21, e2);  // pio2_2t
+  const double y0 = r2 + tail;
+  const double y1 = (r2 - y0) + tail;
+  // x1 = x + P and its rounding error err = (x + P) - x1 (TwoSum)
+  const double P = 1.57079632679489655800e+00;
+  const double x1 = x + P;
+  const double bp = x1 - x;
+  const double err = (x - (x1 - bp)) + (P - bp);
+  const double y1b = y1 - (6.12323399573676603587e-17 + err);
+  const double z = y0 * y0;
+  double ps = 1.58969099521155010221e-10;
+  ps = fma(ps, z, -2.50507602534068634195e-08);
+  ps = fma(ps, z, 2.75573137070700676789e-06);
+  ps = fma(ps, z, -1.98412698298579493134e-04);
+  ps = fma(ps, z, 8.33333333332248946124e-03);
+  const double v = z * y0;
+  const double vs = v * -1.66666666666666324348e-01;
+  const double vps = v * ps;
+  const double sa = y0 - ((z * (0.5 * y1 - vps) - y1) - vs);
+  const double sb = y0 - ((z * (0.5 * y1b - vps) - y1b) - vs);
+  double pc = -1.13596475577881948265e-11;
+  pc = fma(pc, z, 2.08757232129817482790e-09);
+  pc = fma(pc, z, -2.75573143513906633035e-07);
+  pc = fma(pc, z, 2.48015872894767294178e-05);
+  pc = fma(pc, z, -1.38888888888741095749e-03);
+  pc = fma(pc, z, 4.16666666666666019037e-02);
+  const double hz = 0.5 * z;
+  const double wc = 1.0 - hz;
+  const double cz = ((1.0 - wc) - hz) + z * (z * pc);
+  const double ca = wc + (cz - y0 * y1);
+  const double cb = wc + (cz - y0 * y1b);
+  // quadrant q: (sin, cos) = (sa, ca) rotated; quadrant q + 1 for x1
+  const int odd = q & 1;
+  double so = odd ? ca : sa, co = odd ? sa : ca;
+  if (q & 2) so = -so;
+  if ((q + 1) & 2) co = -co;
+  const int q1 = q + 1;
+  double so1 = odd ? sb : cb, co1 = odd ? cb : sb;  // (q1 & 1) == !odd
+  if (q1 & 2) so1 = -so1;
+  if ((q1 + 1) & 2) co1 = -co1;
+  *s0p = (x == 0.0) ? x : so;  // sin(-0) = -0
+  *c0p = co;
+  *s1p = so1;
+  *c1p = co1;
+}
+
 // The action trig (mvmnt.py:113-116, combat.py:147): sin/cos of the float32 angle a and
 // of a + pi/2 (an f64 sum), from which the step derives the float32 forces
 // f32((c0*k0 + c1*k1)*cc*F), f32((s0*k0 + s1*k1)*cc*F) and the melee-ray offsets
@@ -76,10 +137,21 @@ MACM_MATH_FN void macm_sincos(double x, double* sp, double* cp) {
 #endif
 #include "trig_fix.inc"  // kTrigFixNear (|a| < 4), kTrigFixFar
 
+// The action trig before the exception table. The pair form treats the rounding error of
+// x + pi/2 as a first-order correction, which is accurate only while that error is far
+// below ulp(y0): |x| < 4 covers every angle the step produces (it wraps into [-pi, pi]);
+// larger angles (injected state) take two independent reductions.
+MACM_MATH_FN void macm_action_trig_raw(double x, double* s0, double* c0, double* s1, double* c1) {
+  if (fabs(x) < 4.0) {
+    macm_sincos_pair(x, s0, c0, s1, c1);
+  } else {
+    macm_sincos(x, s0, c0);
+    macm_sincos(x + M_PI / 2, s1, c1);
+  }
+}
+
 MACM_MATH_FN void macm_action_trig(float a, double* s0, double* c0, double* s1, double* c1) {
-  const double x = (double)a;
-  macm_sincos(x, s0, c0);
-  macm_sincos(x + M_PI / 2, s1, c1);
+  macm_action_trig_raw((double)a, s0, c0, s1, c1);
   int hit = 0;
   for (int i = 0; i < MACM_TRIG_NNEAR; ++i) hit |= a == (float)kTrigFixNear[i][0];
   if (hit) {

@@ -6,7 +6,7 @@ mvmnt.py:113-116 / combat.py:147 and mvmnt.py:197 call).
 The forces and melee-ray offsets are float32 values derived from sin/cos(angle) and
 sin/cos(angle + pi/2). tools/trig_check.c enumerates every float32 angle |a| < 2^19 and
 requires every derived float32 value to equal glibc's; macm_action_trig gets there with
-a 16-entry table of glibc values (csrc/trig_fix.inc) at the inputs where its polynomial
+a 17-entry table of glibc values (csrc/trig_fix.inc) at the inputs where its polynomial
 would round differently. Host and device builds agree bit for bit (tools/trig_gpu_check.hip
 prints the same digest on the GPU; profiles/r01/trig/)."""
 import ctypes
@@ -36,6 +36,7 @@ def shim(tmp_path_factory):
     lib = ctypes.CDLL(_build(d, "trig_shim.c", str(d / "libtrig.so"), ["-shared", "-fPIC"]))
     lib.shim_sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     lib.shim_action_trig.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_double)]
+    lib.shim_action_trig_raw.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
     lib.shim_obs_atan2.argtypes = [ctypes.c_double, ctypes.c_double]
     lib.shim_obs_atan2.restype = ctypes.c_double
     return lib
@@ -72,7 +73,7 @@ def f32_forces(s0, c0, s1, c1):
 
 def test_table_entries_are_glibc_values(shim):
     angles = table_angles()
-    assert len(angles) == 16
+    assert len(angles) == 17
     for a in angles:
         assert float(np.float32(a)) == a
         got = action_trig(shim, a)
@@ -81,12 +82,12 @@ def test_table_entries_are_glibc_values(shim):
 
 def test_table_entries_are_needed(shim):
     """Without the table these angles would give float32 forces / ray offsets that differ
-    from the reference's (macm_sincos alone)."""
+    from the reference's (macm_action_trig_raw: the shared-reduction pair below |a| = 4,
+    two macm_sincos beyond)."""
     for a in table_angles():
-        s0, c0, s1, c1 = (ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double())
-        shim.shim_sincos(a, ctypes.byref(s0), ctypes.byref(c0))
-        shim.shim_sincos(a + math.pi / 2, ctypes.byref(s1), ctypes.byref(c1))
-        raw = f32_forces(s0.value, c0.value, s1.value, c1.value)
+        out = (ctypes.c_double * 4)()
+        shim.shim_action_trig_raw(a, out)
+        raw = f32_forces(*list(out))
         ref = f32_forces(*glibc4(a))
         assert not np.array_equal(raw.view(np.uint32), ref.view(np.uint32)), f"angle {a!r}"
 

@@ -99,6 +99,12 @@ def main():
     for name, v in (("touching", T), ("islands", nisl), ("list_in", M), ("max_island_contacts", maxisl),
                     ("list_out", cnt)):
         out[name] = {"mean": float(v.mean()), "p95": float(np.percentile(v, 95)), "max": int(v.max())}
+    # the tail: the slowest 1% of waves (they set the kernel's duration), phase by phase
+    slow = total >= np.percentile(total, 99)
+    out["slowest_1pct"] = {"waves": int(slow.sum()), "wave_cycles_mean": float(total[slow].mean()),
+                           "phases": {name: float(d[slow, k].mean()) for k, name in enumerate(phases)},
+                           "touching": float(T[slow].mean()), "islands": float(nisl[slow].mean()),
+                           "list_in": float(M[slow].mean()), "max_island_contacts": float(maxisl[slow].mean())}
     print(json.dumps(out, indent=1))
     if args.json:
         with open(args.json, "w") as f:

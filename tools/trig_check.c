@@ -63,8 +63,7 @@ int main(int argc, char** argv) {
     const double x = (double)f, x1 = x + M_PI / 2;
     double s0m, c0m, s1m, c1m;
     if (raw) {
-      macm_sincos(x, &s0m, &c0m);
-      macm_sincos(x1, &s1m, &c1m);
+      macm_action_trig_raw(x, &s0m, &c0m, &s1m, &c1m);
     } else {
       macm_action_trig(f, &s0m, &c0m, &s1m, &c1m);
     }
@@ -83,24 +82,24 @@ int main(int argc, char** argv) {
 #pragma omp critical
         {
           if (nbad < 4096) bad[nbad++] = u;
-          printf("%s: float32 outcome differs at x=%a (%.9g)\n", raw ? "macm_sincos" : "macm_action_trig", x, x);
+          printf("%s: float32 outcome differs at x=%a (%.9g)\n", raw ? "macm_action_trig_raw" : "macm_action_trig", x, x);
         }
       }
     }
   }
   printf("inputs: %lld float32 values, |x| < 2^19 (stride %lld)\n", n, stride);
-  printf("host %s digest %016llx\n", raw ? "macm_sincos" : "macm_action_trig", (unsigned long long)dig);
+  printf("host %s digest %016llx\n", raw ? "macm_action_trig_raw" : "macm_action_trig", (unsigned long long)dig);
   printf("%s f64 mismatches vs glibc  sin(x) %lld  cos(x) %lld  sin(x+pi/2) %lld  cos(x+pi/2) %lld\n",
-         raw ? "macm_sincos" : "macm_action_trig", mis[0], mis[1], mis[2], mis[3]);
+         raw ? "macm_action_trig_raw" : "macm_action_trig", mis[0], mis[1], mis[2], mis[3]);
   printf("  of which |x| <= pi+0.1: %lld %lld %lld %lld\n", mis_pi[0], mis_pi[1], mis_pi[2], mis_pi[3]);
   printf("%s: inputs whose float32 forces / ray offsets differ from glibc's: %lld (|x| <= pi+0.1: %lld)\n",
-         raw ? "macm_sincos" : "macm_action_trig", f32bad, f32bad_pi);
+         raw ? "macm_action_trig_raw" : "macm_action_trig", f32bad, f32bad_pi);
   if (raw && emit) {  /* the exception table for macm_math.h: glibc's values at these inputs */
     for (int i = 1; i < nbad; ++i)
       for (int j = i; j > 0 && bad[j - 1] > bad[j]; --j) { uint32_t t = bad[j]; bad[j] = bad[j - 1]; bad[j - 1] = t; }
     FILE* fo = fopen(emit, "w");
     if (!fo) { perror(emit); return 2; }
-    fprintf(fo, "// Generated by tools/trig_check.c --raw --emit: the float32 angles a where macm_sincos's\n"
+    fprintf(fo, "// Generated by tools/trig_check.c --raw --emit: the float32 angles a where macm_action_trig_raw's\n"
                 "// derived float32 forces / melee-ray offsets differ from glibc's, with glibc's\n"
                 "// sin(a), cos(a), sin(a + pi/2), cos(a + pi/2) (see macm_action_trig).\n");
     for (int far = 0; far < 2; ++far) {
