@@ -120,6 +120,14 @@ __device__ __forceinline__ double wrap_pi(double t) {
   return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t;
 }
 
+// v_writelane_b32 with a wave-uniform lane index (in M0: on gfx9 the lane select and the
+// data cannot both be SGPRs): lane `l` of v receives the uniform value x. The s_nop covers
+// the SALU write of M0 just before.
+__device__ __forceinline__ uint32_t writelane_m0(int x, int l, uint32_t v) {
+  asm volatile("s_nop 1\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(l));
+  return v;
+}
+
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
@@ -420,12 +428,13 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   __shared__ uint8_t s_adj[W * DEG];
   __shared__ uint8_t s_ord[TCAP];
   __shared__ uint32_t s_cvis[TCAP / 32];
-  __shared__ uint8_t s_deg[W], s_stack[W], s_ibodies[W], s_sleepnow[W];
+  __shared__ uint8_t s_deg[W], s_stack[W], s_ibodies[W], s_bisl[W];
   __shared__ uint16_t s_ic[ICAP + 1];
   __shared__ uint8_t s_ib[ICAP + 1];
   __shared__ uint8_t s_isolved[ICAP];
-  __shared__ float s_slp[W];
+  __shared__ uint32_t s_imin[ICAP];  // per island: min sleep time (float bits, all >= 0)
   __shared__ uint32_t s_oldm[2 * W];  // per agent: 64-bit mask of partners in the old list
+  __shared__ uint32_t s_tm[2 * W];    // per agent: 64-bit mask of its touching contacts (T <= 64)
   __shared__ int s_nisl;
   // TDM only (unreferenced, hence not allocated, in the Flock instantiation)
   __shared__ double s_hpd[W];
@@ -513,6 +522,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   s_cy[lane] = p.y;
   if (lane < TCAP / 32) s_cvis[lane] = 0u;
   s_oldm[2 * lane] = 0u;
+  s_tm[2 * lane] = 0u;
+  s_tm[2 * lane + 1] = 0u;
   s_oldm[2 * lane + 1] = 0u;
   int status = 0;
   STAMP(0);
@@ -662,6 +673,10 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     if (touch) {
       tbits |= 1u << c;
       const int slot = T + __popcll(m & lt);
+      if (slot < W) {  // touching contact `slot` of both bodies (the scalar DFS below)
+        atomicOr(&s_tm[2 * (ab & 0xffffu) + (slot >> 5)], 1u << (slot & 31));
+        atomicOr(&s_tm[2 * (ab >> 16) + (slot >> 5)], 1u << (slot & 31));
+      }
       if (slot < TCAP) {
         s_tab[slot] = ab;
         s_tln[slot] = P.warm_starting ? dt_ratio * lam.x : 0.0f;
@@ -678,8 +693,17 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   STAMP(2);
 
   // ---- per-body touching edges in list (= Box2D edge) order ----------------
+  // T <= 64 (the common case): a body's edges are the set bits of its touching mask, in
+  // ascending contact order = list order. Otherwise an explicit edge array per body.
+  const bool fast_dfs = T <= W;
   int deg = 0;
-  if (act) {
+  unsigned long long tmask = 0ull;
+  if (fast_dfs) {
+    if (act) {
+      tmask = (unsigned long long)s_tm[2 * lane] | ((unsigned long long)s_tm[2 * lane + 1] << 32);
+      deg = __popcll(tmask);
+    }
+  } else if (act) {
     for (int t = 0; t < T; ++t) {
       const uint32_t ab = s_tab[t];
       if ((int)(ab & 0xffffu) == lane || (int)(ab >> 16) == lane) {
@@ -692,7 +716,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     status |= MACM_ST_DEGREE_OVERFLOW;
     deg = DEG;
   }
-  s_deg[lane] = (uint8_t)deg;
+  if (!fast_dfs) s_deg[lane] = (uint8_t)deg;
   const unsigned long long hasdeg = __ballot(act && deg > 0);
   __syncthreads();
   STAMP(3);
@@ -709,7 +733,68 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // Seeds in body-list order (reverse creation); bodies without touching
   // edges are singleton islands and contribute no contact order, so only
   // bodies in `hasdeg` are walked.
-  if (lane == 0 && hasdeg) {
+  if (fast_dfs) {
+    // Wave-uniform (scalar) DFS: bodies' edge masks and contacts' pairs are read from the
+    // owning lanes' registers (v_readlane), visited sets are 64-bit masks, and the outputs
+    // and the stack are built in registers lane by lane (v_writelane), so the walk touches
+    // no LDS. Visiting all unvisited edges of a popped body in ascending order is Box2D's
+    // edge walk (an edge is only ever marked by its own visit).
+    const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
+    const uint32_t tm_lo = (uint32_t)tmask, tm_hi = (uint32_t)(tmask >> 32);
+    uint32_t ordv = 0u, bodv = 0u, islv = 0u, icv = 0u, ibv = 0u, stk = 0u;
+    unsigned long long vis = ~hasdeg, cvis = 0ull;
+    int nord = 0, nisl = 0, nb = 0;
+    for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
+      const int s = 63 - __clzll(todo);
+      icv = writelane_m0(nord, nisl, icv);  // s_ic[nisl]
+      ibv = writelane_m0(nb, nisl, ibv);    // s_ib[nisl]
+      vis |= 1ull << s;
+      stk = writelane_m0(s, 0, stk);
+      int sp = 1;
+      while (sp > 0) {
+        --sp;
+        const int b = __builtin_amdgcn_readlane(stk, sp);
+        bodv = writelane_m0(b, nb, bodv);  // s_ibodies[nb]
+        islv = writelane_m0(nisl, b, islv);  // s_bisl[b]
+        ++nb;
+        unsigned long long m = (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_hi, b) << 32) |
+                                (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_lo, b)) & ~cvis;
+        cvis |= m;
+        while (m) {
+          const int t = __builtin_ctzll(m);
+          m &= m - 1ull;
+          ordv = writelane_m0(t, nord, ordv);  // s_ord[nord]
+          ++nord;
+          const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, t);
+          const int a = ab & 0xffffu, bb = ab >> 16;
+          const int o = (a == b) ? bb : a;
+          if ((vis >> o) & 1ull) continue;
+          vis |= 1ull << o;
+          stk = writelane_m0(o, sp, stk);
+          ++sp;
+        }
+      }
+      ++nisl;
+    }
+    icv = writelane_m0(nord, nisl, icv);
+    ibv = writelane_m0(nb, nisl, ibv);
+    if (lane < nord) s_ord[lane] = (uint8_t)ordv;
+    if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
+    if ((hasdeg >> lane) & 1ull) s_bisl[lane] = (uint8_t)islv;
+    if (lane <= nisl) {
+      s_ic[lane] = (uint16_t)icv;
+      s_ib[lane] = (uint8_t)ibv;
+    }
+    if (lane == 0) {
+      s_nisl = nisl;
+#ifdef MACM_STAMPS
+      int mx = 0;
+      for (int q = 0; q < nisl; ++q) mx = max(mx, __builtin_amdgcn_readlane(icv, q + 1) - __builtin_amdgcn_readlane(icv, q));
+      s_stat_maxisl = mx;
+#endif
+    }
+  }
+  if (!fast_dfs && lane == 0 && hasdeg) {
     unsigned long long vis = ~hasdeg;
     int nord = 0, nisl = 0, nb = 0;
     for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
@@ -721,6 +806,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       vis |= 1ull << s;
       while (sp > 0) {
         const int b = s_stack[--sp];
+        s_bisl[b] = (uint8_t)nisl;
         s_ibodies[nb++] = (uint8_t)b;
         const int db = s_deg[b];
         for (int q = 0; q < db; ++q) {
@@ -750,7 +836,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     }
 #endif
   }
-  if (lane == 0 && !hasdeg) {
+  if (!fast_dfs && lane == 0 && !hasdeg) {
     s_nisl = 0;
 #ifdef MACM_STAMPS
     s_stat_maxisl = 0;
@@ -920,6 +1006,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
 
   // ---- position iterations, one lane per island ------------------------------
   for (int I = lane; I < nisl; I += W) {
+    s_imin[I] = 0xffffffffu;  // island sleep decision below
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
     int solved = 0;
     if (c1 - c0 == 1) {  // single contact: registers
@@ -996,21 +1083,22 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   if (act) {
     const bool moving = vx * vx + vy * vy > kLinearSleepTol * kLinearSleepTol;
     ns = moving ? 0.0f : slp + P.dt;
-    s_slp[lane] = ns;
   }
   __syncthreads();
   STAMP(7);
 
   // ---- island sleep decision ---------------------------------------------------
-  if (act && deg == 0) s_sleepnow[lane] = (ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
-  for (int I = lane; I < nisl; I += W) {
-    const int b0 = s_ib[I], b1 = s_ib[I + 1];
-    float mn = 3.402823466e+38f;
-    for (int k = b0; k < b1; ++k) mn = bmin(mn, s_slp[s_ibodies[k]]);
-    const uint8_t sl = (mn >= kTimeToSleep && s_isolved[I]) ? 1 : 0;
-    for (int k = b0; k < b1; ++k) s_sleepnow[s_ibodies[k]] = sl;
-  }
+  // min sleep time over each island's bodies (b2Island::Solve) by LDS atomicMin on the
+  // float bits (sleep times are >= 0, so their bit patterns order as the values)
+  const bool inisl = act && deg > 0;
+  const int myisl = inisl ? s_bisl[lane] : 0;
+  if (inisl) atomicMin(&s_imin[myisl], __float_as_uint(ns));
   __syncthreads();
+  bool sleepnow = false;
+  if (act) {
+    sleepnow = inisl ? (__uint_as_float(s_imin[myisl]) >= kTimeToSleep && s_isolved[myisl])
+                     : (ns >= kTimeToSleep && P.pos_iters > 0);
+  }
   STAMP(8);
 
   // ---- SynchronizeFixtures: fat-AABB update ------------------------------------
@@ -1029,7 +1117,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       if (dx < 0.0f) fn.x += dx; else fn.z += dx;
       if (dy < 0.0f) fn.y += dy; else fn.w += dy;
     }
-    if (s_sleepnow[lane]) {
+    if (sleepnow) {
       vx = 0.0f;
       vy = 0.0f;
       ns = 0.0f;
