@@ -94,6 +94,18 @@ constexpr bool kChainPriority = true;
 __device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }  // b2Min
 __device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }  // b2Max
 __device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
+// The contact solvers' clamps as single v_min_f32 / v_max_f32 instead of compare + select
+// (b2Min / b2Max): they sit on the serial Gauss-Seidel chain. For non-NaN operands the two
+// forms differ only in the sign of a zero result (b2Max(-0, +0) is +0, v_max may give -0);
+// a zero impulse or velocity of either sign leaves every later value the same, so only
+// zero signs can differ (as they already do through the angular terms).
+#ifdef MACM_EXACT_ZERO_SIGNS
+__device__ __forceinline__ float smax(float a, float b) { return bmax(a, b); }
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return bclamp(a, lo, hi); }
+#else
+__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return fmaxf(lo, fminf(a, hi)); }
+#endif
 
 // b2TestOverlap
 __device__ __forceinline__ bool overlap(float4 a, float4 b) {
@@ -269,7 +281,7 @@ __device__ __forceinline__ void solve_velocity_contact(float& vAx, float& vAy, f
     const float vt = dvx * tx + dvy * ty;
     float lambda = kmass * (-vt);
     const float maxf = friction * ln;
-    const float ni = bclamp(ltg + lambda, -maxf, maxf);
+    const float ni = sclamp(ltg + lambda, -maxf, maxf);
     lambda = ni - ltg;
     ltg = ni;
     const float Px = lambda * tx, Py = lambda * ty;
@@ -282,7 +294,7 @@ __device__ __forceinline__ void solve_velocity_contact(float& vAx, float& vAy, f
     const float dvx = vBx - vAx, dvy = vBy - vAy;
     const float vn = dvx * nx + dvy * ny;
     float lambda = -kmass * (vn - 0.0f);  // velocityBias == 0 (restitution 0)
-    const float ni = bmax(ln + lambda, 0.0f);
+    const float ni = smax(ln + lambda, 0.0f);
     lambda = ni - ln;
     ln = ni;
     const float Px = lambda * nx, Py = lambda * ny;
@@ -299,7 +311,7 @@ __device__ __forceinline__ float solve_position_contact(float& cAx, float& cAy, 
   float nx = cBx - cAx, ny = cBy - cAy;
   normalize(nx, ny);
   const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - radius - radius;
-  const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+  const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
   const float K = mA + mB;
   const float imp = K > 0.0f ? -Cc / K : 0.0f;
   const float Px = imp * nx, Py = imp * ny;

@@ -41,6 +41,18 @@ constexpr int W = 64;
 __device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
+// The contact solvers' clamps as single v_min_f32 / v_max_f32 instead of compare + select
+// (b2Min / b2Max): they sit on the serial Gauss-Seidel chain. For non-NaN operands the two
+// forms differ only in the sign of a zero result (b2Max(-0, +0) is +0, v_max may give -0);
+// a zero impulse or velocity of either sign leaves every later value the same, so only
+// zero signs can differ (as they already do through the angular terms).
+#ifdef MACM_EXACT_ZERO_SIGNS
+__device__ __forceinline__ float smax(float a, float b) { return bmax(a, b); }
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return bclamp(a, lo, hi); }
+#else
+__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return fmaxf(lo, fminf(a, hi)); }
+#endif
 __device__ __forceinline__ bool overlap(float4 a, float4 b) {  // b2TestOverlap
   const float d1x = b.x - a.z, d1y = b.y - a.w;
   const float d2x = a.x - b.z, d2y = a.y - b.w;
@@ -1305,7 +1317,7 @@ __device__ __forceinline__ void gs_velocity(float2& va, float2& vb, float nx, fl
     const float vt = dvx * tx + dvy * ty;
     float lambda = kmass * (-vt);
     const float maxf = friction * ln;
-    const float ni = bclamp(ltg + lambda, -maxf, maxf);
+    const float ni = sclamp(ltg + lambda, -maxf, maxf);
     lambda = ni - ltg;
     ltg = ni;
     const float Px = lambda * tx, Py = lambda * ty;
@@ -1316,7 +1328,7 @@ __device__ __forceinline__ void gs_velocity(float2& va, float2& vb, float nx, fl
     const float dvx = vb.x - va.x, dvy = vb.y - va.y;
     const float vn = dvx * nx + dvy * ny;
     float lambda = -kmass * (vn - 0.0f);
-    const float ni = bmax(ln + lambda, 0.0f);
+    const float ni = smax(ln + lambda, 0.0f);
     lambda = ni - ln;
     ln = ni;
     const float Px = lambda * nx, Py = lambda * ny;
@@ -1340,7 +1352,7 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
   float nx = cb.x - ca.x, ny = cb.y - ca.y;
   normalize(nx, ny);
   const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
-  const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+  const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
   const float K = mA + mB;
   const float imp = K > 0.0f ? -Cc / K : 0.0f;
   const float Px = imp * nx, Py = imp * ny;
