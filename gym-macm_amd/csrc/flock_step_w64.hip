@@ -333,11 +333,31 @@ struct SweepState {
 // overlap bit for agent J into its own partner row (add-with-carry, below); the AABB /
 // distance differences run as packed float2 ops, each lane of which is the same IEEE
 // operation as the scalar form.
+// Records in flight during the sweep: record J + AH is requested while record J is tested,
+// so an LDS broadcast has AH records' worth of VALU work to arrive in (a single record's ~12
+// VALU do not cover the LDS latency with the other waves of the CU reading too).
+#ifndef MACM_SWEEP_AHEAD
+#define MACM_SWEEP_AHEAD 2
+#endif
+constexpr int kSweepAhead = MACM_SWEEP_AHEAD;
+
+struct SweepRec {
+  float4 fn;
+  float2 c;
+};
+
+__device__ __forceinline__ SweepRec load_rec(const PairRec* s_pj, int j) {
+  SweepRec r;
+  r.fn = s_pj[j].fn;  // ds_read_b128
+  r.c = s_pj[j].c;    // ds_read_b64 (the pad is never read)
+  return r;
+}
+
 template <int J, int NCAP, bool NN>
-__device__ __forceinline__ void sweep_step(const PairRec* s_pj, const PairRec q, fvec2 fn_lo, fvec2 fn_hi,
+__device__ __forceinline__ void sweep_step(const PairRec* s_pj, SweepRec* win, fvec2 fn_lo, fvec2 fn_hi,
                                            fvec2 cme, unsigned long long valid, int lane, SweepState& st) {
-  PairRec qn;
-  if constexpr (J + 1 < NCAP) qn = s_pj[J + 1];  // next record in flight while this one is tested
+  const SweepRec q = win[J % kSweepAhead];
+  if constexpr (J + kSweepAhead < NCAP) win[J % kSweepAhead] = load_rec(s_pj, J + kSweepAhead);
   // b2TestOverlap(fn, fj) separates iff one of (fj.lo - fn.hi, fn.lo - fj.hi) > 0;
   // for finite AABBs (and the +-inf dummies) that is max(...) > 0
   const fvec2 a = mk2(q.fn.x, q.fn.y) - fn_hi;
@@ -372,7 +392,7 @@ __device__ __forceinline__ void sweep_step(const PairRec* s_pj, const PairRec q,
   }
   // keep the scheduler from hoisting every record's LDS read (register pressure)
   if constexpr ((J & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-  if constexpr (J + 1 < NCAP) sweep_step<J + 1, NCAP, NN>(s_pj, qn, fn_lo, fn_hi, cme, valid, lane, st);
+  if constexpr (J + 1 < NCAP) sweep_step<J + 1, NCAP, NN>(s_pj, win, fn_lo, fn_hi, cme, valid, lane, st);
 }
 
 // New-pair compaction in descending (a, b) order: lane a owns the bitmask of
@@ -1163,7 +1183,10 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   sw.ov_hi = 0u;
   sw.best = __builtin_inff();
   sw.bj = lane == 0 ? 1 : 0;
-  sweep_step<0, NCAP, !kT>(s_pj, s_pj[0], mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), valid, lane, sw);
+  SweepRec win[kSweepAhead];
+#pragma unroll
+  for (int k = 0; k < kSweepAhead; ++k) win[k] = load_rec(s_pj, k);
+  sweep_step<0, NCAP, !kT>(s_pj, win, mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), valid, lane, sw);
   const float best = sw.best;
   const int bj = sw.bj;
   const uint32_t ov_lo = __builtin_bitreverse32(sw.ov_lo), ov_hi = __builtin_bitreverse32(sw.ov_hi);
