@@ -486,7 +486,10 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   __shared__ uint8_t s_isolved[ICAP];
   __shared__ uint32_t s_imin[ICAP];  // per island: min sleep time (float bits, all >= 0)
   __shared__ uint32_t s_oldm[2 * W];  // per agent: 64-bit mask of partners in the old list
-  __shared__ uint32_t s_tm[2 * W];    // per agent: 64-bit mask of its touching contacts (T <= 64)
+  // per agent: bit mask of its touching contacts for the scalar DFS (T <= 64 TMW); TDM keeps one
+  // 64-bit word (its LDS budget is full), Flock two
+  constexpr int TMW = kT ? 1 : 2;
+  __shared__ uint32_t s_tm[2 * TMW * W];
   __shared__ int s_nisl;
   // TDM only (unreferenced, hence not allocated, in the Flock instantiation)
   __shared__ double s_hpd[W];
@@ -574,8 +577,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   s_cy[lane] = p.y;
   if (lane < TCAP / 32) s_cvis[lane] = 0u;
   s_oldm[2 * lane] = 0u;
-  s_tm[2 * lane] = 0u;
-  s_tm[2 * lane + 1] = 0u;
+#pragma unroll
+  for (int q = 0; q < 2 * TMW; ++q) s_tm[2 * TMW * lane + q] = 0u;
   s_oldm[2 * lane + 1] = 0u;
   int status = 0;
   STAMP(0);
@@ -725,9 +728,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     if (touch) {
       tbits |= 1u << c;
       const int slot = T + __popcll(m & lt);
-      if (slot < W) {  // touching contact `slot` of both bodies (the scalar DFS below)
-        atomicOr(&s_tm[2 * (ab & 0xffffu) + (slot >> 5)], 1u << (slot & 31));
-        atomicOr(&s_tm[2 * (ab >> 16) + (slot >> 5)], 1u << (slot & 31));
+      if (slot < 64 * TMW) {  // touching contact `slot` of both bodies (the scalar DFS below)
+        atomicOr(&s_tm[2 * TMW * (ab & 0xffffu) + (slot >> 5)], 1u << (slot & 31));
+        atomicOr(&s_tm[2 * TMW * (ab >> 16) + (slot >> 5)], 1u << (slot & 31));
       }
       if (slot < TCAP) {
         s_tab[slot] = ab;
@@ -745,15 +748,17 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   STAMP(2);
 
   // ---- per-body touching edges in list (= Box2D edge) order ----------------
-  // T <= 64 (the common case): a body's edges are the set bits of its touching mask, in
+  // T <= 64 TMW (the common case): a body's edges are the set bits of its touching mask, in
   // ascending contact order = list order. Otherwise an explicit edge array per body.
-  const bool fast_dfs = T <= W;
+  const bool fast_dfs = T <= 64 * TMW;
   int deg = 0;
-  unsigned long long tmask = 0ull;
+  unsigned long long tmask = 0ull, tmask1 = 0ull;  // contacts 0..63, 64..127
   if (fast_dfs) {
     if (act) {
-      tmask = (unsigned long long)s_tm[2 * lane] | ((unsigned long long)s_tm[2 * lane + 1] << 32);
-      deg = __popcll(tmask);
+      const uint32_t* tm = s_tm + 2 * TMW * lane;
+      tmask = (unsigned long long)tm[0] | ((unsigned long long)tm[1] << 32);
+      if (TMW == 2 && T > 64) tmask1 = (unsigned long long)tm[2] | ((unsigned long long)tm[3] << 32);
+      deg = __popcll(tmask) + __popcll(tmask1);
     }
   } else if (act) {
     for (int t = 0; t < T; ++t) {
@@ -791,10 +796,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     // and the stack are built in registers lane by lane (v_writelane), so the walk touches
     // no LDS. Visiting all unvisited edges of a popped body in ascending order is Box2D's
     // edge walk (an edge is only ever marked by its own visit).
-    const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
+    const uint32_t tabv = lane < T ? s_tab[lane] : 0u;  // contact `lane`'s pair
+    const uint32_t tabv1 = (TMW == 2 && 64 + lane < T) ? s_tab[64 + lane] : 0u;  // contact 64 + lane's
     const uint32_t tm_lo = (uint32_t)tmask, tm_hi = (uint32_t)(tmask >> 32);
-    uint32_t ordv = 0u, bodv = 0u, islv = 0u, icv = 0u, ibv = 0u, stk = 0u;
-    unsigned long long vis = ~hasdeg, cvis = 0ull;
+    const uint32_t tm1_lo = (uint32_t)tmask1, tm1_hi = (uint32_t)(tmask1 >> 32);
+    uint32_t ordv = 0u, ordv1 = 0u, bodv = 0u, islv = 0u, icv = 0u, ibv = 0u, stk = 0u;
+    unsigned long long vis = ~hasdeg, cvis = 0ull, cvis1 = 0ull;
     int nord = 0, nisl = 0, nb = 0;
     for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
       const int s = 63 - __clzll(todo);
@@ -809,21 +816,32 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         bodv = writelane_m0(b, nb, bodv);  // s_ibodies[nb]
         islv = writelane_m0(nisl, b, islv);  // s_bisl[b]
         ++nb;
+        // the body's unvisited edges in ascending contact order: contacts 0..63, then 64..127
+        auto walk = [&](unsigned long long m, int base, uint32_t tab) {
+          while (m) {
+            const int t = __builtin_ctzll(m);
+            m &= m - 1ull;
+            if (nord < 64) ordv = writelane_m0(base + t, nord, ordv);  // s_ord[nord]
+            else ordv1 = writelane_m0(base + t, nord - 64, ordv1);
+            ++nord;
+            const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tab, t);
+            const int a = ab & 0xffffu, bb = ab >> 16;
+            const int o = (a == b) ? bb : a;
+            if ((vis >> o) & 1ull) continue;
+            vis |= 1ull << o;
+            stk = writelane_m0(o, sp, stk);
+            ++sp;
+          }
+        };
         unsigned long long m = (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_hi, b) << 32) |
                                 (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_lo, b)) & ~cvis;
         cvis |= m;
-        while (m) {
-          const int t = __builtin_ctzll(m);
-          m &= m - 1ull;
-          ordv = writelane_m0(t, nord, ordv);  // s_ord[nord]
-          ++nord;
-          const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, t);
-          const int a = ab & 0xffffu, bb = ab >> 16;
-          const int o = (a == b) ? bb : a;
-          if ((vis >> o) & 1ull) continue;
-          vis |= 1ull << o;
-          stk = writelane_m0(o, sp, stk);
-          ++sp;
+        walk(m, 0, tabv);
+        if (TMW == 2 && T > 64) {
+          unsigned long long m1 = (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_hi, b) << 32) |
+                                   (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_lo, b)) & ~cvis1;
+          cvis1 |= m1;
+          walk(m1, 64, tabv1);
         }
       }
       ++nisl;
@@ -831,6 +849,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     icv = writelane_m0(nord, nisl, icv);
     ibv = writelane_m0(nb, nisl, ibv);
     if (lane < nord) s_ord[lane] = (uint8_t)ordv;
+    if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv1;
     if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
     if ((hasdeg >> lane) & 1ull) s_bisl[lane] = (uint8_t)islv;
     if (lane <= nisl) {
