@@ -780,7 +780,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // The serial Box2D chain (DFS, Gauss-Seidel, position passes) is a latency chain; the
   // waves sharing this SIMD run throughput phases (sweep, obs) that can fill its gaps.
   // Raising the issue priority of a wave that has touching contacts while it walks the
-  // chain (3), and keeping it above the contact-free waves afterwards (1), shortens the
+  // chain (3), and keeping it above the contact-free waves afterwards (1 or 2, below), shortens the
   // envs with the most contacts, which set the kernel's duration (tools/timeline.py:
   // waves end at 15.5 us median, 25 us at the latest). Measured -8% per step at the metric
   // config against no priority; per-island-size or list-size priorities did no better.
@@ -1148,7 +1148,13 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     s_isolved[I] = (uint8_t)solved;
   }
 
-  if (kChainPriority && hasdeg) __builtin_amdgcn_s_setprio(1);
+  // After the chain a wave with touching contacts stays above the contact-free ones, and one
+  // with >= 3 touching contacts (the envs that end last) above those: -2% per step against a
+  // single level (profiles/r01/ab2 s24/s25; thresholds 2 and 4, or a third level, did no better).
+  if (kChainPriority && hasdeg) {
+    if (T >= 3) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(1);
+  }
   // ---- per-body sleep clock ---------------------------------------------------
   float ns = 0.0f;
   if (act) {
