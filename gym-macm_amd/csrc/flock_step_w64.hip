@@ -360,6 +360,11 @@ struct SweepState {
 #define MACM_SWEEP_AHEAD 2
 #endif
 constexpr int kSweepAhead = MACM_SWEEP_AHEAD;
+#ifdef MACM_SWEEP_ONE_CHAIN  // A/B knob: the single-chain sweep at NCAP = 64 too
+constexpr bool kSweepTwoChains = false;
+#else
+constexpr bool kSweepTwoChains = true;
+#endif
 
 struct SweepRec {
   float4 fn;
@@ -413,6 +418,60 @@ __device__ __forceinline__ void sweep_step(const PairRec* s_pj, SweepRec* win, f
   // keep the scheduler from hoisting every record's LDS read (register pressure)
   if constexpr ((J & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   if constexpr (J + 1 < NCAP) sweep_step<J + 1, NCAP, NN>(s_pj, win, fn_lo, fn_hi, cme, valid, lane, st);
+}
+
+// NCAP = 64 with the nearest neighbour: the records of the two halves are taken in turns
+// (0, 32, 1, 33, ...) with a running minimum per half, so the two loop-carried chains (the
+// overlap bits of ov_lo / ov_hi and the minimum of each half) are independent and their
+// compare -> mask -> select steps issue interleaved; each half's compare result goes to its own
+// SGPR pair instead of VCC. Each half still scans its records in increasing j with strict '<',
+// and the halves merge with the lower half winning ties, which is the single scan's result.
+struct SweepState2 {
+  uint32_t ov_lo, ov_hi;
+  float best_a, best_b;
+  int bj_a, bj_b;
+};
+
+template <int S, int AH>
+__device__ __forceinline__ void sweep2_step(const PairRec* s_pj, SweepRec* win, fvec2 fn_lo, fvec2 fn_hi,
+                                            fvec2 cme, SweepState2& st) {
+  constexpr int JA = S, JB = 32 + S;  // records of this step: JA (lower half), JB (upper half)
+  const SweepRec qa = win[(2 * S) % AH], qb = win[(2 * S + 1) % AH];
+  // the records of step S + AH / 2 (record order 0, 32, 1, 33, ...)
+  if constexpr (2 * S + AH < 64) {
+    constexpr int K = 2 * S + AH;
+    win[(2 * S) % AH] = load_rec(s_pj, (K & 1) ? 32 + (K >> 1) : (K >> 1));
+  }
+  if constexpr (2 * S + 1 + AH < 64) {
+    constexpr int K = 2 * S + 1 + AH;
+    win[(2 * S + 1) % AH] = load_rec(s_pj, (K & 1) ? 32 + (K >> 1) : (K >> 1));
+  }
+  const fvec2 aa = mk2(qa.fn.x, qa.fn.y) - fn_hi, ba = fn_lo - mk2(qa.fn.z, qa.fn.w);
+  const fvec2 ab = mk2(qb.fn.x, qb.fn.y) - fn_hi, bb = fn_lo - mk2(qb.fn.z, qb.fn.w);
+  const float sa = fmaxf(fmaxf(aa.x, aa.y), fmaxf(ba.x, ba.y));
+  const float sb = fmaxf(fmaxf(ab.x, ab.y), fmaxf(bb.x, bb.y));
+  const fvec2 da = mk2(qa.c.x, qa.c.y) - cme, db = mk2(qb.c.x, qb.c.y) - cme;
+  const fvec2 dda = da * da, ddb = db * db;
+  const float d2a = dda.x + dda.y, d2b = ddb.x + ddb.y;
+  unsigned long long ca, cb, ma, mb;
+  asm volatile(
+      "v_cmp_nlt_f32_e64 %[ca], 0, %[sa]\n\t"
+      "v_cmp_nlt_f32_e64 %[cb], 0, %[sb]\n\t"
+      "v_cmp_lt_f32_e64 %[ma], %[da], %[ba]\n\t"
+      "v_cmp_lt_f32_e64 %[mb], %[db], %[bb]\n\t"
+      "v_addc_co_u32_e64 %[lo], %[ca], %[lo], %[lo], %[ca]\n\t"
+      "v_addc_co_u32_e64 %[hi], %[cb], %[hi], %[hi], %[cb]\n\t"
+      "s_bitset0_b64 %[ma], %[JA]\n\t"
+      "s_bitset0_b64 %[mb], %[JB]\n\t"
+      "v_cndmask_b32_e64 %[ba], %[ba], %[da], %[ma]\n\t"
+      "v_cndmask_b32_e64 %[ja], %[ja], %[JA], %[ma]\n\t"
+      "v_cndmask_b32_e64 %[bb], %[bb], %[db], %[mb]\n\t"
+      "v_cndmask_b32_e64 %[jb], %[jb], %[JB], %[mb]"
+      : [lo] "+v"(st.ov_lo), [hi] "+v"(st.ov_hi), [ba] "+v"(st.best_a), [bb] "+v"(st.best_b), [ja] "+v"(st.bj_a),
+        [jb] "+v"(st.bj_b), [ca] "=&s"(ca), [cb] "=&s"(cb), [ma] "=&s"(ma), [mb] "=&s"(mb)
+      : [sa] "v"(sa), [sb] "v"(sb), [da] "v"(d2a), [db] "v"(d2b), [JA] "i"(JA), [JB] "i"(JB));
+  if constexpr ((S & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  if constexpr (S + 1 < 32) sweep2_step<S + 1, AH>(s_pj, win, fn_lo, fn_hi, cme, st);
 }
 
 // New-pair compaction in descending (a, b) order: lane a owns the bitmask of
@@ -1228,10 +1287,30 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   sw.ov_hi = 0u;
   sw.best = __builtin_inff();
   sw.bj = lane == 0 ? 1 : 0;
-  SweepRec win[kSweepAhead];
+  if constexpr (NCAP == 64 && !kT && kSweepTwoChains) {
+    constexpr int AH2 = 2 * kSweepAhead;  // records in flight (two per step)
+    SweepState2 s2;
+    s2.ov_lo = 0u;
+    s2.ov_hi = 0u;
+    s2.best_a = __builtin_inff();
+    s2.best_b = __builtin_inff();
+    s2.bj_a = lane == 0 ? 1 : 0;
+    s2.bj_b = 32;
+    SweepRec win[AH2];
 #pragma unroll
-  for (int k = 0; k < kSweepAhead; ++k) win[k] = load_rec(s_pj, k);
-  sweep_step<0, NCAP, !kT>(s_pj, win, mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), valid, lane, sw);
+    for (int k = 0; k < AH2; ++k) win[k] = load_rec(s_pj, (k & 1) ? 32 + (k >> 1) : (k >> 1));
+    sweep2_step<0, AH2>(s_pj, win, mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), s2);
+    sw.ov_lo = s2.ov_lo;
+    sw.ov_hi = s2.ov_hi;
+    const bool upper = s2.best_b < s2.best_a;  // the lower half wins ties (lower indices)
+    sw.best = upper ? s2.best_b : s2.best_a;
+    sw.bj = upper ? s2.bj_b : s2.bj_a;
+  } else {
+    SweepRec win[kSweepAhead];
+#pragma unroll
+    for (int k = 0; k < kSweepAhead; ++k) win[k] = load_rec(s_pj, k);
+    sweep_step<0, NCAP, !kT>(s_pj, win, mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), valid, lane, sw);
+  }
   const float best = sw.best;
   const int bj = sw.bj;
   const uint32_t ov_lo = __builtin_bitreverse32(sw.ov_lo), ov_hi = __builtin_bitreverse32(sw.ov_hi);
