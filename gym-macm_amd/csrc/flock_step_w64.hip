@@ -226,7 +226,7 @@ __device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __re
     const float rx = xj - xi, ry = yj - yi;  // row i: other.position - agent.position
     const float qx = xi - xj, qy = yi - yj;  // row j
     const float d2 = rx * rx + ry * ry;      // b2DistanceSquared (the same for row j)
-    r = sqrt((double)d2);
+    r = obs_sqrt<OT>(d2);
     const double core = obs_atan2_core(fabs((double)rx), fabs((double)ry));
     t1 = wrap_pi(obs_atan2_finish(core, (double)ry, (double)rx) - (double)ai);
     t2 = wrap_pi(obs_atan2_finish(core, (double)qy, (double)qx) - (double)aj);
