@@ -526,7 +526,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   const int nxt = cur ^ 1;
   const unsigned long long lt = lanemask_lt(lane);
 
-  __shared__ float s_cx[W], s_cy[W], s_vx[W], s_vy[W];
+  __shared__ float s_cx[W], s_cy[W];
+  __shared__ float2 s_v[W];  // velocities (one ds_read_b64 / ds_write_b64 per body)
   __shared__ uint32_t s_tab[TCAP];
   __shared__ float s_tln[TCAP], s_tlt[TCAP];
   // contact normals live until the velocity solve ends; the all-pairs records are
@@ -981,8 +982,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     vx = vx * P.damp;
     vy = vy * P.damp;
   }
-  s_vx[lane] = vx;
-  s_vy[lane] = vy;
+  s_v[lane] = make_float2(vx, vy);
 
   // ---- contact normals from start-of-step positions (InitializeVelocityConstraints)
   for (int t = lane; t < T; t += W) {
@@ -1018,14 +1018,13 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       const int a = ab & 0xffffu, b = ab >> 16;
       const float nx = s_tnx[t], ny = s_tny[t];
       float ln = s_tln[t], ltg = s_tlt[t];
-      float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+      const float2 vA0 = s_v[a], vB0 = s_v[b];
+        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
       if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB);
       for (int it = 0; it < P.vel_iters; ++it)
         solve_velocity_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB, kmass, friction);
-      s_vx[a] = vAx;
-      s_vy[a] = vAy;
-      s_vx[b] = vBx;
-      s_vy[b] = vBy;
+      s_v[a] = make_float2(vAx, vAy);
+      s_v[b] = make_float2(vBx, vBy);
       s_tln[t] = ln;
       s_tlt[t] = ltg;
       continue;
@@ -1050,12 +1049,11 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         for (int q = 0; q < KREC; ++q) {
           if (q < L) {
             const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
-            float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+            const float2 vA0 = s_v[a], vB0 = s_v[b];
+        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
             warm_start_contact(vAx, vAy, vBx, vBy, rnx[q], rny[q], rln[q], rlt[q], mA, mB);
-            s_vx[a] = vAx;
-            s_vy[a] = vAy;
-            s_vx[b] = vBx;
-            s_vy[b] = vBy;
+            s_v[a] = make_float2(vAx, vAy);
+            s_v[b] = make_float2(vBx, vBy);
           }
         }
       }
@@ -1064,12 +1062,11 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         for (int q = 0; q < KREC; ++q) {
           if (q < L) {
             const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
-            float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+            const float2 vA0 = s_v[a], vB0 = s_v[b];
+        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
             solve_velocity_contact(vAx, vAy, vBx, vBy, rnx[q], rny[q], rln[q], rlt[q], mA, mB, kmass, friction);
-            s_vx[a] = vAx;
-            s_vy[a] = vAy;
-            s_vx[b] = vBx;
-            s_vy[b] = vBy;
+            s_v[a] = make_float2(vAx, vAy);
+            s_v[b] = make_float2(vBx, vBy);
           }
         }
       }
@@ -1087,12 +1084,11 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         const int t = s_ord[k];
         const uint32_t ab = s_tab[t];
         const int a = ab & 0xffffu, b = ab >> 16;
-        float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+        const float2 vA0 = s_v[a], vB0 = s_v[b];
+        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
         warm_start_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], s_tln[t], s_tlt[t], mA, mB);
-        s_vx[a] = vAx;
-        s_vy[a] = vAy;
-        s_vx[b] = vBx;
-        s_vy[b] = vBy;
+        s_v[a] = make_float2(vAx, vAy);
+        s_v[b] = make_float2(vBx, vBy);
       }
     }
     for (int it = 0; it < P.vel_iters; ++it) {
@@ -1100,13 +1096,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         const int t = s_ord[k];
         const uint32_t ab = s_tab[t];
         const int a = ab & 0xffffu, b = ab >> 16;
-        float vAx = s_vx[a], vAy = s_vy[a], vBx = s_vx[b], vBy = s_vy[b];
+        const float2 vA0 = s_v[a], vB0 = s_v[b];
+        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
         float ln = s_tln[t], ltg = s_tlt[t];
         solve_velocity_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], ln, ltg, mA, mB, kmass, friction);
-        s_vx[a] = vAx;
-        s_vy[a] = vAy;
-        s_vx[b] = vBx;
-        s_vy[b] = vBy;
+        s_v[a] = make_float2(vAx, vAy);
+        s_v[b] = make_float2(vBx, vBy);
         s_tln[t] = ln;
         s_tlt[t] = ltg;
       }
@@ -1118,8 +1113,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // ---- integrate positions --------------------------------------------------
   float cx = p.x, cy = p.y;
   if (act) {
-    vx = s_vx[lane];
-    vy = s_vy[lane];
+    vx = s_v[lane].x;
+    vy = s_v[lane].y;
     const float tx = P.dt * vx, ty = P.dt * vy;
     if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
       const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
