@@ -217,12 +217,13 @@ __device__ __forceinline__ void store4(OT* o, double a, double b, double c, doub
 // to evaluating the two slots separately, with half the f64 atan2 work.
 template <typename OT>
 __device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __restrict__ mask, int S, int i, int j,
-                                             unsigned long long livem, const TdmParams& TP, const float* sx,
-                                             const float* sy, const float* sa) {
+                                             unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                             const float* sa) {
   const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
   double r = 0.0, t1 = 0.0, t2 = 0.0, p1 = 0.0, p2 = 0.0, ty = 0.0;
   if (m) {
-    const float xi = sx[i], yi = sy[i], xj = sx[j], yj = sy[j], ai = sa[i], aj = sa[j];
+    const float2 ci = sc[i], cj = sc[j];
+    const float xi = ci.x, yi = ci.y, xj = cj.x, yj = cj.y, ai = sa[i], aj = sa[j];
     const float rx = xj - xi, ry = yj - yi;  // row i: other.position - agent.position
     const float qx = xi - xj, qy = yi - yj;  // row j
     const float d2 = rx * rx + ry * ry;      // b2DistanceSquared (the same for row j)
@@ -253,8 +254,8 @@ __device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __re
 // 28 pairs (a < b) go two tiles per pass.
 template <typename OT>
 __device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
-                                              unsigned long long livem, const TdmParams& TP, const float* sx,
-                                              const float* sy, const float* sa) {
+                                              unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                              const float* sa) {
   const int S = N - 1;
   const int nb = (N + 7) >> 3;
   const int a = lane >> 3, b = lane & 7;
@@ -262,7 +263,7 @@ __device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __r
     const int i = 8 * I + a;
     for (int J = I + 1; J < nb; ++J) {
       const int j = 8 * J + b;
-      if (i < N && j < N) tdm_obs_pair<OT>(obs, mask, S, i, j, livem, TP, sx, sy, sa);
+      if (i < N && j < N) tdm_obs_pair<OT>(obs, mask, S, i, j, livem, TP, sc, sa);
     }
   }
   // diagonal tiles: pair k < 28 of tile D (row-major over r < c) on lane 32 (D & 1) + k
@@ -276,7 +277,7 @@ __device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __r
   for (int D0 = 0; D0 < nb; D0 += 2) {
     const int D = D0 + (lane >> 5);
     const int i = 8 * D + r, j = 8 * D + c;
-    if (k < 28 && D < nb && j < N) tdm_obs_pair<OT>(obs, mask, S, i, j, livem, TP, sx, sy, sa);
+    if (k < 28 && D < nb && j < N) tdm_obs_pair<OT>(obs, mask, S, i, j, livem, TP, sc, sa);
   }
 }
 
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   const int nxt = cur ^ 1;
   const unsigned long long lt = lanemask_lt(lane);
 
-  __shared__ float s_cx[W], s_cy[W];
+  __shared__ float2 s_c[W];  // positions (one 8-byte access per body)
   __shared__ float2 s_v[W];  // velocities (one ds_read_b64 / ds_write_b64 per body)
   __shared__ uint32_t s_tab[TCAP];
   __shared__ float s_tln[TCAP], s_tlt[TCAP];
@@ -633,8 +634,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       rim[c] = cimp[k];
     }
   }
-  s_cx[lane] = p.x;
-  s_cy[lane] = p.y;
+  s_c[lane] = p;
   if (lane < TCAP / 32) s_cvis[lane] = 0u;
   s_oldm[2 * lane] = 0u;
 #pragma unroll
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     alive0_m = __ballot(act);
     att_m = __ballot(attacking);
     s_hpd[lane] = hp;
-    __syncthreads();  // s_cx / s_cy / s_hpd visible
+    __syncthreads();  // s_c / s_hpd visible
     if (att_m) {
       // b2World::RayCast + RayCastClosestCallback (cm_framework.py:56-86): each
       // b2CircleShape::RayCast hit clips maxFraction to its fraction; candidates in
@@ -716,7 +716,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       float maxf = 1.0f;
       for (unsigned long long m = alive0_m; m; m &= m - 1ull) {
         const int j = __builtin_ctzll(m);
-        const float sx = p.x - s_cx[j], sy = p.y - s_cy[j];  // s = p1 - position
+        const float2 cj = s_c[j];
+        const float sx = p.x - cj.x, sy = p.y - cj.y;  // s = p1 - position
         const float bb = (sx * sx + sy * sy) - rad2;
         const float c = sx * rvx + sy * rvy;
         const float sigma = c * c - rrr * bb;
@@ -778,7 +779,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       const int a = ab & 0xffffu, b = ab >> 16;
       // TDM: contacts of a body that died this step were destroyed with its proxy
       if (!kT || ((livem >> a) & (livem >> b) & 1ull)) {
-        const float dx = s_cx[b] - s_cx[a], dy = s_cy[b] - s_cy[a];
+        const float2 ca = s_c[a], cb = s_c[b];
+        const float dx = cb.x - ca.x, dy = cb.y - ca.y;
         touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
         atomicOr(&s_oldm[2 * a + (b >> 5)], 1u << (b & 31));
         atomicOr(&s_oldm[2 * b + (a >> 5)], 1u << (a & 31));
@@ -988,7 +990,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   for (int t = lane; t < T; t += W) {
     const uint32_t ab = s_tab[t];
     const int a = ab & 0xffffu, b = ab >> 16;
-    const float pax = s_cx[a], pay = s_cy[a], pbx = s_cx[b], pby = s_cy[b];
+    const float2 pa = s_c[a], pb = s_c[b];
+    const float pax = pa.x, pay = pa.y, pbx = pb.x, pby = pb.y;
     float nx = 1.0f, ny = 0.0f;
     const float ddx = pax - pbx, ddy = pay - pby;
     if (ddx * ddx + ddy * ddy > kEps * kEps) {
@@ -1123,8 +1126,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     }
     cx = cx + P.dt * vx;
     cy = cy + P.dt * vy;
-    s_cx[lane] = cx;
-    s_cy[lane] = cy;
+    s_c[lane] = make_float2(cx, cy);
   }
   __syncthreads();
   STAMP(6);
@@ -1137,7 +1139,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     if (c1 - c0 == 1) {  // single contact: registers
       const uint32_t ab = s_tab[s_ord[c0]];
       const int a = ab & 0xffffu, b = ab >> 16;
-      float cAx = s_cx[a], cAy = s_cy[a], cBx = s_cx[b], cBy = s_cy[b];
+      const float2 cA0 = s_c[a], cB0 = s_c[b];
+        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
       for (int it = 0; it < P.pos_iters; ++it) {
         const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
         const float min_sep = bmin(0.0f, sep);
@@ -1146,10 +1149,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
           break;
         }
       }
-      s_cx[a] = cAx;
-      s_cy[a] = cAy;
-      s_cx[b] = cBx;
-      s_cy[b] = cBy;
+      s_c[a] = make_float2(cAx, cAy);
+      s_c[b] = make_float2(cBx, cBy);
       s_isolved[I] = (uint8_t)solved;
       continue;
     }
@@ -1164,13 +1165,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         for (int q = 0; q < KREC; ++q) {
           if (q < L) {
             const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
-            float cAx = s_cx[a], cAy = s_cy[a], cBx = s_cx[b], cBy = s_cy[b];
+            const float2 cA0 = s_c[a], cB0 = s_c[b];
+        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
             const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
             min_sep = bmin(min_sep, sep);
-            s_cx[a] = cAx;
-            s_cy[a] = cAy;
-            s_cx[b] = cBx;
-            s_cy[b] = cBy;
+            s_c[a] = make_float2(cAx, cAy);
+            s_c[b] = make_float2(cBx, cBy);
           }
         }
         if (min_sep >= -3.0f * kLinearSlop) {
@@ -1186,13 +1186,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       for (int k = c0; k < c1; ++k) {
         const uint32_t ab = s_tab[s_ord[k]];
         const int a = ab & 0xffffu, b = ab >> 16;
-        float cAx = s_cx[a], cAy = s_cy[a], cBx = s_cx[b], cBy = s_cy[b];
+        const float2 cA0 = s_c[a], cB0 = s_c[b];
+        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
         const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
         min_sep = bmin(min_sep, sep);
-        s_cx[a] = cAx;
-        s_cy[a] = cAy;
-        s_cx[b] = cBx;
-        s_cy[b] = cBy;
+        s_c[a] = make_float2(cAx, cAy);
+        s_c[b] = make_float2(cBx, cBy);
       }
       if (min_sep >= -3.0f * kLinearSlop) {
         solved = 1;
@@ -1235,8 +1234,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // ---- SynchronizeFixtures: fat-AABB update ------------------------------------
   float4 fn = fo;
   if (act) {
-    cx = s_cx[lane];
-    cy = s_cy[lane];
+    cx = s_c[lane].x;
+    cy = s_c[lane].y;
     const float r = P.radius;
     const float c0x = p.x, c0y = p.y;
     const float lox = bmin(c0x - r, cx - r), loy = bmin(c0y - r, cy - r);
@@ -1263,7 +1262,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     r.pad = make_float2(0.0f, 0.0f);
     s_pj[lane] = r;
   }
-  __syncthreads();  // s_pj and final s_cx/s_cy visible to every lane
+  __syncthreads();  // s_pj and final s_c visible to every lane
   STAMP(9);
 
   // ---- contact set, new pairs, nearest neighbour ---------------------------------
@@ -1375,7 +1374,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       if (nbr_out) nbr_out[ag] = bj;
       if (obs) {
         const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-        const float rx = s_cx[bj] - cx, ry = s_cy[bj] - cy;
+        const float2 cn = s_c[bj];
+        const float rx = cn.x - cx, ry = cn.y - cy;
         write_obs<OT>(obs + ag * od, P.coord, ang, best, rx, ry, tdx, tdy, td2);
       }
       // ---- state write-back ----
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
     tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
-                     s_cx, s_cy, s_ang);
+                     s_c, s_ang);
   }
   STAMP(12);
 
@@ -1594,7 +1594,8 @@ __global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, 
   const int C = P.max_contacts;
   const bool act = lane < N;
   const size_t ag = (size_t)e * N + lane;
-  __shared__ float s_x[W], s_y[W], s_a[W];
+  __shared__ float2 s_p[W];
+  __shared__ float s_a[W];
   float2 p = make_float2(0.0f, 0.0f);
   float4 f = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   float ang = 0.0f;
@@ -1625,14 +1626,13 @@ __global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, 
     st = MACM_ST_CONTACT_OVERFLOW;
     total = C;
   }
-  s_x[lane] = p.x;
-  s_y[lane] = p.y;
+  s_p[lane] = p;
   s_a[lane] = ang;
   const unsigned long long livem = __ballot(act);
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
   tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
-                   s_x, s_y, s_a);
+                   s_p, s_a);
   if (lane == 0) {
     B.ccount[cur][e] = total;
     B.step_count[e] = 0;
@@ -1653,12 +1653,12 @@ __global__ __launch_bounds__(W) void tdm_observe_w64(StepParams P, WorldBuffers 
   const int lane = threadIdx.x;
   const int N = P.n_agents;
   const size_t ag = (size_t)e * N + lane;
-  __shared__ float s_x[W], s_y[W], s_a[W];
+  __shared__ float2 s_p[W];
+  __shared__ float s_a[W];
   bool live = false;
   if (lane < N) {
     const float2 p = B.pos[ag];
-    s_x[lane] = p.x;
-    s_y[lane] = p.y;
+    s_p[lane] = p;
     s_a[lane] = B.angle[ag];
     live = TB.alive[ag] != 0;
   }
@@ -1666,7 +1666,7 @@ __global__ __launch_bounds__(W) void tdm_observe_w64(StepParams P, WorldBuffers 
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
   tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
-                   s_x, s_y, s_a);
+                   s_p, s_a);
 }
 
 // ---- host-side launchers (C++ linkage, used by macm_capi.hip) -----------------
