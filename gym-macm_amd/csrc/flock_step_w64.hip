@@ -136,7 +136,11 @@ __device__ __forceinline__ double wrap_pi(double t) {
 // data cannot both be SGPRs): lane `l` of v receives the uniform value x. The s_nop covers
 // the SALU write of M0 just before.
 __device__ __forceinline__ uint32_t writelane_m0(int x, int l, uint32_t v) {
-  asm volatile("s_nop 1\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "{m0}"(l));
+  // x and l are wave-uniform; readfirstlane makes that visible where the compiler cannot
+  // prove it (an SGPR operand)
+  asm volatile("s_nop 1\n\tv_writelane_b32 %0, %1, m0"
+               : "+v"(v)
+               : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(__builtin_amdgcn_readfirstlane(l)));
   return v;
 }
 
@@ -342,6 +346,11 @@ __device__ __forceinline__ float solve_position_contact(float& cAx, float& cAy, 
   cBy = cBy + mB * Py;
   return sep;
 }
+
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
 
 struct SweepState {
   uint32_t ov_lo, ov_hi;  // partner row of this lane's agent (written by lane j = row owner)
@@ -863,8 +872,11 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     const uint32_t tm_lo = (uint32_t)tmask, tm_hi = (uint32_t)(tmask >> 32);
     const uint32_t tm1_lo = (uint32_t)tmask1, tm1_hi = (uint32_t)(tmask1 >> 32);
     uint32_t ordv = 0u, ordv1 = 0u, bodv = 0u, islv = 0u, icv = 0u, ibv = 0u, stk = 0u;
-    unsigned long long vis = ~hasdeg, cvis = 0ull, cvis1 = 0ull;
     int nord = 0, nisl = 0, nb = 0;
+    // one instantiation per width so that the common T <= 64 walk carries no second word
+    auto dfs = [&](auto wide) {
+    constexpr bool W2 = decltype(wide)::value;
+    unsigned long long vis = ~hasdeg, cvis = 0ull, cvis1 = 0ull;
     for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
       const int s = 63 - __clzll(todo);
       icv = writelane_m0(nord, nisl, icv);  // s_ic[nisl]
@@ -883,7 +895,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
           while (m) {
             const int t = __builtin_ctzll(m);
             m &= m - 1ull;
-            if (nord < 64) ordv = writelane_m0(base + t, nord, ordv);  // s_ord[nord]
+            if (!W2 || nord < 64) ordv = writelane_m0(base + t, nord, ordv);  // s_ord[nord]
             else ordv1 = writelane_m0(base + t, nord - 64, ordv1);
             ++nord;
             const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tab, t);
@@ -899,7 +911,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
                                 (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_lo, b)) & ~cvis;
         cvis |= m;
         walk(m, 0, tabv);
-        if (TMW == 2 && T > 64) {
+        if constexpr (W2) {
           unsigned long long m1 = (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_hi, b) << 32) |
                                    (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_lo, b)) & ~cvis1;
           cvis1 |= m1;
@@ -908,6 +920,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       }
       ++nisl;
     }
+    };
+    if (TMW == 2 && T > 64) dfs(BoolC<true>{});
+    else dfs(BoolC<false>{});
     icv = writelane_m0(nord, nisl, icv);
     ibv = writelane_m0(nb, nisl, ibv);
     if (lane < nord) s_ord[lane] = (uint8_t)ordv;
