@@ -784,6 +784,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       lam = cimp[k];
     }
     bool touch = false;
+    float tnx = 1.0f, tny = 0.0f;
     if (k < M) {
       const int a = ab & 0xffffu, b = ab >> 16;
       // TDM: contacts of a body that died this step were destroyed with its proxy
@@ -791,6 +792,15 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         const float2 ca = s_c[a], cb = s_c[b];
         const float dx = cb.x - ca.x, dy = cb.y - ca.y;
         touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+        if (touch) {
+          // the contact normal from the same start-of-step positions (InitializeVelocityConstraints:
+          // (1, 0) when the centres coincide; (pA - pB)^2 == (pB - pA)^2 exactly)
+          if (dx * dx + dy * dy > kEps * kEps) {
+            tnx = dx;
+            tny = dy;
+            normalize(tnx, tny);
+          }
+        }
         atomicOr(&s_oldm[2 * a + (b >> 5)], 1u << (b & 31));
         atomicOr(&s_oldm[2 * b + (a >> 5)], 1u << (a & 31));
       }
@@ -807,6 +817,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         s_tab[slot] = ab;
         s_tln[slot] = P.warm_starting ? dt_ratio * lam.x : 0.0f;
         s_tlt[slot] = P.warm_starting ? dt_ratio * lam.y : 0.0f;
+        s_tnx[slot] = tnx;
+        s_tny[slot] = tny;
       }
     }
     T += __popcll(m);
@@ -1001,22 +1013,6 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   }
   s_v[lane] = make_float2(vx, vy);
 
-  // ---- contact normals from start-of-step positions (InitializeVelocityConstraints)
-  for (int t = lane; t < T; t += W) {
-    const uint32_t ab = s_tab[t];
-    const int a = ab & 0xffffu, b = ab >> 16;
-    const float2 pa = s_c[a], pb = s_c[b];
-    const float pax = pa.x, pay = pa.y, pbx = pb.x, pby = pb.y;
-    float nx = 1.0f, ny = 0.0f;
-    const float ddx = pax - pbx, ddy = pay - pby;
-    if (ddx * ddx + ddy * ddy > kEps * kEps) {
-      nx = pbx - pax;
-      ny = pby - pay;
-      normalize(nx, ny);
-    }
-    s_tnx[t] = nx;
-    s_tny[t] = ny;
-  }
   __syncthreads();
   STAMP(4);
 
