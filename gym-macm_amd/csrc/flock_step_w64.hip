@@ -26,13 +26,15 @@
 // restricted to the body's contacts, so the DFS below visits contacts in exactly
 // Box2D's order and the solver reproduces Box2D's rounding sequence.
 //
-// Where the time goes (tools/phase_profile.py, profiles/r01/): the step is
-// latency-bound, not bandwidth-bound — a few dependent global round trips plus
-// short serial chains (DFS, per-island Gauss-Seidel). Hence: every global load
-// the step needs is issued up front; list entries and their impulses arrive in
-// one round trip and stay in registers; all-pairs loops broadcast lane values
-// with v_readlane (uniform j) instead of LDS round trips; the DFS seeds only
-// bodies that have touching edges; per-env counters instead of global atomics.
+// Where the time goes (tools/phase_profile.py, tools/timeline.py, profiles/r01/): the
+// step is latency-bound, not bandwidth-bound, and its duration is that of the envs with
+// the most touching contacts, whose serial Box2D chain (island DFS, Gauss-Seidel, position
+// passes) outlasts the other waves. Hence: every global load the step needs is issued up
+// front; list entries and their impulses arrive in one round trip and stay in registers;
+// the chain runs at raised issue priority (s_setprio), the DFS walks scalar bit masks
+// through v_readlane / v_writelane, small islands keep their records in registers, and
+// bodies sit in LDS as float2; the all-pairs sweep reads records by LDS broadcast in two
+// interleaved chains; per-env counters instead of global atomics.
 //
 // Exactness notes (checked by tests/test_gpu_parity.py against the oracle):
 //   * fixedRotation bodies have invI = 0 and w = 0, so every angular term in the
