@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 B_ALG = 107  # bytes per agent-step: state r+w 2x40, action 3, obs 20, reward 4
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+SCALAR_SWEEP_MIN_ENVS = 2048  # = kScalarSweepMinEnvs in gym-macm_amd/csrc/flock_step_w64.hip
 
 
 def log(msg):
@@ -233,7 +234,10 @@ def main():
             kname = f"env_step_w64<1, {ncap}, float>"
         else:
             # N > 64: the workgroup path's three launches per step (split step; kernel_ms covers all)
-            kname = (f"env_step_w64<0, {ncap}, float>" if N <= 64
+            # N > 32 with >= 2048 envs: the scalar-sweep instantiation (flock_step_w64.hip,
+            # kScalarSweepMinEnvs)
+            scal = ", true" if (ncap == 64 and E >= SCALAR_SWEEP_MIN_ENVS) else ""
+            kname = (f"env_step_w64<0, {ncap}, float{scal}>" if N <= 64
                      else "flock_step_wg_a + flock_solve_wg + flock_step_wg_c<float>")
         traffic = None
         tj = load_traffic(args.traffic_json)

@@ -432,6 +432,12 @@ __device__ __forceinline__ void sweep_step(const PairRec* s_pj, SweepRec* win, f
   if constexpr (J + 1 < NCAP) sweep_step<J + 1, NCAP, NN>(s_pj, win, fn_lo, fn_hi, cme, valid, lane, st);
 }
 
+// The sweep's differences as scalar VALU (SCAL) or as v_pk_* pairs: with 16 envs per CU (the
+// waves share the SIMDs' issue) the scalar form is 1.9% faster per step, with 4 per CU (1024
+// envs: latency-bound) the packed form is 2.2% faster (profiles/r01/ab2 s36). The float32 launch
+// with N > 32 picks by the number of envs.
+constexpr int kScalarSweepMinEnvs = 2048;
+
 // NCAP = 64 with the nearest neighbour: the records of the two halves are taken in turns
 // (0, 32, 1, 33, ...) with a running minimum per half, so the two loop-carried chains (the
 // overlap bits of ov_lo / ov_hi and the minimum of each half) are independent and their
@@ -444,7 +450,7 @@ struct SweepState2 {
   int bj_a, bj_b;
 };
 
-template <int S, int AH>
+template <int S, int AH, bool SCAL>
 __device__ __forceinline__ void sweep2_step(const PairRec* s_pj, SweepRec* win, fvec2 fn_lo, fvec2 fn_hi,
                                             fvec2 cme, SweepState2& st) {
   constexpr int JA = S, JB = 32 + S;  // records of this step: JA (lower half), JB (upper half)
@@ -458,13 +464,23 @@ __device__ __forceinline__ void sweep2_step(const PairRec* s_pj, SweepRec* win, 
     constexpr int K = 2 * S + 1 + AH;
     win[(2 * S + 1) % AH] = load_rec(s_pj, (K & 1) ? 32 + (K >> 1) : (K >> 1));
   }
+  float sa, sb, d2a, d2b;
+  if constexpr (SCAL) {  // see kScalarSweepMinEnvs
+  sa = fmaxf(fmaxf(qa.fn.x - fn_hi.x, qa.fn.y - fn_hi.y), fmaxf(fn_lo.x - qa.fn.z, fn_lo.y - qa.fn.w));
+  sb = fmaxf(fmaxf(qb.fn.x - fn_hi.x, qb.fn.y - fn_hi.y), fmaxf(fn_lo.x - qb.fn.z, fn_lo.y - qb.fn.w));
+  const float dax = qa.c.x - cme.x, day = qa.c.y - cme.y, dbx = qb.c.x - cme.x, dby = qb.c.y - cme.y;
+  d2a = dax * dax + day * day;
+  d2b = dbx * dbx + dby * dby;
+  } else {
   const fvec2 aa = mk2(qa.fn.x, qa.fn.y) - fn_hi, ba = fn_lo - mk2(qa.fn.z, qa.fn.w);
   const fvec2 ab = mk2(qb.fn.x, qb.fn.y) - fn_hi, bb = fn_lo - mk2(qb.fn.z, qb.fn.w);
-  const float sa = fmaxf(fmaxf(aa.x, aa.y), fmaxf(ba.x, ba.y));
-  const float sb = fmaxf(fmaxf(ab.x, ab.y), fmaxf(bb.x, bb.y));
+  sa = fmaxf(fmaxf(aa.x, aa.y), fmaxf(ba.x, ba.y));
+  sb = fmaxf(fmaxf(ab.x, ab.y), fmaxf(bb.x, bb.y));
   const fvec2 da = mk2(qa.c.x, qa.c.y) - cme, db = mk2(qb.c.x, qb.c.y) - cme;
   const fvec2 dda = da * da, ddb = db * db;
-  const float d2a = dda.x + dda.y, d2b = ddb.x + ddb.y;
+  d2a = dda.x + dda.y;
+  d2b = ddb.x + ddb.y;
+  }
   unsigned long long ca, cb, ma, mb;
   asm volatile(
       "v_cmp_nlt_f32_e64 %[ca], 0, %[sa]\n\t"
@@ -483,7 +499,7 @@ __device__ __forceinline__ void sweep2_step(const PairRec* s_pj, SweepRec* win, 
         [jb] "+v"(st.bj_b), [ca] "=&s"(ca), [cb] "=&s"(cb), [ma] "=&s"(ma), [mb] "=&s"(mb)
       : [sa] "v"(sa), [sb] "v"(sb), [da] "v"(d2a), [db] "v"(d2b), [JA] "i"(JA), [JB] "i"(JB));
   if constexpr ((S & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-  if constexpr (S + 1 < 32) sweep2_step<S + 1, AH>(s_pj, win, fn_lo, fn_hi, cme, st);
+  if constexpr (S + 1 < 32) sweep2_step<S + 1, AH, SCAL>(s_pj, win, fn_lo, fn_hi, cme, st);
 }
 
 // New-pair compaction in descending (a, b) order: lane a owns the bitmask of
@@ -516,7 +532,7 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
 // relative observation; `TP`/`TB` are unused for Flock.
 // waves_per_eu(4): <= 128 VGPRs, so the 16 envs per CU of a 4096-env launch are
 // resident together (the unrolled sweep would otherwise hoist every LDS record).
-template <int MODE, int NCAP, typename OT>
+template <int MODE, int NCAP, typename OT, bool SCAL = false>
 __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_step_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
                                                   int cur, const void* __restrict__ actions,
                                                   OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
@@ -1306,7 +1322,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     SweepRec win[AH2];
 #pragma unroll
     for (int k = 0; k < AH2; ++k) win[k] = load_rec(s_pj, (k & 1) ? 32 + (k >> 1) : (k >> 1));
-    sweep2_step<0, AH2>(s_pj, win, mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), s2);
+    sweep2_step<0, AH2, SCAL>(s_pj, win, mk2(fn.x, fn.y), mk2(fn.z, fn.w), mk2(cx, cy), s2);
     sw.ov_lo = s2.ov_lo;
     sw.ov_hi = s2.ov_hi;
     const bool upper = s2.best_b < s2.best_a;  // the lower half wins ties (lower indices)
@@ -1700,6 +1716,9 @@ hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, 
   } else {
     if (small)
       hipLaunchKernelGGL((env_step_w64<kFlock, 32, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
+                         (float*)obs, nbr, rew, coll, done);
+    else if (P.n_envs >= kScalarSweepMinEnvs)
+      hipLaunchKernelGGL((env_step_w64<kFlock, 64, float, true>), grid, block, 0, s, P, B, TP, TB, cur, actions,
                          (float*)obs, nbr, rew, coll, done);
     else
       hipLaunchKernelGGL((env_step_w64<kFlock, 64, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,

@@ -30,7 +30,7 @@ def kernel_means(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="env_step_w64<0, 64, float>")
+    ap.add_argument("--kernel", default="env_step_w64<0, 64, float, true>")
     ap.add_argument("--policy", default="random")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--agents", type=int, default=64)
