@@ -148,6 +148,37 @@ __device__ __forceinline__ double obs_sqrt(float x) {
   else return sqrt((double)x);
 }
 
+// Correctly rounded 1.0f / x and sqrtf(x) in fewer instructions than HIP's default lowering,
+// for the contact normal (b2Vec2::Normalize), which sits on the serial position-solve chain.
+// rcp_rn: v_rcp_f32 plus one fma Newton step; equals 1.0f / x for every float32 x in
+// [2^-23, 2^64] (Normalize only divides by len >= FLT_EPSILON; len <= sqrt(FLT_MAX) < 2^64).
+// sqrt_rn: v_sqrt_f32 with the +-1 ulp residual correction of the default lowering but
+// without its denormal scaling; equals sqrtf(x) for every float32 x >= 2^-48, and below
+// that both results are < FLT_EPSILON, so Normalize takes the same branch.
+// Both checked on the device over every float32 input (tools/rcp_sqrt_gpu_check.hip).
+__device__ __forceinline__ float rcp_rn(float x) {
+#ifdef MACM_LIB_SQRT_DIV
+  return 1.0f / x;
+#else
+  const float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  return __builtin_fmaf(e, y, y);
+#endif
+}
+
+__device__ __forceinline__ float sqrt_rn(float x) {
+#ifdef MACM_LIB_SQRT_DIV
+  return sqrtf(x);
+#else
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+  const float su = __uint_as_float(__float_as_uint(s) + 1u);
+  float r = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
+  r = __builtin_fmaf(-su, s, x) > 0.0f ? su : r;
+  return r;
+#endif
+}
+
 // Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).
 constexpr int kMtStride = 640;  // words per env: 624 state words, [624] = position
 

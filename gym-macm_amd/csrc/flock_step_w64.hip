@@ -104,9 +104,13 @@ __device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bm
 #ifdef MACM_EXACT_ZERO_SIGNS
 __device__ __forceinline__ float smax(float a, float b) { return bmax(a, b); }
 __device__ __forceinline__ float sclamp(float a, float lo, float hi) { return bclamp(a, lo, hi); }
-#else
+#elif defined(MACM_NO_MED3)
 __device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
 __device__ __forceinline__ float sclamp(float a, float lo, float hi) { return fmaxf(lo, fminf(a, hi)); }
+#else
+// sclamp as one v_med3_f32: the median of (a, lo, hi) is the clamp for lo <= hi and non-NaN a.
+__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
 #endif
 
 // b2TestOverlap
@@ -118,11 +122,11 @@ __device__ __forceinline__ bool overlap(float4 a, float4 b) {
   return true;
 }
 
-// b2Vec2::Normalize
+// b2Vec2::Normalize (sqrt_rn / rcp_rn: the correctly rounded sqrtf and 1.0f / len, flock_common.hpp)
 __device__ __forceinline__ void normalize(float& x, float& y) {
-  const float len = sqrtf(x * x + y * y);
+  const float len = sqrt_rn(x * x + y * y);
   if (len < kEps) return;
-  const float inv = 1.0f / len;
+  const float inv = rcp_rn(len);
   x *= inv;
   y *= inv;
 }

@@ -64,10 +64,10 @@ __device__ __forceinline__ bool overlap(float4 a, float4 b) {  // b2TestOverlap
 __device__ __forceinline__ float sep_max(float4 a, float4 b) {
   return fmaxf(fmaxf(b.x - a.z, b.y - a.w), fmaxf(a.x - b.z, a.y - b.w));
 }
-__device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Normalize
-  const float len = sqrtf(x * x + y * y);
+__device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Normalize (see sqrt_rn / rcp_rn)
+  const float len = sqrt_rn(x * x + y * y);
   if (len < kEps) return;
-  const float inv = 1.0f / len;
+  const float inv = rcp_rn(len);
   x *= inv;
   y *= inv;
 }
