@@ -231,13 +231,13 @@ def main():
         achieved_gbs = b_alg * E * N / (kernel_ms * 1e-3) / 1e9
         ncap = 32 if N <= 32 else 64
         if args.env == "tdm":
-            kname = f"env_step_w64<1, {ncap}, float>"
+            kname = f"env_step_w64<1, {ncap}, float, false>"
         else:
             # N > 64: the workgroup path's three launches per step (split step; kernel_ms covers all)
             # N > 32 with >= 2048 envs: the scalar-sweep instantiation (flock_step_w64.hip,
             # kScalarSweepMinEnvs)
-            scal = ", true" if (ncap == 64 and E >= SCALAR_SWEEP_MIN_ENVS) else ""
-            kname = (f"env_step_w64<0, {ncap}, float{scal}>" if N <= 64
+            scal = "true" if (ncap == 64 and E >= SCALAR_SWEEP_MIN_ENVS) else "false"
+            kname = (f"env_step_w64<0, {ncap}, float, {scal}>" if N <= 64
                      else "flock_step_wg_a + flock_solve_wg + flock_step_wg_c<float>")
         traffic = None
         tj = load_traffic(args.traffic_json)

@@ -2,7 +2,7 @@
 that bench.py reads for `roofline.traffic`.
 
     python tools/pmc_summary.py gpurun_out/<dir> --envs 4096 --agents 64 -o profiles/pmc_flock_step.json
-    python tools/pmc_summary.py gpurun_out/<dir> --kernel "env_step_w64<1, 32, float>" --agents 32 \
+    python tools/pmc_summary.py gpurun_out/<dir> --kernel "env_step_w64<1, 32, float, false>" --agents 32 \
         -o profiles/pmc_tdm_step.json
 
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE
