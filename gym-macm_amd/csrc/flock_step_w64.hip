@@ -61,6 +61,15 @@ constexpr int RCH = 2;      // list chunks (of 64 entries) cached in registers
 #endif
 constexpr int KREC = MACM_REC_ISLAND;
 constexpr int KRECA = KREC > 0 ? KREC : 1;
+// In a wave that has 2..KREC-contact islands, its single-contact islands join the same
+// register-record solve (as islands of one contact) instead of running their own register
+// loop before it: the wave then walks max-island-size x 9 updates instead of 9 more on top
+// (single-contact lanes pay the LDS round trip that the multi-contact lanes wait on anyway).
+#ifdef MACM_NO_MERGE_SINGLETONS
+constexpr bool kMergeSingletons = false;
+#else
+constexpr bool kMergeSingletons = KREC > 1;
+#endif
 #ifdef MACM_NO_CHAIN_PRIORITY  // A/B knob: no s_setprio around the serial solver chain
 constexpr bool kChainPriority = false;
 #else
@@ -1046,9 +1055,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // ---- warm start + velocity iterations, one lane per island ---------------
   // A single-contact island (the common case) runs entirely in registers; larger
   // islands go through LDS in Box2D's order.
+  // any 2..KREC-contact island in this wave (wave-uniform; nisl <= ICAP < W, one island per lane)
+  const int lsz = lane < nisl ? s_ic[lane + 1] - s_ic[lane] : 0;
+  const bool krec_wave = kMergeSingletons && __builtin_amdgcn_ballot_w64(lsz >= 2 && lsz <= KREC) != 0ull;
   for (int I = lane; I < nisl; I += W) {
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
-    if (c1 - c0 == 1) {
+    if (c1 - c0 == 1 && !krec_wave) {
       const int t = s_ord[c0];
       const uint32_t ab = s_tab[t];
       const int a = ab & 0xffffu, b = ab >> 16;
@@ -1169,7 +1181,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     s_imin[I] = 0xffffffffu;  // island sleep decision below
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
     int solved = 0;
-    if (c1 - c0 == 1) {  // single contact: registers
+    if (c1 - c0 == 1 && !krec_wave) {  // single contact: registers
       const uint32_t ab = s_tab[s_ord[c0]];
       const int a = ab & 0xffffu, b = ab >> 16;
       const float2 cA0 = s_c[a], cB0 = s_c[b];
