@@ -179,6 +179,26 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 #endif
 }
 
+// RN(n / K) for a loop-invariant K > 0 (the position solve's -C / (mA + mB)) from rK = RN(1 / K),
+// hoisted out of the loop: q0 = n * rK is within a few ulps, one fma correction makes it
+// faithful and a second is Markstein's correction step, which returns the correctly rounded
+// quotient for a faithful one and rK = RN(1 / K), away from underflow. Here n = -b2Clamp(0.2f *
+// fl(sep + 0.005f), -0.2f, 0) is 0 or >= 2^-35: a nonzero fl(sep + 0.005f) is >= 0.0025 in
+// magnitude unless sep is in (-0.01, -0.0025), where the sum is exact (Sterbenz) and a multiple
+// of ulp(0.0025) = 2^-32. Checked on the device for every float32 n in {0} u [2^-40, 0.2] and K of
+// the default and 255 random configs: 0 mismatches (tools/rcp_sqrt_gpu_check.hip; below 2^-40
+// the sequence can differ, and is never given such n).
+__device__ __forceinline__ float div_by_invariant(float n, float K) {
+#ifdef MACM_LIB_SQRT_DIV
+  return n / K;
+#else
+  const float rK = 1.0f / K;
+  const float q0 = n * rK;
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-K, q0, n), rK, q0);
+  return __builtin_fmaf(__builtin_fmaf(-K, q1, n), rK, q1);
+#endif
+}
+
 // Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).
 constexpr int kMtStride = 640;  // words per env: 624 state words, [624] = position
 

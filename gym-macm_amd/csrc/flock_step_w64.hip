@@ -353,7 +353,7 @@ __device__ __forceinline__ float solve_position_contact(float& cAx, float& cAy, 
   const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - radius - radius;
   const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
   const float K = mA + mB;
-  const float imp = K > 0.0f ? -Cc / K : 0.0f;
+  const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
   const float Px = imp * nx, Py = imp * ny;
   cAx = cAx - mA * Px;
   cAy = cAy - mA * Py;

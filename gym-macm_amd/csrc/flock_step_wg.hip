@@ -622,7 +622,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers
         min_sep = bmin(min_sep, sep);
         const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
         const float K = mA + mB;
-        const float imp = K > 0.0f ? -Cc / K : 0.0f;
+        const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
         const float Px = imp * nx, Py = imp * ny;
         ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
         cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
@@ -1354,7 +1354,7 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
   const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
   const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
   const float K = mA + mB;
-  const float imp = K > 0.0f ? -Cc / K : 0.0f;
+  const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
   const float Px = imp * nx, Py = imp * ny;
   ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
   cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
