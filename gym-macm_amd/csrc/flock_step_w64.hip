@@ -70,6 +70,9 @@ constexpr bool kMergeSingletons = false;
 #else
 constexpr bool kMergeSingletons = KREC > 1;
 #endif
+#ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
+#define MACM_PRIO2_T 3
+#endif
 #ifdef MACM_NO_CHAIN_PRIORITY  // A/B knob: no s_setprio around the serial solver chain
 constexpr bool kChainPriority = false;
 #else
@@ -1250,7 +1253,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // with >= 3 touching contacts (the envs that end last) above those: -2% per step against a
   // single level (profiles/r01/ab2 s24/s25; thresholds 2 and 4, or a third level, did no better).
   if (kChainPriority && hasdeg) {
-    if (T >= 3) __builtin_amdgcn_s_setprio(2);
+    if (T >= MACM_PRIO2_T) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_s_setprio(1);
   }
   // ---- per-body sleep clock ---------------------------------------------------
