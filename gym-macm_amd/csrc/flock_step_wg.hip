@@ -49,9 +49,12 @@ __device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bm
 #ifdef MACM_EXACT_ZERO_SIGNS
 __device__ __forceinline__ float smax(float a, float b) { return bmax(a, b); }
 __device__ __forceinline__ float sclamp(float a, float lo, float hi) { return bclamp(a, lo, hi); }
-#else
+#elif defined(MACM_NO_MED3)
 __device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
 __device__ __forceinline__ float sclamp(float a, float lo, float hi) { return fmaxf(lo, fminf(a, hi)); }
+#else  // one v_med3_f32 (as in flock_step_w64.hip)
+__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
 #endif
 __device__ __forceinline__ bool overlap(float4 a, float4 b) {  // b2TestOverlap
   const float d1x = b.x - a.z, d1y = b.y - a.w;
