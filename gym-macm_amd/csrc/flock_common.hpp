@@ -32,6 +32,7 @@ struct StepParams {
   int32_t n_envs, n_agents, n_targets, max_contacts;  // TDM: n_targets = 0
   int32_t vel_iters, pos_iters, warm_starting;
   int32_t action_mode, reward_mode, coord;
+  int32_t force_spill;  // test hook (macm_world_set_debug): every env takes the spill step
   float dt;          // fl32(1.0 / hz)                       cm_framework.py:182-185 -> world.Step
   float inv_dt;      // 1.0f / dt                            b2World::Step
   float inv_mass;    // 1 / (density * b2_pi * r * r)        b2CircleShape::ComputeMass
@@ -79,7 +80,25 @@ struct WorldBuffers {
   float2* x_vout;                // [E, N]    velocities after the solve (max-translation clamped)
   uint8_t* x_deg;                // [E, N]    body has touching edges
   uint8_t* x_isolv;              // [E, IS]   island position-solved
+  // Spill step (flock_spill.hpp): per-env HBM working set for envs whose touching contacts exceed
+  // the fast kernels' LDS capacities; capacity C = max_contacts (touching contacts are in the list).
+  uint32_t* sp_tab;              // [E, C]    touching contacts in list order (bit 31: DFS visited)
+  uint32_t* sp_adj;              // [E, 2C]   CSR edges (touching-contact indices)
+  uint32_t* sp_ord;              // [E, C]    island order -> touching index
+  float4* sp_cst;                // [E, C]    island-ordered records (ab bits, nx, ny, 0)
+  float2* sp_cim;                // [E, C]    their impulses
+  float2* sp_lam;                // [E, C]    list-order impulses of the touching contacts
+  void* sp_rec;                  // [E, N]    pair-sweep records (48 B) when not in LDS (N > 64)
+  uint32_t* spill_count;         // [E]       steps taken by the spill step (macm_world_spilled)
+  uint32_t* host_status;         // mapped pinned host word: nonzero once any env set a status bit
 };
+
+// A status bit was set in some env: tell the host without a synchronisation (macm_world_step
+// reads the word before each launch). Rare path; a plain store, so bits of different envs may
+// overwrite each other (the per-env B.status keeps the exact OR for macm_world_status).
+__device__ __forceinline__ void report_status(const WorldBuffers& B, int st) {
+  if (B.host_status) __hip_atomic_store(B.host_status, (uint32_t)st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Env modes of the wave-per-env kernel: same physics, different env layer.
 enum EnvMode : int { kFlock = 0, kTdm = 1 };
@@ -195,7 +214,9 @@ __device__ __forceinline__ float div_by_invariant(float n, float K) {
   const float rK = 1.0f / K;
   const float q0 = n * rK;
   const float q1 = __builtin_fmaf(__builtin_fmaf(-K, q0, n), rK, q0);
-  return __builtin_fmaf(__builtin_fmaf(-K, q1, n), rK, q1);
+  // the sign of the quotient is the sign of n (K > 0); copysign keeps it for n = -0, where the
+  // fma corrections would return +0 and n / K gives -0 (the sign can reach a zero position)
+  return __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-K, q1, n), rK, q1), n);
 #endif
 }
 

@@ -1,0 +1,653 @@
+// flock_spill.hpp — the spill step: one env's whole Flock env.step by one workgroup, with the
+// touching-contact working set in HBM, for envs whose contacts exceed the fast kernels' LDS
+// capacities (dense worlds: small start_spread, injected states).
+//
+// The fast kernels keep every per-contact array in LDS with fixed capacities: the wave kernel
+// (flock_step_w64.hip) 256 touching contacts and 16 per body, the workgroup kernel A
+// (flock_step_wg.hip) 5 x blockDim up to 4608. The reference (Box2D) has no such limits: any
+// start_spread is valid (gym_macm/settings.py:119-121,143-144 -> envs/mvmnt.py:62-63). When a
+// fast kernel finds, after Collide and before it has written any state, that an env's touching
+// contacts do not fit, the SAME workgroup calls spill::step_env for that env and returns: the
+// env is stepped from its untouched start-of-step state with the touching contacts, their CSR
+// edges, the island order and the island-ordered records in per-env HBM arrays sized by the
+// contact-list capacity C (touching contacts are a subset of the list, so nothing can overflow
+// except the list itself). Only the per-body arrays (positions, velocities, DFS state, pair
+// records) stay in LDS, about 40 B per body (+ 48 B with the pair records in LDS).
+//
+// The arithmetic and its order are those of the fast kernels (Box2D 2.3 order, see the header
+// of flock_step_w64.hip): Collide in list order, CSR edges in list (= Box2D edge) order, island
+// DFS seeded in reverse body order, Gauss-Seidel in island order, position passes with the early
+// exit, sleep, SynchronizeFixtures, new pairs prepended in descending (a, b) order, rewards,
+// observation. Results are bit-exact against the oracle like the fast kernels
+// (tests/test_gpu_dense.py forces every env through this path too).
+#pragma once
+
+#include "flock_common.hpp"
+
+namespace macm {
+namespace spill {
+
+constexpr int W = 64;
+
+struct __align__(16) Rec {  // per-agent pair-sweep record (48 B)
+  float4 fn;               // fat AABB after SynchronizeFixtures
+  float4 fo;               // fat AABB at the start of the step
+  float2 c;                // final position
+};
+
+__host__ __device__ constexpr int a16(int x) { return (x + 15) & ~15; }
+
+// LDS layout of the per-body arrays (host: size check; device: carve). 16-B aligned offsets.
+struct Layout {
+  int c, v, slp, deg, flags, oldc, off, todo, ib, ibod, stk, ic, isolv, scan, misc, recs, total;
+};
+
+__host__ __device__ constexpr Layout layout(int N, bool recs_in_lds) {
+  Layout L{};
+  int o = 0;
+  auto take = [&](int bytes) {
+    const int r = o;
+    o = a16(o + bytes);
+    return r;
+  };
+  L.c = take(8 * N);                   // float2 positions
+  L.v = take(8 * N);                   // float2 velocities
+  L.slp = take(4 * N);                 // sleep clocks
+  L.deg = take(4 * (N + 2));           // uint32 touching degree, then the CSR fill cursor
+  L.flags = take(N);                   // uint8 sleep-now
+  L.oldc = take(4 * ((N + 31) / 32));  // bitmask: agent in the old list (world.contacts before)
+  L.off = take(4 * (N + 1));           // uint32 CSR offsets
+  L.todo = take(8 * ((N + 63) / 64));  // bodies with edges not yet in an island
+  L.ib = take(2 * (N / 2 + 2));        // uint16 island body ranges
+  L.ibod = take(2 * N);                // uint16 island bodies
+  L.stk = take(2 * N);                 // uint16 DFS stack
+  L.ic = take(4 * (N / 2 + 2));        // uint32 island contact ranges
+  L.isolv = take(N / 2 + 2);           // uint8 island position-solved
+  L.scan = take(4 * 32);               // block scan scratch (<= 16 waves)
+  L.misc = take(4 * 8);                // nisl, status
+  L.recs = recs_in_lds ? take((int)sizeof(Rec) * N) : o;
+  L.total = o;
+  return L;
+}
+
+__device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }  // b2Min
+__device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }  // b2Max
+__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
+__device__ __forceinline__ bool overlap(float4 a, float4 b) {  // b2TestOverlap
+  const float d1x = b.x - a.z, d1y = b.y - a.w;
+  const float d2x = a.x - b.z, d2y = a.y - b.w;
+  if (d1x > 0.0f || d1y > 0.0f) return false;
+  if (d2x > 0.0f || d2y > 0.0f) return false;
+  return true;
+}
+__device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Normalize
+  const float len = sqrt_rn(x * x + y * y);
+  if (len < kEps) return;
+  const float inv = rcp_rn(len);
+  x *= inv;
+  y *= inv;
+}
+__device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
+__device__ __forceinline__ double wrap_pi(double t) { return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t; }
+
+// Exclusive scan over the block in thread order; returns the block total.
+__device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
+  const int tid = threadIdx.x, lane = tid & (W - 1), wid = tid / W, nw = blockDim.x / W;
+  int incl = v;
+  for (int d = 1; d < W; d <<= 1) {
+    const int o = __shfl_up(incl, d, W);
+    if (lane >= d) incl += o;
+  }
+  if (lane == W - 1) s_scan[wid] = incl;
+  __syncthreads();
+  int base = 0, total = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int s = s_scan[w];
+    if (w < wid) base += s;
+    total += s;
+  }
+  __syncthreads();
+  excl = base + incl - v;
+  return total;
+}
+
+template <typename OT>
+__device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float best, float rx, float ry, float tdx,
+                                          float tdy, float td2) {
+  const double t0 = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)ang);
+  const double t1 = wrap_pi(obs_atan2((double)tdy, (double)tdx) - (double)ang);
+  const double r0 = obs_sqrt<OT>(best), r1 = obs_sqrt<OT>(td2);
+  if (coord == MACM_COORD_CARTESIAN) {
+    o[0] = (OT)r0; o[1] = (OT)cos(t0); o[2] = (OT)sin(t0);
+    o[3] = (OT)r1; o[4] = (OT)cos(t1); o[5] = (OT)sin(t1);
+  } else {
+    o[0] = (OT)r0; o[1] = (OT)t0; o[2] = (OT)r1; o[3] = (OT)t1;
+  }
+}
+
+// One env.step of env e by the calling workgroup (blockDim.x = BS >= N, a multiple of 64; every
+// thread of the block must call it). `lds` holds layout(N, RECS_LDS).total bytes; the caller's
+// LDS contents are dead (a barrier on entry orders its last accesses). RECS_LDS = false keeps the
+// pair records in HBM (B.sp_rec) for callers whose LDS is smaller than 88 B per body.
+template <typename OT, bool RECS_LDS>
+__device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers& B, int e, int cur,
+                                         const void* __restrict__ actions, OT* __restrict__ obs,
+                                         int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
+                                         uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out,
+                                         unsigned char* lds) {
+  const int tid = threadIdx.x;
+  const int BS = blockDim.x;
+  const int N = P.n_agents;
+  const int C = P.max_contacts;
+  const bool act = tid < N;
+  const size_t ag = (size_t)e * N + tid;
+  const int nxt = cur ^ 1;
+  const Layout L = layout(N, RECS_LDS);
+  float2* s_c = (float2*)(lds + L.c);
+  float2* s_v = (float2*)(lds + L.v);
+  float* s_slp = (float*)(lds + L.slp);
+  uint32_t* s_deg = (uint32_t*)(lds + L.deg);
+  uint8_t* s_flag = (uint8_t*)(lds + L.flags);
+  uint32_t* s_oldc = (uint32_t*)(lds + L.oldc);
+  uint32_t* s_off = (uint32_t*)(lds + L.off);
+  unsigned long long* s_todo = (unsigned long long*)(lds + L.todo);
+  uint16_t* s_ib = (uint16_t*)(lds + L.ib);
+  uint16_t* s_ibod = (uint16_t*)(lds + L.ibod);
+  uint16_t* s_stk = (uint16_t*)(lds + L.stk);
+  uint32_t* s_ic = (uint32_t*)(lds + L.ic);
+  uint8_t* s_isolv = (uint8_t*)(lds + L.isolv);
+  int* s_scan = (int*)(lds + L.scan);
+  int* s_misc = (int*)(lds + L.misc);
+  Rec* recs;
+  if constexpr (RECS_LDS) recs = (Rec*)(lds + L.recs);
+  else recs = (Rec*)B.sp_rec + (size_t)e * N;
+  // per-env HBM working set, capacity C (touching contacts are a subset of the list)
+  uint32_t* g_tab = B.sp_tab + (size_t)e * C;
+  uint32_t* g_adj = B.sp_adj + (size_t)e * 2 * C;
+  uint32_t* g_ord = B.sp_ord + (size_t)e * C;
+  float4* g_cst = B.sp_cst + (size_t)e * C;
+  float2* g_cim = B.sp_cim + (size_t)e * C;
+  float2* g_lam = B.sp_lam + (size_t)e * C;
+  __syncthreads();  // the caller's last LDS accesses are done before the arrays are reused
+
+  // ---- loads ------------------------------------------------------------------------------
+  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
+  const float2* cimp = B.cimp[cur] + (size_t)e * C;
+  const int step_count = B.step_count[e];
+  const int M = B.ccount[cur][e];
+  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
+  float ang = 0.0f, slp = 0.0f;
+  float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  int a0 = 1, a1 = 1, a2 = 1;
+  float ax = 0.0f, ay = 0.0f;
+  if (act) {
+    p = B.pos[ag];
+    v = B.vel[ag];
+    ang = B.angle[ag];
+    fo = B.fat[ag];
+    slp = B.sleep[ag];
+    if (P.action_mode == MACM_ACTION_DISCRETE) {
+      const uint8_t* a = (const uint8_t*)actions + ag * 3;
+      a0 = a[0]; a1 = a[1]; a2 = a[2];
+    } else {
+      const float2 c = ((const float2*)actions)[ag];
+      ax = c.x; ay = c.y;
+    }
+    tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
+    s_c[tid] = p;
+  }
+  for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
+  for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0u;
+  if (tid < 8) s_misc[tid] = 0;
+
+  // ---- actions -> angle, force (mvmnt.py:97-129) -------------------------------------------
+  float Fx = 0.0f, Fy = 0.0f;
+  if (act) {
+    if (P.action_mode == MACM_ACTION_DISCRETE) {
+      float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
+      const double ad = (double)af;
+      if (fabs(ad) > M_PI) af = (float)(ad - sgn(ad) * (2.0 * M_PI));
+      ang = af;
+      const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
+      const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
+      double s0, c0, s1, c1;
+      act_trig(af, &s0, &c0, &s1, &c1);
+      Fx = (float)((c0 * k0 + c1 * k1) * cc * P.force);
+      Fy = (float)((s0 * k0 + s1 * k1) * cc * P.force);
+    } else {
+      float x = ax, y = ay;
+      if ((x * x + y * y) > 1.0f) {  // mvmnt.py:124-126 (the updated x, signs dropped)
+        x = sqrtf(x * x / (x * x + y * y));
+        y = sqrtf(y * y / (x * x + y * y));
+      }
+      Fx = x * P.force_f32;
+      Fy = y * P.force_f32;
+    }
+    Fx = 0.0f + Fx;  // m_force += force, from ClearForces' zero
+    Fy = 0.0f + Fy;
+  }
+  __syncthreads();
+
+  // ---- Collide: ordered compaction of the touching contacts (list order) ----------------------
+  const float rr = (P.radius + P.radius) * (P.radius + P.radius);
+  const float dt_ratio = step_count > 0 ? P.inv_dt * P.dt : 0.0f;  // m_inv_dt0 * dt
+  int T = 0;
+  for (int k0 = 0; k0 < M; k0 += BS) {
+    const int k = k0 + tid;
+    bool touch = false;
+    uint32_t ab = 0u;
+    float2 lam = make_float2(0.0f, 0.0f);
+    if (k < M) {
+      ab = cab[k];
+      lam = cimp[k];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      const float2 pa = s_c[a], pb = s_c[b];
+      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
+      touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+      atomicOr(&s_oldc[a >> 5], 1u << (a & 31));
+      atomicOr(&s_oldc[b >> 5], 1u << (b & 31));
+    }
+    int pos;
+    const int n = block_scan_excl(touch ? 1 : 0, pos, s_scan);
+    if (touch) {
+      g_tab[T + pos] = ab;
+      g_lam[T + pos] = P.warm_starting ? make_float2(dt_ratio * lam.x, dt_ratio * lam.y) : make_float2(0.0f, 0.0f);
+    }
+    T += n;
+  }
+  __syncthreads();
+
+  // ---- CSR touching edges, each body's segment in list (= Box2D edge) order -------------------
+  for (int t = tid; t < T; t += BS) {
+    const uint32_t ab = g_tab[t];
+    atomicAdd(&s_deg[ab & 0xffffu], 1u);
+    atomicAdd(&s_deg[ab >> 16], 1u);
+  }
+  __syncthreads();
+  const int deg = act ? (int)s_deg[tid] : 0;
+  {
+    int off;
+    block_scan_excl(deg, off, s_scan);
+    if (act) s_off[tid] = (uint32_t)off;
+    if (tid == 0) s_off[N] = (uint32_t)(2 * T);
+    const unsigned long long m = __ballot(act && deg > 0);  // DFS seeds / unvisited bodies
+    if ((tid & (W - 1)) == 0 && tid / W < (N + 63) / 64) s_todo[tid / W] = m;
+  }
+  __syncthreads();
+  if (act) s_deg[tid] = s_off[tid];  // fill cursor
+  __syncthreads();
+  for (int t = tid; t < T; t += BS) {
+    const uint32_t ab = g_tab[t];
+    g_adj[atomicAdd(&s_deg[ab & 0xffffu], 1u)] = (uint32_t)t;
+    g_adj[atomicAdd(&s_deg[ab >> 16], 1u)] = (uint32_t)t;
+  }
+  __syncthreads();
+  if (act && deg > 1) {  // insertion sort back into list order == Box2D edge order
+    const int o0 = (int)s_off[tid];
+    for (int x = o0 + 1; x < o0 + deg; ++x) {
+      const uint32_t key = g_adj[x];
+      int y = x - 1;
+      while (y >= o0 && g_adj[y] > key) {
+        g_adj[y + 1] = g_adj[y];
+        --y;
+      }
+      g_adj[y + 1] = key;
+    }
+  }
+  __syncthreads();
+
+  // ---- island DFS in Box2D order, serial on thread 0 ---------------------------------------------
+  // Seeds: bodies with touching edges, highest index first (reverse creation order). A body is
+  // visited once its s_todo bit is cleared; a contact once bit 31 of its g_tab entry is set
+  // (b < 32768). One thread does every global access of the walk, so program order orders them.
+  if (tid == 0) {
+    int nord = 0, nisl = 0, nb = 0;
+    for (int w = (N + 63) / 64 - 1; w >= 0;) {
+      const unsigned long long m = s_todo[w];
+      if (m == 0ull) {
+        --w;
+        continue;
+      }
+      const int s = w * 64 + 63 - __clzll(m);
+      s_todo[w] = m & ~(1ull << (s & 63));
+      s_ic[nisl] = (uint32_t)nord;
+      s_ib[nisl] = (uint16_t)nb;
+      int sp = 0;
+      s_stk[sp++] = (uint16_t)s;
+      while (sp > 0) {
+        const int b = s_stk[--sp];
+        s_ibod[nb++] = (uint16_t)b;
+        const int e0 = (int)s_off[b], e1 = (int)s_off[b + 1];
+        for (int q = e0; q < e1; ++q) {
+          const int t = (int)g_adj[q];
+          const uint32_t ab = g_tab[t];
+          if (ab & 0x80000000u) continue;
+          g_tab[t] = ab | 0x80000000u;
+          g_ord[nord++] = (uint32_t)t;
+          const int a = ab & 0xffffu, bb = ab >> 16;
+          const int o = (a == b) ? bb : a;
+          const unsigned long long ob = 1ull << (o & 63);
+          const unsigned long long tw = s_todo[o >> 6];
+          if (!(tw & ob)) continue;
+          s_todo[o >> 6] = tw & ~ob;
+          s_stk[sp++] = (uint16_t)o;
+        }
+      }
+      ++nisl;
+    }
+    s_ic[nisl] = (uint32_t)nord;
+    s_ib[nisl] = (uint16_t)nb;
+    s_misc[0] = nisl;
+  }
+  __syncthreads();
+  const int nisl = s_misc[0];
+  const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
+
+  // ---- integrate velocities + damping; island-ordered records with normals --------------------
+  if (act) {
+    const float vx = v.x + P.dt * (0.0f + P.inv_mass * Fx);  // gravityScale * gravity == 0
+    const float vy = v.y + P.dt * (0.0f + P.inv_mass * Fy);
+    s_v[tid] = make_float2(vx * P.damp, vy * P.damp);
+  }
+  for (int k = tid; k < nord; k += BS) {
+    const int t = (int)g_ord[k];
+    const uint32_t ab = g_tab[t] & 0x7fffffffu;
+    const int a = ab & 0xffffu, b = ab >> 16;
+    const float2 pa = s_c[a], pb = s_c[b];
+    float nx = 1.0f, ny = 0.0f;  // InitializeVelocityConstraints: (1, 0) when the centres coincide
+    const float ddx = pa.x - pb.x, ddy = pa.y - pb.y;
+    if (ddx * ddx + ddy * ddy > kEps * kEps) {
+      nx = pb.x - pa.x;
+      ny = pb.y - pa.y;
+      normalize(nx, ny);
+    }
+    g_cst[k] = make_float4(__uint_as_float(ab), nx, ny, 0.0f);
+    g_cim[k] = g_lam[t];
+  }
+  __syncthreads();
+
+  const float mA = P.inv_mass, mB = P.inv_mass;
+  const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;  // normalMass == tangentMass
+  const float friction = P.friction;
+
+  // ---- warm start + velocity iterations, one thread per island (b2ContactSolver) ---------------
+  for (int I = tid; I < nisl; I += BS) {
+    const int c0 = (int)s_ic[I], c1 = (int)s_ic[I + 1];
+    if (P.warm_starting) {
+      for (int k = c0; k < c1; ++k) {
+        const float4 r = g_cst[k];
+        const float2 im = g_cim[k];
+        const uint32_t ab = __float_as_uint(r.x);
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const float nx = r.y, ny = r.z, tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
+        const float Px = im.x * nx + im.y * tx, Py = im.x * ny + im.y * ty;
+        float2 va = s_v[a], vb = s_v[b];
+        va.x = va.x - mA * Px;
+        va.y = va.y - mA * Py;
+        vb.x = vb.x + mB * Px;
+        vb.y = vb.y + mB * Py;
+        s_v[a] = va;
+        s_v[b] = vb;
+      }
+    }
+    for (int it = 0; it < P.vel_iters; ++it) {
+      for (int k = c0; k < c1; ++k) {
+        const float4 r = g_cst[k];
+        float2 im = g_cim[k];
+        const uint32_t ab = __float_as_uint(r.x);
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const float nx = r.y, ny = r.z, tx = ny, ty = -nx;
+        float2 va = s_v[a], vb = s_v[b];
+        {  // tangent first
+          const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+          const float vt = dvx * tx + dvy * ty;
+          float lambda = kmass * (-vt);
+          const float maxf = friction * im.x;
+          const float ni = sclamp(im.y + lambda, -maxf, maxf);
+          lambda = ni - im.y;
+          im.y = ni;
+          const float Px = lambda * tx, Py = lambda * ty;
+          va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+          vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+        }
+        {  // normal (velocityBias == 0: restitution 0)
+          const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+          const float vn = dvx * nx + dvy * ny;
+          float lambda = -kmass * (vn - 0.0f);
+          const float ni = fmaxf(im.x + lambda, 0.0f);
+          lambda = ni - im.x;
+          im.x = ni;
+          const float Px = lambda * nx, Py = lambda * ny;
+          va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+          vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+        }
+        s_v[a] = va;
+        s_v[b] = vb;
+        g_cim[k] = im;
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < nord; k += BS) g_lam[g_ord[k]] = g_cim[k];  // StoreImpulses, list order
+
+  // ---- integrate positions ----------------------------------------------------------------------
+  float cx = p.x, cy = p.y, vx = 0.0f, vy = 0.0f;
+  if (act) {
+    const float2 vv = s_v[tid];
+    vx = vv.x;
+    vy = vv.y;
+    const float tx = P.dt * vx, ty = P.dt * vy;
+    if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
+      const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
+      vx = vx * ratio;
+      vy = vy * ratio;
+    }
+    cx = cx + P.dt * vx;
+    cy = cy + P.dt * vy;
+    s_c[tid] = make_float2(cx, cy);
+  }
+  __syncthreads();
+
+  // ---- position iterations, one thread per island (early exit at -3 linearSlop) ---------------------
+  for (int I = tid; I < nisl; I += BS) {
+    const int c0 = (int)s_ic[I], c1 = (int)s_ic[I + 1];
+    int solved = 0;
+    for (int it = 0; it < P.pos_iters; ++it) {
+      float min_sep = 0.0f;
+      for (int k = c0; k < c1; ++k) {
+        const uint32_t ab = __float_as_uint(g_cst[k].x);
+        const int a = ab & 0xffffu, b = ab >> 16;
+        float2 ca = s_c[a], cb = s_c[b];
+        float nx = cb.x - ca.x, ny = cb.y - ca.y;
+        normalize(nx, ny);
+        const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - P.radius - P.radius;
+        min_sep = bmin(min_sep, sep);
+        const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+        const float K = mA + mB;
+        const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
+        const float Px = imp * nx, Py = imp * ny;
+        ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
+        cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
+        s_c[a] = ca;
+        s_c[b] = cb;
+      }
+      if (min_sep >= -3.0f * kLinearSlop) {
+        solved = 1;
+        break;
+      }
+    }
+    s_isolv[I] = (uint8_t)solved;
+  }
+
+  // ---- sleep clock + island sleep decision (b2Island::Solve) --------------------------------------
+  float ns = 0.0f;
+  if (act) {
+    const bool moving = vx * vx + vy * vy > kLinearSleepTol * kLinearSleepTol;
+    ns = moving ? 0.0f : slp + P.dt;
+    s_slp[tid] = ns;
+    s_flag[tid] = (deg == 0 && ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
+  }
+  __syncthreads();
+  for (int I = tid; I < nisl; I += BS) {
+    const int b0 = s_ib[I], b1 = s_ib[I + 1];
+    float mn = 3.402823466e+38f;
+    for (int k = b0; k < b1; ++k) mn = bmin(mn, s_slp[s_ibod[k]]);
+    const uint8_t sl = (mn >= kTimeToSleep && s_isolv[I]) ? 1 : 0;
+    for (int k = b0; k < b1; ++k) s_flag[s_ibod[k]] = sl;
+  }
+  __syncthreads();
+
+  // ---- SynchronizeFixtures: fat-AABB hysteresis ------------------------------------------------------
+  float4 fn = fo;
+  if (act) {
+    const float2 cc = s_c[tid];
+    cx = cc.x;
+    cy = cc.y;
+    const float r = P.radius;
+    const float c0x = p.x, c0y = p.y;
+    const float lox = bmin(c0x - r, cx - r), loy = bmin(c0y - r, cy - r);
+    const float hix = bmax(c0x + r, cx + r), hiy = bmax(c0y + r, cy + r);
+    const bool contains = fo.x <= lox && fo.y <= loy && hix <= fo.z && hiy <= fo.w;
+    if (!contains) {
+      fn = make_float4(lox - kAabbExtension, loy - kAabbExtension, hix + kAabbExtension, hiy + kAabbExtension);
+      const float dx = kAabbMultiplier * (cx - c0x), dy = kAabbMultiplier * (cy - c0y);
+      if (dx < 0.0f) fn.x += dx; else fn.z += dx;
+      if (dy < 0.0f) fn.y += dy; else fn.w += dy;
+    }
+    if (s_flag[tid]) {
+      vx = 0.0f;
+      vy = 0.0f;
+      ns = 0.0f;
+    }
+    Rec r0;
+    r0.fn = fn;
+    r0.fo = fo;
+    r0.c = make_float2(cx, cy);
+    recs[tid] = r0;
+  }
+  __syncthreads();
+
+  // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour (mvmnt.py:185-196) ------------
+  //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t); new contacts = Ov(F_t) \ Ov(F_{t-1})
+  bool coll = act && ((s_oldc[tid >> 5] >> (tid & 31)) & 1u);
+  int newcnt = 0;
+  float best = __builtin_inff();
+  int bj = tid == 0 ? 1 : 0;
+  if (act) {
+    for (int j = 0; j < N; ++j) {
+      const Rec r = recs[j];
+      const bool ovn = overlap(fn, r.fn);
+      const float dx = r.c.x - cx, dy = r.c.y - cy;
+      const float d2 = dx * dx + dy * dy;  // b2DistanceSquared(other, agent)
+      const bool other = j != tid;
+      coll |= other && ovn;
+      if (other && d2 < best) {  // strict '<': the lowest index wins ties (mvmnt.py:194)
+        best = d2;
+        bj = j;
+      }
+      if (j > tid && ovn && !overlap(fo, r.fo)) ++newcnt;
+    }
+  }
+  // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs -------------------------
+  uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
+  float2* ocimp = B.cimp[nxt] + (size_t)e * C;
+  int excl;
+  const int nnew = block_scan_excl(newcnt, excl, s_scan);
+  if (act && newcnt > 0) {
+    int w = nnew - excl - newcnt;  // agents > tid come first
+    for (int j = N - 1; j > tid; --j) {
+      const Rec r = recs[j];
+      if (overlap(fn, r.fn) && !overlap(fo, r.fo)) {
+        if (w < C) {
+          ocab[w] = (uint32_t)tid | ((uint32_t)j << 16);
+          ocimp[w] = make_float2(0.0f, 0.0f);
+        }
+        ++w;
+      }
+    }
+  }
+  int kept = 0, Tr = 0;
+  for (int k0 = 0; k0 < M; k0 += BS) {
+    const int k = k0 + tid;
+    bool keep = false, touch = false;
+    uint32_t ab = 0u;
+    if (k < M) {
+      ab = cab[k];
+      const int a = ab & 0xffffu, b = ab >> 16;
+      keep = overlap(recs[a].fn, recs[b].fn);
+      // touching at Collide, from the start-of-step positions (the state is not yet written back)
+      const float2 pa = B.pos[(size_t)e * N + a], pb = B.pos[(size_t)e * N + b];
+      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
+      touch = !(dx * dx + dy * dy > rr);
+    }
+    int tpos, kpos;
+    const int tn = block_scan_excl(touch ? 1 : 0, tpos, s_scan);
+    const int kn = block_scan_excl(keep ? 1 : 0, kpos, s_scan);
+    if (keep) {
+      const int w = nnew + kept + kpos;
+      if (w < C) {
+        ocab[w] = ab;
+        ocimp[w] = touch ? g_lam[Tr + tpos] : make_float2(0.0f, 0.0f);
+      }
+    }
+    Tr += tn;
+    kept += kn;
+  }
+  int status = 0;
+  int total = nnew + kept;
+  if (total > C) {
+    status |= MACM_ST_CONTACT_OVERFLOW;
+    total = C;
+  }
+
+  // ---- rewards (mvmnt.py:160-179) + obs (mvmnt.py:181-222) -------------------------------------------
+  float rew = 0.0f;
+  if (act) {
+    const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
+    const float td2 = tdx * tdx + tdy * tdy;
+    const double d = sqrt((double)td2);
+    if (coll) rew = -1.0f;
+    else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
+    else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
+    rew_out[ag] = rew;
+    if (coll_out) coll_out[ag] = coll ? 1 : 0;
+    if (nbr_out) nbr_out[ag] = bj;
+    if (obs) {
+      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+      const float2 cb = recs[bj].c;
+      write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
+    }
+  }
+  int dummy;
+  const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
+  const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
+  if (act) {
+    B.pos[ag] = make_float2(cx, cy);
+    B.vel[ag] = make_float2(vx, vy);
+    B.angle[ag] = ang;
+    B.fat[ag] = fn;
+    B.sleep[ag] = ns;
+  }
+  if (tid == 0) {
+    const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz (mvmnt.py:134-136)
+    const uint8_t dn = tp > P.time_limit ? 1 : 0;
+    B.time_passed[e] = tp;
+    B.done[e] = dn;
+    if (done_out) done_out[e] = dn;
+    B.step_count[e] = step_count + 1;
+    B.ccount[nxt][e] = total;
+    if (status) {
+      B.status[e] |= status;
+      report_status(B, status);
+    }
+    unsigned long long* ec = B.env_counters + (size_t)e * 4;
+    ec[0] += (unsigned long long)N;
+    ec[1] += (unsigned long long)ncoll;
+    ec[2] += (unsigned long long)npos;
+    ec[3] += (unsigned long long)dn;
+    if (B.spill_count) B.spill_count[e] += 1u;
+  }
+}
+
+}  // namespace spill
+}  // namespace macm

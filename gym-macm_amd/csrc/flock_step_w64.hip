@@ -42,6 +42,7 @@
 //     velocity/impulse component, never a nonzero value or any position.
 //   * circles sit at the body origin, so b2Mul(xf, m_p) == position exactly.
 #include "flock_common.hpp"
+#include "flock_spill.hpp"
 
 namespace macm {
 
@@ -572,15 +573,32 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
 
   __shared__ float2 s_c[W];  // positions (one 8-byte access per body)
   __shared__ float2 s_v[W];  // velocities (one ds_read_b64 / ds_write_b64 per body)
-  __shared__ uint32_t s_tab[TCAP];
-  __shared__ float s_tln[TCAP], s_tlt[TCAP];
-  // contact normals live until the velocity solve ends; the all-pairs records are
-  // written after it, so both share one LDS region
-  __shared__ __align__(32) float s_tn[2 * TCAP];
+  // per agent: bit mask of its touching contacts for the scalar DFS (T <= 64 TMW); TDM keeps one
+  // 64-bit word (its LDS budget is full), Flock two
+  constexpr int TMW = kT ? 1 : 2;
+  // The contact arrays in one block, which the spill step (flock_spill.hpp) reuses as its
+  // per-body LDS when an env's touching contacts overflow TCAP / DEG.
+  struct __align__(32) Pool {
+    // contact normals live until the velocity solve ends; the all-pairs records are
+    // written after it, so both share one LDS region
+    float tn[2 * TCAP];
+    uint32_t tab[TCAP];
+    float tln[TCAP], tlt[TCAP];
+    uint32_t tm[2 * TMW * W];
+    uint32_t oldm[2 * W];  // per agent: 64-bit mask of partners in the old list
+  };
+  __shared__ Pool s_pool;
+  static_assert(kT || spill::layout(W, true).total <= (int)sizeof(Pool), "the spill step must fit the pool");
+  uint32_t* const s_tab = s_pool.tab;
+  float* const s_tln = s_pool.tln;
+  float* const s_tlt = s_pool.tlt;
+  float* const s_tn = s_pool.tn;
   float* const s_tnx = s_tn;
   float* const s_tny = s_tn + TCAP;
   PairRec* const s_pj = reinterpret_cast<PairRec*>(s_tn);
   static_assert(sizeof(PairRec) * W <= sizeof(float) * 2 * TCAP, "s_pj must fit in s_tn");
+  uint32_t* const s_tm = s_pool.tm;
+  uint32_t* const s_oldm = s_pool.oldm;
   __shared__ uint8_t s_adj[W * DEG];
   __shared__ uint8_t s_ord[TCAP];
   __shared__ uint32_t s_cvis[TCAP / 32];
@@ -589,11 +607,6 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   __shared__ uint8_t s_ib[ICAP + 1];
   __shared__ uint8_t s_isolved[ICAP];
   __shared__ uint32_t s_imin[ICAP];  // per island: min sleep time (float bits, all >= 0)
-  __shared__ uint32_t s_oldm[2 * W];  // per agent: 64-bit mask of partners in the old list
-  // per agent: bit mask of its touching contacts for the scalar DFS (T <= 64 TMW); TDM keeps one
-  // 64-bit word (its LDS budget is full), Flock two
-  constexpr int TMW = kT ? 1 : 2;
-  __shared__ uint32_t s_tm[2 * TMW * W];
   __shared__ int s_nisl;
   // TDM only (unreferenced, hence not allocated, in the Flock instantiation)
   __shared__ double s_hpd[W];
@@ -857,7 +870,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     }
     T += __popcll(m);
   }
-  if (T > TCAP) {
+  const bool touch_over = T > TCAP;
+  if (touch_over) {
     status |= MACM_ST_TOUCH_OVERFLOW;
     T = TCAP;
   }
@@ -886,7 +900,20 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       }
     }
   }
-  if (deg > DEG) {
+  if constexpr (!kT) {
+    // More touching contacts than TCAP, or a body with more than DEG: the env is stepped by the
+    // spill step instead (HBM working set, flock_spill.hpp). Nothing has been written to global
+    // memory yet, so it starts from the untouched start-of-step state; this wave returns after it.
+    // (The scalar DFS of T <= 64 TMW has no degree cap: it walks bit masks.)
+#ifndef MACM_AB_NO_SPILL  // A/B knob: the fast path alone (dense envs then overflow)
+    if (touch_over || (!fast_dfs && __builtin_amdgcn_ballot_w64(deg > DEG) != 0ull) || P.force_spill) {
+      spill::step_env<OT, true>(P, B, e, cur, actions, obs, nbr_out, rew_out, coll_out, done_out,
+                                reinterpret_cast<unsigned char*>(&s_pool));
+      return;
+    }
+#endif
+  }
+  if (!fast_dfs && deg > DEG) {
     status |= MACM_ST_DEGREE_OVERFLOW;
     deg = DEG;
   }
@@ -1499,7 +1526,10 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     B.step_count[e] = step_count + 1;
     B.ccount[nxt][e] = total;
     const int st = (mst1 ? 1 : 0) | (mst2 ? 2 : 0) | (mst4 ? 4 : 0);
-    if (st) B.status[e] = st_prev | st;
+    if (st) {
+      B.status[e] = st_prev | st;
+      report_status(B, st);
+    }
     const unsigned long long c0 = kT ? (unsigned long long)__popcll(alive0_m) : (unsigned long long)N;
     ulonglong2* ec = reinterpret_cast<ulonglong2*>(B.env_counters + (size_t)e * 4);
     ec[0] = make_ulonglong2(ctr[0] + c0, ctr[1] + c1);
@@ -1590,6 +1620,7 @@ __global__ __launch_bounds__(W) void flock_init_w64(StepParams P, WorldBuffers B
     B.time_passed[e] = 0.0;
     B.done[e] = 0;
     B.status[e] = st;
+    if (st) report_status(B, st);
   }
 }
 
@@ -1687,6 +1718,7 @@ __global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, 
     B.time_passed[e] = 0.0;
     B.done[e] = 0;
     B.status[e] = st;
+    if (st) report_status(B, st);
     TB.listener[e] = make_int2(0, -1);
     TB.winner[e] = -1;
     if (TB.winner_out) TB.winner_out[e] = -1;

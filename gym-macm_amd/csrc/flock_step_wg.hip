@@ -13,9 +13,11 @@
 //   * all-pairs sweep over per-agent records in LDS (broadcast reads); new
 //     contacts = Ov(F_t) \ Ov(F_{t-1}) by testing the old fat AABBs, counted per
 //     agent then written in descending (a, b) order after a descending scan.
-// LDS is dynamic and laid out by wg_layout() with lifetime aliasing (adjacency,
-// DFS scratch and contact normals die before the pair records are written).
+// The step is split in three launches (kernels A, B, C below). An env whose touching
+// contacts exceed kernel A's LDS capacity is stepped whole by the spill step
+// (flock_spill.hpp) inside kernel A, and B and C skip it.
 #include "flock_common.hpp"
+#include "flock_spill.hpp"
 
 namespace macm {
 namespace wg {
@@ -83,64 +85,6 @@ struct __align__(16) Rec {  // per-agent record for the pair sweep (48 B with fl
   float2 c;                // final position
 };
 
-struct Contact {  // touching contact in island order (20 B)
-  uint32_t ab;
-  float ln, lt;
-  float nx, ny;
-};
-
-}  // namespace wg
-
-// LDS layout, shared by host (size) and device (carve). All offsets 16-B aligned.
-// Lifetimes: [tab, adj] live Collide..record build; the island-ordered contact
-// records replace them until the position solve ends; the pair-sweep records
-// replace those. List-order impulses live in a per-env global scratch (B.scratch).
-struct WgLayout {
-  int c, v, slp, deg, flags, oldc, csr_off, todo, ord, ib, ibod, stk, ic, isolv, scan, misc, region, tab, adj,
-      cont, recs, total;
-};
-
-__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
-
-__host__ __device__ inline WgLayout wg_layout(int N, int tcap) {
-  WgLayout L;
-  int o = 0;
-  auto take = [&](int bytes) {
-    int r = o;
-    o = align16(o + bytes);
-    return r;
-  };
-  L.c = take(8 * N);                   // float2 positions (working copy)
-  L.v = take(8 * N);                   // float2 velocities
-  L.slp = take(4 * N);                 // sleep clocks
-  L.deg = take(2 * (N + 2));           // uint16 touching degree, then CSR cursor
-  L.flags = take(N);                   // uint8 sleep-now
-  L.oldc = take(4 * ((N + 31) / 32));  // bitmask: agent appears in the old list
-  L.csr_off = take(2 * (N + 1));       // uint16 CSR offsets
-  L.todo = take(8 * ((N + 63) / 64));  // bodies with edges not yet in an island (DFS)
-  L.ord = take(2 * tcap);              // uint16 island-ordered touching indices
-  L.ib = take(2 * (N / 2 + 2));        // uint16 island body ranges
-  L.ibod = take(2 * N);                // uint16 island bodies
-  L.stk = take(2 * N);                 // uint16 DFS stack
-  L.ic = take(2 * (N / 2 + 2));        // uint16 island contact ranges
-  L.isolv = take(N / 2 + 2);           // uint8 island position-solved
-  L.scan = take(4 * 32);               // block scan scratch (<= 16 waves)
-  L.misc = take(4 * 8);                // nisl, status
-  L.region = o;
-  const int part1 = align16(4 * tcap) + align16(2 * 2 * tcap);  // tab + adj
-  const int part2 = align16(20 * tcap);                         // contacts (20 B)
-  const int part3 = align16((int)sizeof(wg::Rec) * N);          // pair records
-  L.tab = L.region;
-  L.adj = L.region + align16(4 * tcap);
-  L.cont = L.region;
-  L.recs = L.region;
-  int rs = part1 > part2 ? part1 : part2;
-  rs = rs > part3 ? rs : part3;
-  L.total = align16(L.region + rs);
-  return L;
-}
-
-namespace wg {
 
 // Exclusive scan over the block in thread order; returns the block total.
 __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
@@ -179,642 +123,7 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 
 }  // namespace wg
 
-template <typename OT>
-__global__ __launch_bounds__(1024) void flock_step_wg(StepParams P, WorldBuffers B, int cur, int tcap,
-                                                      const void* __restrict__ actions, OT* __restrict__ obs,
-                                                      int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
-                                                      uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out) {
-  using namespace wg;
-  extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int BS = blockDim.x;
-  const int N = P.n_agents;
-  const int C = P.max_contacts;
-  const bool act = tid < N;
-  const size_t ag = (size_t)e * N + tid;
-  const int nxt = cur ^ 1;
-  const WgLayout L = wg_layout(N, tcap);
-  float2* s_c = (float2*)(lds + L.c);
-  float2* s_v = (float2*)(lds + L.v);
-  float* s_slp = (float*)(lds + L.slp);
-  uint16_t* s_deg = (uint16_t*)(lds + L.deg);
-  uint8_t* s_flag = (uint8_t*)(lds + L.flags);
-  uint32_t* s_oldc = (uint32_t*)(lds + L.oldc);
-  uint16_t* s_off = (uint16_t*)(lds + L.csr_off);
-  unsigned long long* s_todo = (unsigned long long*)(lds + L.todo);
-  uint16_t* s_ord = (uint16_t*)(lds + L.ord);
-  uint16_t* s_ib = (uint16_t*)(lds + L.ib);
-  uint16_t* s_ibod = (uint16_t*)(lds + L.ibod);
-  uint16_t* s_stk = (uint16_t*)(lds + L.stk);
-  uint16_t* s_ic = (uint16_t*)(lds + L.ic);
-  uint8_t* s_isolv = (uint8_t*)(lds + L.isolv);
-  int* s_scan = (int*)(lds + L.scan);
-  int* s_misc = (int*)(lds + L.misc);
-  uint32_t* s_tab = (uint32_t*)(lds + L.tab);   // region, part 1
-  uint16_t* s_adj = (uint16_t*)(lds + L.adj);   // region, part 1
-  Contact* s_ct = (Contact*)(lds + L.cont);     // region, part 2
-  Rec* s_rec = (Rec*)(lds + L.recs);            // region, part 3
-  float2* g_lam = B.scratch + (size_t)e * tcap;  // list-order impulses of touching contacts
-
-  // ---- loads ------------------------------------------------------------------
-  const uint32_t* cab = B.cab[cur] + (size_t)e * C;
-  const float2* cimp = B.cimp[cur] + (size_t)e * C;
-  const int step_count = B.step_count[e];
-  const int M = B.ccount[cur][e];
-  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
-  float ang = 0.0f, slp = 0.0f;
-  float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  int a0 = 1, a1 = 1, a2 = 1;
-  float ax = 0.0f, ay = 0.0f;
-  if (act) {
-    p = B.pos[ag];
-    v = B.vel[ag];
-    ang = B.angle[ag];
-    fo = B.fat[ag];
-    slp = B.sleep[ag];
-    if (P.action_mode == MACM_ACTION_DISCRETE) {
-      const uint8_t* a = (const uint8_t*)actions + ag * 3;
-      a0 = a[0]; a1 = a[1]; a2 = a[2];
-    } else {
-      const float2 c = ((const float2*)actions)[ag];
-      ax = c.x; ay = c.y;
-    }
-    tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
-    s_c[tid] = p;
-  }
-  for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
-  for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0;
-  if (tid < 8) s_misc[tid] = 0;
-  int status = 0;
-  WSTAMP(0);
-
-  // ---- actions -> angle, force (mvmnt.py:97-129) ---------------------------------
-  float Fx = 0.0f, Fy = 0.0f;
-  if (act) {
-    if (P.action_mode == MACM_ACTION_DISCRETE) {
-      float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
-      double ad = (double)af;
-      if (fabs(ad) > M_PI) {
-        af = (float)(ad - sgn(ad) * (2.0 * M_PI));
-        ad = (double)af;
-      }
-      ang = af;
-      const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
-      const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
-      double s0, c0, s1, c1;
-      act_trig(af, &s0, &c0, &s1, &c1);
-      Fx = (float)((c0 * k0 + c1 * k1) * cc * P.force);
-      Fy = (float)((s0 * k0 + s1 * k1) * cc * P.force);
-    } else {
-      float x = ax, y = ay;
-      if ((x * x + y * y) > 1.0f) {
-        x = sqrtf(x * x / (x * x + y * y));
-        y = sqrtf(y * y / (x * x + y * y));
-      }
-      Fx = x * P.force_f32;
-      Fy = y * P.force_f32;
-    }
-    Fx = 0.0f + Fx;
-    Fy = 0.0f + Fy;
-  }
-  __syncthreads();
-  WSTAMP(1);
-
-  // ---- Collide: ordered compaction of the touching contacts -----------------------
-  const float rr = (P.radius + P.radius) * (P.radius + P.radius);
-  const float dt_ratio = step_count > 0 ? P.inv_dt * P.dt : 0.0f;
-  int T = 0;
-  for (int k0 = 0; k0 < M; k0 += BS) {
-    const int k = k0 + tid;
-    bool touch = false;
-    uint32_t ab = 0u;
-    float2 lam = make_float2(0.0f, 0.0f);
-    if (k < M) {
-      ab = cab[k];
-      lam = cimp[k];
-      const int a = ab & 0xffffu, b = ab >> 16;
-      const float2 pa = s_c[a], pb = s_c[b];
-      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
-      touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
-      atomicOr(&s_oldc[a >> 5], 1u << (a & 31));
-      atomicOr(&s_oldc[b >> 5], 1u << (b & 31));
-    }
-    int pos;
-    const int n = block_scan_excl(touch ? 1 : 0, pos, s_scan);
-    if (touch && T + pos < tcap) {
-      s_tab[T + pos] = ab;
-      g_lam[T + pos] = P.warm_starting ? make_float2(dt_ratio * lam.x, dt_ratio * lam.y) : make_float2(0.0f, 0.0f);
-    }
-    T += n;
-  }
-  if (T > tcap) {
-    status |= MACM_ST_TOUCH_OVERFLOW;
-    T = tcap;
-  }
-  __syncthreads();
-  WSTAMP(2);
-
-  // ---- CSR touching edges, each body's segment in list (= Box2D edge) order ---------
-  // 16-bit counters packed in 32-bit LDS words
-#define DEG_WORD(i) ((unsigned int*)(s_deg + ((i) & ~1)))
-#define DEG_INC(i) (((i) & 1) ? 0x10000u : 1u)
-#define DEG_GET(w, i) (((i) & 1) ? ((w) >> 16) : ((w) & 0xffffu))
-  for (int t = tid; t < T; t += BS) {
-    const uint32_t ab = s_tab[t];
-    const int a = ab & 0xffffu, b = ab >> 16;
-    atomicAdd(DEG_WORD(a), DEG_INC(a));
-    atomicAdd(DEG_WORD(b), DEG_INC(b));
-  }
-  __syncthreads();
-  const int deg = act ? (int)s_deg[tid] : 0;
-  {
-    int off;
-    block_scan_excl(deg, off, s_scan);
-    if (act) s_off[tid] = (uint16_t)off;
-    if (tid == 0) s_off[N] = (uint16_t)(2 * T);
-    // bodies with touching edges, as a bitmask (DFS seeds / visited marks)
-    const unsigned long long m = __ballot(act && deg > 0);
-    if ((tid & (W - 1)) == 0 && tid / W < (N + 63) / 64) s_todo[tid / W] = m;
-  }
-  __syncthreads();
-  if (act) s_deg[tid] = s_off[tid];  // fill cursor
-  __syncthreads();
-  for (int t = tid; t < T; t += BS) {
-    const uint32_t ab = s_tab[t];
-    const int a = ab & 0xffffu, b = ab >> 16;
-    const unsigned wa = atomicAdd(DEG_WORD(a), DEG_INC(a));
-    const unsigned wb = atomicAdd(DEG_WORD(b), DEG_INC(b));
-    s_adj[DEG_GET(wa, a)] = (uint16_t)t;
-    s_adj[DEG_GET(wb, b)] = (uint16_t)t;
-  }
-#undef DEG_WORD
-#undef DEG_INC
-#undef DEG_GET
-  __syncthreads();
-  if (act && deg > 1) {  // insertion sort: list order == Box2D edge order
-    const int o0 = s_off[tid];
-    for (int x = o0 + 1; x < o0 + deg; ++x) {
-      const uint16_t key = s_adj[x];
-      int y = x - 1;
-      while (y >= o0 && s_adj[y] > key) {
-        s_adj[y + 1] = s_adj[y];
-        --y;
-      }
-      s_adj[y + 1] = key;
-    }
-  }
-  __syncthreads();
-  WSTAMP(3);
-
-  // ---- island DFS in Box2D order ------------------------------------------------------
-  const bool par_dfs = 2 * T >= 4 * N;
-  // ---- island DFS in Box2D order, serial on thread 0 ----------------------------------
-  // Seeds: bodies with touching edges, highest index first (reverse creation order).
-  // A body is "visited" once its s_todo bit is cleared; a contact once bit 31 of its
-  // s_tab entry is set (b < 32768, so the bit is free).
-  if (!par_dfs && tid == 0) {
-    int nord = 0, nisl = 0, nb = 0;
-    for (int w = (N + 63) / 64 - 1; w >= 0;) {
-      const unsigned long long m = s_todo[w];
-      if (m == 0ull) {
-        --w;
-        continue;
-      }
-      const int s = w * 64 + 63 - __clzll(m);
-      s_todo[w] = m & ~(1ull << (s & 63));
-      s_ic[nisl] = (uint16_t)nord;
-      s_ib[nisl] = (uint16_t)nb;
-      int sp = 0;
-      s_stk[sp++] = (uint16_t)s;
-      while (sp > 0) {
-        const int b = s_stk[--sp];
-        s_ibod[nb++] = (uint16_t)b;
-        const int e0 = s_off[b], e1 = s_off[b + 1];
-        for (int q = e0; q < e1; ++q) {
-          const int t = s_adj[q];
-          const uint32_t ab = s_tab[t];
-          if (ab & 0x80000000u) continue;
-          s_tab[t] = ab | 0x80000000u;
-          s_ord[nord++] = (uint16_t)t;
-          const int a = ab & 0xffffu, bb = ab >> 16;
-          const int o = (a == b) ? bb : a;
-          const unsigned long long ob = 1ull << (o & 63);
-          const unsigned long long tw = s_todo[o >> 6];
-          if (!(tw & ob)) continue;
-          s_todo[o >> 6] = tw & ~ob;
-          s_stk[sp++] = (uint16_t)o;
-        }
-      }
-      ++nisl;
-    }
-    s_ic[nisl] = (uint16_t)nord;
-    s_ib[nisl] = (uint16_t)nb;
-    s_misc[0] = nisl;
-  }
-  // Dense worlds (average touching degree >= 4): the DFS on wave 0.
-  // Seeds: bodies with touching edges, highest index first (reverse creation order).
-  // A body is "visited" once its s_todo bit is cleared; a contact once bit 31 of its
-  // s_tab entry is set (b < 32768, so the bit is free). The edges of a popped body
-  // are taken together, one lane per edge: within one body's edge loop Box2D's
-  // decisions are independent (every edge has its own contact and its own other
-  // body), so ballot ranks in edge order reproduce its appends and pushes exactly.
-  if (par_dfs && tid < W) {
-    const int lane = tid;
-    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    int nord = 0, nisl = 0, nb = 0;
-    for (int w = (N + 63) / 64 - 1; w >= 0;) {
-      const unsigned long long m = s_todo[w];
-      if (m == 0ull) {
-        --w;
-        continue;
-      }
-      const int sd = w * 64 + 63 - __clzll(m);
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        s_todo[w] = m & ~(1ull << (sd & 63));
-        s_ic[nisl] = (uint16_t)nord;
-        s_ib[nisl] = (uint16_t)nb;
-        s_stk[0] = (uint16_t)sd;
-      }
-      int sp = 1;
-      __builtin_amdgcn_wave_barrier();
-      while (sp > 0) {
-        const int bdy = s_stk[--sp];
-        if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
-        ++nb;
-        const int e0 = s_off[bdy], e1 = s_off[bdy + 1];
-        for (int q0 = e0; q0 < e1; q0 += W) {
-          const int q = q0 + lane;
-          bool newc = false, push = false;
-          int t = 0, o = 0;
-          uint32_t ab = 0u;
-          if (q < e1) {
-            t = s_adj[q];
-            ab = s_tab[t];
-            newc = !(ab & 0x80000000u);
-          }
-          const unsigned long long mc = __ballot(newc);
-          if (newc) {
-            s_tab[t] = ab | 0x80000000u;
-            s_ord[nord + __popcll(mc & lt)] = (uint16_t)t;
-            const int a = ab & 0xffffu, bb = ab >> 16;
-            o = (a == bdy) ? bb : a;
-            push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
-          }
-          nord += __popcll(mc);
-          const unsigned long long mp = __ballot(push);
-          if (push) {
-            atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
-            s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
-          }
-          sp += __popcll(mp);
-          __builtin_amdgcn_wave_barrier();  // stack / marks visible before the next read
-        }
-      }
-      ++nisl;
-    }
-    if (lane == 0) {
-      s_ic[nisl] = (uint16_t)nord;
-      s_ib[nisl] = (uint16_t)nb;
-      s_misc[0] = nisl;
-    }
-  }
-  __syncthreads();
-  WSTAMP(4);
-  const int nisl = s_misc[0];
-  const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
-
-  // ---- integrate velocities; island-ordered contact records with normals -------------
-  if (act) {
-    const float vx = v.x + P.dt * (0.0f + P.inv_mass * Fx);
-    const float vy = v.y + P.dt * (0.0f + P.inv_mass * Fy);
-    s_v[tid] = make_float2(vx * P.damp, vy * P.damp);
-  }
-  constexpr int KREG = 5;  // records staged per thread (tcap <= KREG * blockDim)
-  Contact stage[KREG];
-#pragma unroll
-  for (int r = 0; r < KREG; ++r) {
-    const int k = tid + r * BS;
-    if (k < nord) {
-      const int t = s_ord[k];
-      const uint32_t ab = s_tab[t] & 0x7fffffffu;
-      const int a = ab & 0xffffu, b = ab >> 16;
-      const float2 pa = s_c[a], pb = s_c[b];
-      float nx = 1.0f, ny = 0.0f;
-      const float ddx = pa.x - pb.x, ddy = pa.y - pb.y;
-      if (ddx * ddx + ddy * ddy > kEps * kEps) {
-        nx = pb.x - pa.x;
-        ny = pb.y - pa.y;
-        normalize(nx, ny);
-      }
-      const float2 lam = g_lam[t];
-      stage[r].ab = ab;
-      stage[r].ln = lam.x;
-      stage[r].lt = lam.y;
-      stage[r].nx = nx;
-      stage[r].ny = ny;
-    }
-  }
-  __syncthreads();  // tab/adj dead: the contact records take their place
-#pragma unroll
-  for (int r = 0; r < KREG; ++r) {
-    const int k = tid + r * BS;
-    if (k < nord) s_ct[k] = stage[r];
-  }
-  __syncthreads();
-  WSTAMP(5);
-
-  const float mA = P.inv_mass, mB = P.inv_mass;
-  const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
-  const float friction = P.friction;
-
-  // ---- warm start + velocity iterations, one thread per island --------------------------
-  for (int I = tid; I < nisl; I += BS) {
-    const int c0 = s_ic[I], c1 = s_ic[I + 1];
-    if (P.warm_starting) {
-      for (int k = c0; k < c1; ++k) {
-        const Contact c = s_ct[k];
-        const int a = c.ab & 0xffffu, b = c.ab >> 16;
-        const float tx = c.ny, ty = -c.nx;
-        const float Px = c.ln * c.nx + c.lt * tx, Py = c.ln * c.ny + c.lt * ty;
-        float2 va = s_v[a], vb = s_v[b];
-        va.x = va.x - mA * Px;
-        va.y = va.y - mA * Py;
-        vb.x = vb.x + mB * Px;
-        vb.y = vb.y + mB * Py;
-        s_v[a] = va;
-        s_v[b] = vb;
-      }
-    }
-    for (int it = 0; it < P.vel_iters; ++it) {
-      for (int k = c0; k < c1; ++k) {
-        const Contact c = s_ct[k];
-        const int a = c.ab & 0xffffu, b = c.ab >> 16;
-        const float nx = c.nx, ny = c.ny, tx = ny, ty = -nx;
-        float2 va = s_v[a], vb = s_v[b];
-        float ln = c.ln, ltg = c.lt;
-        {
-          const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-          const float vt = dvx * tx + dvy * ty;
-          float lambda = kmass * (-vt);
-          const float maxf = friction * ln;
-          const float ni = bclamp(ltg + lambda, -maxf, maxf);
-          lambda = ni - ltg;
-          ltg = ni;
-          const float Px = lambda * tx, Py = lambda * ty;
-          va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-          vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
-        }
-        {
-          const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-          const float vn = dvx * nx + dvy * ny;
-          float lambda = -kmass * (vn - 0.0f);
-          const float ni = bmax(ln + lambda, 0.0f);
-          lambda = ni - ln;
-          ln = ni;
-          const float Px = lambda * nx, Py = lambda * ny;
-          va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-          vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
-        }
-        s_v[a] = va;
-        s_v[b] = vb;
-        s_ct[k].ln = ln;
-        s_ct[k].lt = ltg;
-      }
-    }
-  }
-  __syncthreads();
-  WSTAMP(6);
-  for (int k = tid; k < nord; k += BS) {  // StoreImpulses, back in list order
-    const Contact c = s_ct[k];
-    g_lam[s_ord[k]] = make_float2(c.ln, c.lt);
-  }
-
-  // ---- integrate positions --------------------------------------------------------------
-  float cx = p.x, cy = p.y, vx = 0.0f, vy = 0.0f;
-  if (act) {
-    const float2 vv = s_v[tid];
-    vx = vv.x;
-    vy = vv.y;
-    const float tx = P.dt * vx, ty = P.dt * vy;
-    if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
-      const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
-      vx = vx * ratio;
-      vy = vy * ratio;
-    }
-    cx = cx + P.dt * vx;
-    cy = cy + P.dt * vy;
-    s_c[tid] = make_float2(cx, cy);
-  }
-  __syncthreads();
-
-  // ---- position iterations, one thread per island --------------------------------------------
-  for (int I = tid; I < nisl; I += BS) {
-    const int c0 = s_ic[I], c1 = s_ic[I + 1];
-    int solved = 0;
-    for (int it = 0; it < P.pos_iters; ++it) {
-      float min_sep = 0.0f;
-      for (int k = c0; k < c1; ++k) {
-        const uint32_t ab = s_ct[k].ab;
-        const int a = ab & 0xffffu, b = ab >> 16;
-        float2 ca = s_c[a], cb = s_c[b];
-        float nx = cb.x - ca.x, ny = cb.y - ca.y;
-        normalize(nx, ny);
-        const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - P.radius - P.radius;
-        min_sep = bmin(min_sep, sep);
-        const float Cc = bclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-        const float K = mA + mB;
-        const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
-        const float Px = imp * nx, Py = imp * ny;
-        ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
-        cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
-        s_c[a] = ca;
-        s_c[b] = cb;
-      }
-      if (min_sep >= -3.0f * kLinearSlop) {
-        solved = 1;
-        break;
-      }
-    }
-    s_isolv[I] = (uint8_t)solved;
-  }
-  WSTAMP(7);
-  // ---- sleep clock + island sleep decision --------------------------------------------------------
-  float ns = 0.0f;
-  if (act) {
-    const bool moving = vx * vx + vy * vy > kLinearSleepTol * kLinearSleepTol;
-    ns = moving ? 0.0f : slp + P.dt;
-    s_slp[tid] = ns;
-    s_flag[tid] = (deg == 0 && ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
-  }
-  __syncthreads();
-  for (int I = tid; I < nisl; I += BS) {
-    const int b0 = s_ib[I], b1 = s_ib[I + 1];
-    float mn = 3.402823466e+38f;
-    for (int k = b0; k < b1; ++k) mn = bmin(mn, s_slp[s_ibod[k]]);
-    const uint8_t sl = (mn >= kTimeToSleep && s_isolv[I]) ? 1 : 0;
-    for (int k = b0; k < b1; ++k) s_flag[s_ibod[k]] = sl;
-  }
-  __syncthreads();
-  WSTAMP(8);
-
-  // ---- SynchronizeFixtures ----------------------------------------------------------------------
-  float4 fn = fo;
-  if (act) {
-    const float2 cc = s_c[tid];
-    cx = cc.x;
-    cy = cc.y;
-    const float r = P.radius;
-    const float c0x = p.x, c0y = p.y;
-    const float lox = bmin(c0x - r, cx - r), loy = bmin(c0y - r, cy - r);
-    const float hix = bmax(c0x + r, cx + r), hiy = bmax(c0y + r, cy + r);
-    const bool contains = fo.x <= lox && fo.y <= loy && hix <= fo.z && hiy <= fo.w;
-    if (!contains) {
-      fn = make_float4(lox - kAabbExtension, loy - kAabbExtension, hix + kAabbExtension, hiy + kAabbExtension);
-      const float dx = kAabbMultiplier * (cx - c0x), dy = kAabbMultiplier * (cy - c0y);
-      if (dx < 0.0f) fn.x += dx; else fn.z += dx;
-      if (dy < 0.0f) fn.y += dy; else fn.w += dy;
-    }
-    if (s_flag[tid]) {
-      vx = 0.0f;
-      vy = 0.0f;
-      ns = 0.0f;
-    }
-    Rec r0;  // the contact records are dead (position solve done, sync above)
-    r0.fn = fn;
-    r0.fo = fo;
-    r0.c = make_float2(cx, cy);
-    s_rec[tid] = r0;
-  }
-  __syncthreads();
-  WSTAMP(9);
-
-  // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour ----------------------------
-  //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t); new contacts = Ov(F_t) \ Ov(F_{t-1})
-  bool coll = act && ((s_oldc[tid >> 5] >> (tid & 31)) & 1u);
-  int newcnt = 0;
-  float best = __builtin_inff();
-  int bj = tid == 0 ? 1 : 0;
-  if (act) {
-#pragma unroll 4
-    for (int j = 0; j < N; ++j) {
-      const Rec r = s_rec[j];
-      // b2TestOverlap as one VALU test: separated iff max(lo_j - hi_i, lo_i - hi_j) > 0
-      const bool ovn = !(sep_max(fn, r.fn) > 0.0f);
-      const float dx = r.c.x - cx, dy = r.c.y - cy;
-      const float d2 = dx * dx + dy * dy;
-      const bool other = j != tid;
-      coll |= other && ovn;
-      if (other && d2 < best) {
-        best = d2;
-        bj = j;
-      }
-      if (j > tid && ovn && sep_max(fo, r.fo) > 0.0f) ++newcnt;
-    }
-  }
-  WSTAMP(10);
-  // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs ------------------------
-  uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
-  float2* ocimp = B.cimp[nxt] + (size_t)e * C;
-  int excl;
-  const int nnew = block_scan_excl(newcnt, excl, s_scan);
-  if (act && newcnt > 0) {
-    int w = nnew - excl - newcnt;  // agents > tid come first
-    for (int j = N - 1; j > tid; --j) {
-      const Rec r = s_rec[j];
-      if (overlap(fn, r.fn) && !overlap(fo, r.fo)) {
-        if (w < C) {
-          ocab[w] = (uint32_t)tid | ((uint32_t)j << 16);
-          ocimp[w] = make_float2(0.0f, 0.0f);
-        }
-        ++w;
-      }
-    }
-  }
-  int kept = 0, Tr = 0;
-  for (int k0 = 0; k0 < M; k0 += BS) {
-    const int k = k0 + tid;
-    bool keep = false, touch = false;
-    uint32_t ab = 0u;
-    if (k < M) {
-      ab = cab[k];
-      const int a = ab & 0xffffu, b = ab >> 16;
-      keep = overlap(s_rec[a].fn, s_rec[b].fn);
-      // touching at Collide, from the start-of-step positions (global state not yet overwritten)
-      const float2 pa = B.pos[(size_t)e * N + a], pb = B.pos[(size_t)e * N + b];
-      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
-      touch = !(dx * dx + dy * dy > rr);
-    }
-    int tpos, kpos;
-    const int tn = block_scan_excl(touch ? 1 : 0, tpos, s_scan);
-    const int kn = block_scan_excl(keep ? 1 : 0, kpos, s_scan);
-    if (keep) {
-      const int w = nnew + kept + kpos;
-      const int trank = Tr + tpos;
-      if (w < C) {
-        ocab[w] = ab;
-        ocimp[w] = (touch && trank < tcap) ? g_lam[trank] : make_float2(0.0f, 0.0f);
-      }
-    }
-    Tr += tn;
-    kept += kn;
-  }
-  int total = nnew + kept;
-  if (total > C) {
-    status |= MACM_ST_CONTACT_OVERFLOW;
-    total = C;
-  }
-
-  WSTAMP(11);
-  // ---- rewards + obs -----------------------------------------------------------------------------
-  float rew = 0.0f;
-  if (act) {
-    const float tdx = tg.x - cx, tdy = tg.y - cy;
-    const float td2 = tdx * tdx + tdy * tdy;
-    const double d = sqrt((double)td2);
-    if (coll) rew = -1.0f;
-    else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
-    else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
-    rew_out[ag] = rew;
-    if (coll_out) coll_out[ag] = coll ? 1 : 0;
-    if (nbr_out) nbr_out[ag] = bj;
-    if (obs) {
-      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-      const float2 cb = s_rec[bj].c;
-      write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
-    }
-  }
-  int dummy;
-  const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
-  const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
-  if (status) atomicOr(&s_misc[1], status);
-  __syncthreads();
-  if (act) {
-    B.pos[ag] = make_float2(cx, cy);
-    B.vel[ag] = make_float2(vx, vy);
-    B.angle[ag] = ang;
-    B.fat[ag] = fn;
-    B.sleep[ag] = ns;
-  }
-  if (tid == 0) {
-    const int nst = s_misc[1];
-    const double tp = B.time_passed[e] + P.inv_hz;
-    const uint8_t dn = tp > P.time_limit ? 1 : 0;
-    B.time_passed[e] = tp;
-    B.done[e] = dn;
-    if (done_out) done_out[e] = dn;
-    B.step_count[e] = step_count + 1;
-    B.ccount[nxt][e] = total;
-    if (nst) B.status[e] |= nst;
-    unsigned long long* ec = B.env_counters + (size_t)e * 4;
-    ec[0] += (unsigned long long)N;
-    ec[1] += (unsigned long long)ncoll;
-    ec[2] += (unsigned long long)npos;
-    ec[3] += (unsigned long long)dn;
-  }
-  WSTAMP(12);
-}
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
 // Reset for the workgroup variant: fat AABBs, first FindNewContacts list (all
 // overlapping pairs, descending), zeroed dynamics, initial observation.
@@ -893,6 +202,7 @@ __global__ __launch_bounds__(1024) void flock_init_wg(StepParams P, WorldBuffers
     B.time_passed[e] = 0.0;
     B.done[e] = 0;
     B.status[e] = total > C ? MACM_ST_CONTACT_OVERFLOW : 0;
+    if (total > C) report_status(B, MACM_ST_CONTACT_OVERFLOW);
   }
 }
 
@@ -934,18 +244,21 @@ __global__ __launch_bounds__(1024) void flock_observe_wg(StepParams P, WorldBuff
 }
 
 // ==== split step for large N =========================================================================
-// The fused kernel above keeps one env's whole world in LDS (up to ~134 KB at N = 1024), so a CU
-// holds one env, and while that env's single Gauss-Seidel lane walks a dense island the rest of
-// the CU idles. The split step runs the same algorithm as three launches:
+// A single fused kernel would keep one env's whole world in LDS (up to ~134 KB at N = 1024), so a
+// CU would hold one env, and while that env's single Gauss-Seidel lane walks a dense island the
+// rest of the CU would idle (measured 72.6 ms vs 18.2 ms per C5 step in round 1). The step runs
+// as three launches:
 //   A  flock_step_wg_a : actions, Collide, CSR edges, island DFS, velocity integration, and the
-//                        island-ordered contact records written to HBM (x_cst / x_cimp).
+//                        island-ordered contact records written to HBM (x_cst / x_cimp). Envs
+//                        with more than tcap touching contacts take the spill step here instead
+//                        (x_nisl = -1 tells B and C to skip them).
 //   B  flock_solve_wg  : one wave per env, LDS = positions + velocities only (16 B per body):
 //                        warm start, velocity iterations, StoreImpulses, position integration,
 //                        position iterations. Contacts stream from HBM two records ahead
 //                        (islands of >= 3 contacts; smaller islands stay in registers).
 //   C  flock_step_wg_c : sleep, SynchronizeFixtures, pair sweep, next contact list, rewards, obs,
 //                        write-back.
-// Every arithmetic operation and its order are those of the fused kernel.
+// Every arithmetic operation and its order are those of the wave kernel and the spill step.
 
 struct WgLayoutA {
   int c, deg, csr_off, todo, ord, ib, ibod, stk, ic, scan, misc, tab, adj, total;
@@ -1000,8 +313,12 @@ __host__ __device__ inline int wg_isl_stride(int N) { return N / 2 + 2; }
 // solver LDS: velocities + positions (16 B per body), record/impulse/ab rings, big-island list
 __host__ __device__ inline int wg_solve_lds(int N) { return 16 * N + 2 * 64 * (16 + 8 + 4) + 4 * (64 + 1); }
 
+template <typename OT>
 __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffers B, int cur, int tcap,
-                                                        const void* __restrict__ actions) {
+                                                        const void* __restrict__ actions, OT* __restrict__ obs,
+                                                        int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
+                                                        uint8_t* __restrict__ coll_out,
+                                                        uint8_t* __restrict__ done_out) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
   const int e = blockIdx.x;
@@ -1050,7 +367,6 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   }
   for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0;
   if (tid < 8) s_misc[tid] = 0;
-  int status = 0;
 
   // ---- actions -> angle, force (mvmnt.py:97-129) ---------------------------------
   float Fx = 0.0f, Fy = 0.0f;
@@ -1080,7 +396,6 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     }
     Fx = 0.0f + Fx;
     Fy = 0.0f + Fy;
-    B.angle[ag] = ang;  // kernel C reads it for the observation
   }
   __syncthreads();
 
@@ -1109,10 +424,15 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     }
     T += n;
   }
-  if (T > tcap) {
-    status |= MACM_ST_TOUCH_OVERFLOW;
-    T = tcap;
+  if (T > tcap || P.force_spill) {
+    // More touching contacts than this kernel's LDS holds: the env's whole step runs here as the
+    // spill step (HBM working set, flock_spill.hpp) from its untouched start-of-step state (only
+    // scratch has been written so far), and kernels B and C skip it.
+    spill::step_env<OT, false>(P, B, e, cur, actions, obs, nbr_out, rew_out, coll_out, done_out, lds);
+    if (tid == 0) B.x_nisl[e] = -1;
+    return;
   }
+  if (act) B.angle[ag] = ang;  // kernel C reads it for the observation
   __syncthreads();
 
   // ---- CSR touching edges, each body's segment in list (= Box2D edge) order ---------
@@ -1302,10 +622,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     B.x_ic[(size_t)e * IS + q] = s_ic[q];
     B.x_ib[(size_t)e * IS + q] = s_ib[q];
   }
-  if (tid == 0) {
-    B.x_nisl[e] = nisl;
-    if (status) B.status[e] |= status;
-  }
+  if (tid == 0) B.x_nisl[e] = nisl;
 }
 
 namespace wg {
@@ -1382,11 +699,12 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   const uint32_t* cab = (const uint32_t*)cst;  // .x of each record, stride 4 words
   float2* cimp = B.x_cimp + (size_t)e * tcap;
   const uint16_t* ic = B.x_ic + (size_t)e * IS;
+  const int nisl = B.x_nisl[e];
+  if (nisl < 0) return;  // stepped whole by the spill step in kernel A
   for (int i = lane; i < N; i += W) {
     s_c[i] = B.pos[en + i];
     s_v[i] = B.x_vmid[en + i];
   }
-  const int nisl = B.x_nisl[e];
   if (lane == 0) s_big[W] = 0;
   __syncthreads();
   const int tid = lane;  // for WSTAMP (slots 13..15, diagnostic build)
@@ -1699,11 +1017,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   Rec* s_rec = (Rec*)(lds + L.recs);
   const float2* g_lam = B.scratch + (size_t)e * tcap;
   const int IS = wg_isl_stride(N);
+  const int nisl = B.x_nisl[e];
+  if (nisl < 0) return;  // stepped whole by the spill step in kernel A
 
   const uint32_t* cab = B.cab[cur] + (size_t)e * C;
   const int step_count = B.step_count[e];
   const int M = B.ccount[cur][e];
-  const int nisl = B.x_nisl[e];
   float2 p = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
   float ang = 0.0f, slp = 0.0f, cx = 0.0f, cy = 0.0f, vx = 0.0f, vy = 0.0f;
   float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1890,7 +1209,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     if (done_out) done_out[e] = dn;
     B.step_count[e] = step_count + 1;
     B.ccount[nxt][e] = total;
-    if (nst) B.status[e] |= nst;
+    if (nst) {
+      B.status[e] |= nst;
+      report_status(B, nst);
+    }
     unsigned long long* ec = B.env_counters + (size_t)e * 4;
     ec[0] += (unsigned long long)N;
     ec[1] += (unsigned long long)ncoll;
@@ -1901,59 +1223,56 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 
 // ---- launchers -------------------------------------------------------------------------------------
 int wg_block(int N) { return ((N + 63) / 64) * 64; }
-int wg_lds_bytes(int N, int tcap) { return wg_layout(N, tcap).total; }
 int wg_init_lds_bytes(int N) { return align16((int)sizeof(wg::Rec) * N) + 4 * 32; }
+// kernel A's dynamic LDS: its own layout, and room for the spill step's per-body arrays (pair
+// records in HBM) for the envs that take it
+static int wg_a_lds_bytes(int N, int tcap) {
+  const int a = wg_layout_a(N, tcap).total, s = spill::layout(N, false).total;
+  return a > s ? a : s;
+}
+// the largest dynamic LDS of the step's kernels (checked against the device at world creation)
+int wg_lds_bytes(int N, int tcap) {
+  int m = wg_a_lds_bytes(N, tcap);
+  if (wg_solve_lds(N) > m) m = wg_solve_lds(N);
+  if (wg_layout_c(N).total > m) m = wg_layout_c(N).total;
+  if (wg_init_lds_bytes(N) > m) m = wg_init_lds_bytes(N);
+  return m;
+}
 
 // Raise the dynamic-LDS limit of the workgroup kernels once (world creation).
 hipError_t wg_configure(int N, int tcap) {
-  const int step = wg_lds_bytes(N, tcap), init = wg_init_lds_bytes(N);
   hipError_t e = hipSuccess;
-  const void* fs[] = {(const void*)flock_step_wg<float>, (const void*)flock_step_wg<double>};
   const void* fi[] = {(const void*)flock_init_wg<float>, (const void*)flock_init_wg<double>};
-  for (const void* f : fs)
-    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, step);
   for (const void* f : fi)
-    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, init);
-  const void* fsplit[] = {(const void*)flock_step_wg_a, (const void*)flock_solve_wg,
-                          (const void*)flock_step_wg_c<float>, (const void*)flock_step_wg_c<double>};
-  const int lsplit[] = {wg_layout_a(N, tcap).total, wg_solve_lds(N), wg_layout_c(N).total, wg_layout_c(N).total};
-  for (int i = 0; i < 4; ++i)
+    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, wg_init_lds_bytes(N));
+  const void* fsplit[] = {(const void*)flock_step_wg_a<float>, (const void*)flock_step_wg_a<double>,
+                          (const void*)flock_solve_wg, (const void*)flock_step_wg_c<float>,
+                          (const void*)flock_step_wg_c<double>};
+  const int la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
+  const int lsplit[] = {la, la, wg_solve_lds(N), lc, lc};
+  for (int i = 0; i < 5; ++i)
     if (e == hipSuccess) e = hipFuncSetAttribute(fsplit[i], hipFuncAttributeMaxDynamicSharedMemorySize, lsplit[i]);
   return e;
-}
-
-// The split step (kernels A, B, C above) unless MACM_WG_FUSED=1 (A/B comparisons).
-static bool wg_use_split() {
-  static const int v = [] {
-    const char* s = getenv("MACM_WG_FUSED");
-    return (s && s[0] == '1') ? 0 : 1;
-  }();
-  return v != 0;
 }
 
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
                           hipStream_t s) {
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
-  if (wg_use_split()) {
-    const int N = P.n_agents, lc = wg_layout_c(N).total;
-    hipLaunchKernelGGL(flock_step_wg_a, grid, block, wg_layout_a(N, tcap).total, s, P, B, cur, tcap, actions);
+  const int N = P.n_agents, la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
+  if (obs_f64) {
+    hipLaunchKernelGGL(flock_step_wg_a<double>, grid, block, la, s, P, B, cur, tcap, actions, (double*)obs, nbr, rew,
+                       coll, done);
     hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
-    if (obs_f64)
-      hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, s, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
-                         done);
-    else
-      hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, s, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
-                         done);
-    return hipGetLastError();
+    hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, s, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
+                       done);
+  } else {
+    hipLaunchKernelGGL(flock_step_wg_a<float>, grid, block, la, s, P, B, cur, tcap, actions, (float*)obs, nbr, rew,
+                       coll, done);
+    hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
+    hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, s, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
+                       done);
   }
-  const int lds = wg_lds_bytes(P.n_agents, tcap);
-  if (obs_f64)
-    hipLaunchKernelGGL(flock_step_wg<double>, grid, block, lds, s, P, B, cur, tcap, actions, (double*)obs, nbr, rew,
-                       coll, done);
-  else
-    hipLaunchKernelGGL(flock_step_wg<float>, grid, block, lds, s, P, B, cur, tcap, actions, (float*)obs, nbr, rew,
-                       coll, done);
   return hipGetLastError();
 }
 

@@ -44,6 +44,8 @@ hipError_t launch_bots_combat(const void* obs, const uint8_t* mask, bool obs_f64
 hipError_t wg_configure(int N, int tcap);
 int wg_block(int N);
 int wg_lds_bytes(int N, int tcap);
+hipError_t launch_check_actions(const void* actions, int mode, const uint8_t* alive, long long rows,
+                                unsigned long long* first_bad, hipStream_t s);
 }  // namespace macm
 
 using namespace macm;
@@ -55,12 +57,14 @@ struct macm_world {
   int cur;  // which contact-list buffer holds the current ordered list
   int device;
   bool wave;  // N <= 64: one wavefront per env (flock_step_w64); else one workgroup per env
-  int tcap;   // touching-contact capacity per env
+  int tcap;   // touching-contact capacity per env of the fast kernels (more: the spill step)
   std::vector<int32_t> tidx;
   std::vector<void*> allocs;
   uint32_t* mt = nullptr;     // [E][kMtStride] per-env MT19937 streams (valid after reset)
   uint8_t* rmask = nullptr;   // [E] reset mask scratch
   bool mt_valid = false;
+  uint32_t* hstat = nullptr;  // host-mapped status word (B.host_status is its device alias)
+  unsigned long long* bad = nullptr;  // validate_actions: first failing row (device scratch)
 };
 
 struct macm_tdm {
@@ -76,6 +80,8 @@ struct macm_tdm {
   uint32_t* mt = nullptr;
   uint8_t* rmask = nullptr;
   bool mt_valid = false;
+  uint32_t* hstat = nullptr;
+  unsigned long long* bad = nullptr;
 };
 
 static thread_local std::string g_last_error;
@@ -150,6 +156,51 @@ void fill_body_params(StepParams& P, double hz, float radius, float density, flo
 void free_world(macm_world* w) {
   for (void* p : w->allocs) (void)hipFree(p);
   w->allocs.clear();
+  if (w->hstat) (void)hipHostFree(w->hstat);
+  w->hstat = nullptr;
+}
+
+// The host-mapped status word: kernels store nonzero status bits into it (report_status), and
+// the step entry points read it without synchronising. Returns its device alias.
+hipError_t alloc_host_status(uint32_t** host, uint32_t** dev) {
+  hipError_t e = hipHostMalloc((void**)host, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return e;
+  **host = 0u;
+  return hipHostGetDevicePointer((void**)dev, *host, 0);
+}
+
+uint32_t read_host_status(const uint32_t* h) { return h ? __atomic_load_n(h, __ATOMIC_ACQUIRE) : 0u; }
+void clear_host_status(uint32_t* h) {
+  if (h) __atomic_store_n(h, 0u, __ATOMIC_RELEASE);
+}
+
+// Per-env contact capacity C (see macm_world_create in include/macm.h): every pair when that
+// fits the memory budget (and always for N <= 64, the wave kernel), else the budget's C.
+int64_t default_capacity(int N, int E) {
+  const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
+  if (N <= 64) return all_pairs;
+  const int64_t budget = 8LL << 30, per_entry = 80;  // lists 2 x (4 + 8) B + spill working set 56 B
+  if (all_pairs * per_entry * E <= budget) return all_pairs;
+  int64_t c = budget / (per_entry * E);
+  if (c < 32LL * N) c = 32LL * N;
+  return c < all_pairs ? c : all_pairs;
+}
+
+// validate_actions (macm_config / macm_tdm_config): run the check kernel and wait for it.
+int check_actions(unsigned long long* bad, const void* actions, int mode, const uint8_t* alive, int E, int N,
+                  hipStream_t s) {
+  HIP_TRY(hipMemsetAsync(bad, 0xff, sizeof(unsigned long long), s));
+  HIP_TRY(launch_check_actions(actions, mode, alive, (long long)E * N, bad, s));
+  unsigned long long h = ~0ull;
+  HIP_TRY(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (h != ~0ull) {
+    const char* space = mode == 0 ? "MultiDiscrete([3, 3, 3])" : mode == 1 ? "Box([-1, -1], [1, 1])"
+                                                                           : "MultiDiscrete([3, 3, 3, 2])";
+    return fail(MACM_E_INVALID, "action of env " + std::to_string(h / N) + " agent " + std::to_string(h % N) +
+                                    " is not in the action space " + space + " (no env was stepped)");
+  }
+  return MACM_OK;
 }
 
 hipError_t launch_init(macm_world* w, const macm_outputs* out, const uint8_t* mask, hipStream_t s) {
@@ -171,8 +222,8 @@ void save_stream(std::vector<uint32_t>& host, int e, const PyMT19937& r) {
 extern "C" {
 
 const char* macm_version(void) {
-  return "macm-hip 0.3.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernel N<=1024; "
-         "TDM: wave-per-env kernel N<=64)";
+  return "macm-hip 0.4.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernels N<=1024, "
+         "spill step for dense envs; TDM: wave-per-env kernel N<=64)";
 }
 int macm_abi_version(void) { return MACM_ABI_VERSION; }
 const char* macm_last_error(void) { return g_last_error.c_str(); }
@@ -232,11 +283,11 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       tidx[i] = targets_idx[i];
     }
   const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
-  // N <= 64: room for every pair (never overflows). Larger N: 32 list entries per
-  // agent by default (fat-AABB pairs; ~7.3 per agent even in C5's dense start).
-  const int64_t dflt = N <= 64 ? all_pairs : (all_pairs < 32LL * N ? all_pairs : 32LL * N);
-  int C = max_contacts > 0 ? max_contacts : (int)dflt;
-  if (C > all_pairs) C = (int)all_pairs;
+  if (max_contacts < 0) return fail(MACM_E_INVALID, "max_contacts must be >= 0");
+  int64_t C64 = max_contacts > 0 ? (int64_t)max_contacts : default_capacity(N, n_envs);
+  if (C64 > all_pairs) C64 = all_pairs;
+  if (C64 < 1) C64 = 1;
+  const int C = (int)C64;
 
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -265,6 +316,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   P.action_mode = c.action_mode;
   P.reward_mode = c.reward_mode;
   P.coord = c.coord;
+  P.force_spill = 0;
   fill_body_params(P, c.hz, c.radius, c.density, c.friction, c.linear_damping, c.agent_force,
                    c.agent_rotation_speed);
   P.reward_radius = c.reward_radius;
@@ -296,16 +348,28 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
                     (rc = dalloc(w, &B.x_vmid, EN)) || (rc = dalloc(w, &B.x_cout, EN)) ||
                     (rc = dalloc(w, &B.x_vout, EN)) || (rc = dalloc(w, &B.x_deg, EN)) ||
                     (rc = dalloc(w, &B.x_isolv, (size_t)n_envs * (N / 2 + 2))))) ||
+      // spill step working set (flock_spill.hpp), capacity C per env
+      (rc = dalloc(w, &B.sp_tab, (size_t)n_envs * C)) || (rc = dalloc(w, &B.sp_adj, (size_t)n_envs * 2 * C)) ||
+      (rc = dalloc(w, &B.sp_ord, (size_t)n_envs * C)) || (rc = dalloc(w, &B.sp_cst, (size_t)n_envs * C)) ||
+      (rc = dalloc(w, &B.sp_cim, (size_t)n_envs * C)) || (rc = dalloc(w, &B.sp_lam, (size_t)n_envs * C)) ||
+      (!w->wave && (rc = dalloc(w, (float4**)&B.sp_rec, EN * 3))) ||  // 48-B records
+      (rc = dalloc(w, &B.spill_count, (size_t)n_envs)) || (rc = dalloc(w, &w->bad, 1)) ||
       (rc = dalloc(w, &w->mt, (size_t)n_envs * kMtStride)) || (rc = dalloc(w, &w->rmask, (size_t)n_envs))
   ) {
     free_world(w);
     delete w;
     return rc;
   }
+  if (hipError_t he = alloc_host_status(&w->hstat, &B.host_status); he != hipSuccess) {
+    free_world(w);
+    delete w;
+    return fail(MACM_E_OOM, std::string("hipHostMalloc (status word): ") + hipGetErrorString(he));
+  }
   hipError_t e = hipMemcpy(B.tidx, tidx.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemset(B.env_counters, 0, (size_t)n_envs * 4 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
+  if (e == hipSuccess) e = hipMemset(B.spill_count, 0, sizeof(uint32_t) * n_envs);
   if (e == hipSuccess && !w->wave) {
     hipDeviceProp_t prop;
     e = hipGetDeviceProperties(&prop, device);
@@ -372,6 +436,8 @@ int macm_world_reset(macm_world* w, uint64_t seed, int64_t env_offset, const mac
     save_stream(mts, e, r);
   }
   hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipStreamSynchronize(s));  // earlier steps' status stores land before the word is cleared
+  clear_host_status(w->hstat);
   HIP_TRY(hipMemcpyAsync(w->B.pos, pos.data(), pos.size() * sizeof(float2), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w->B.angle, ang.data(), ang.size() * sizeof(float), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w->B.targets, tg.data(), tg.size() * sizeof(float2), hipMemcpyHostToDevice, s));
@@ -390,6 +456,8 @@ int macm_world_place(macm_world* w, const void* pos, const void* angle, const vo
   DeviceGuard g(w->device);
   const size_t EN = (size_t)w->P.n_envs * w->P.n_agents, ET = (size_t)w->P.n_envs * w->P.n_targets;
   hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  clear_host_status(w->hstat);
   HIP_TRY(hipMemcpyAsync(w->B.pos, pos, EN * sizeof(float2), hipMemcpyDefault, s));
   HIP_TRY(hipMemcpyAsync(w->B.angle, angle, EN * sizeof(float), hipMemcpyDefault, s));
   HIP_TRY(hipMemcpyAsync(w->B.targets, targets, ET * sizeof(float2), hipMemcpyDefault, s));
@@ -427,9 +495,25 @@ int macm_world_reset_envs(macm_world* w, const uint8_t* env_mask, const macm_out
   return MACM_OK;
 }
 
+static int overflow_error(uint32_t st) {
+  std::string what;
+  if (st & MACM_ST_CONTACT_OVERFLOW) what += " contact-list capacity (max_contacts);";
+  if (st & MACM_ST_TOUCH_OVERFLOW) what += " touching-contact capacity;";
+  if (st & MACM_ST_DEGREE_OVERFLOW) what += " per-body contact capacity;";
+  return fail(MACM_E_OVERFLOW, "an env outgrew its" + what +
+                                   " the results since that step are not the reference's (status bits " +
+                                   std::to_string(st) + "; reset, place or set_state clears them)");
+}
+
 int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream) {
   if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
   DeviceGuard g(w->device);
+  if (w->cfg.validate_actions) {
+    const int rc = check_actions(w->bad, actions, w->cfg.action_mode == MACM_ACTION_DISCRETE ? 0 : 1, nullptr,
+                                 w->P.n_envs, w->P.n_agents, (hipStream_t)stream);
+    if (rc) return rc;
+  }
   if (w->wave)
     HIP_TRY(launch_step_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
                             out->collided, out->done, (hipStream_t)stream));
@@ -450,11 +534,41 @@ int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
   return MACM_OK;
 }
 
+// set_state: the kernels index a list by its count and its packed pairs (cab + e*C, LDS arrays
+// by body index), so only lists with 0 <= count <= C and a < b < N in every entry are accepted.
+static int validate_lists(const void* count, const void* ab, size_t E, size_t C, int N, hipStream_t s) {
+  if (!count && !ab) return MACM_OK;
+  if (!count || !ab) return fail(MACM_E_INVALID, "contact_count and contact_ab must be given together");
+  std::vector<int32_t> cnt(E);
+  std::vector<uint32_t> lst(E * C);
+  HIP_TRY(hipMemcpyAsync(cnt.data(), count, E * sizeof(int32_t), hipMemcpyDefault, s));
+  HIP_TRY(hipMemcpyAsync(lst.data(), ab, E * C * sizeof(uint32_t), hipMemcpyDefault, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (size_t e = 0; e < E; ++e) {
+    if (cnt[e] < 0 || (size_t)cnt[e] > C)
+      return fail(MACM_E_INVALID, "env " + std::to_string(e) + ": contact_count " + std::to_string(cnt[e]) +
+                                      " outside [0, max_contacts = " + std::to_string(C) + "]");
+    for (int k = 0; k < cnt[e]; ++k) {
+      const uint32_t v = lst[e * C + k], a = v & 0xffffu, b = v >> 16;
+      if (!(a < b && b < (uint32_t)N))
+        return fail(MACM_E_INVALID, "env " + std::to_string(e) + ": contact_ab[" + std::to_string(k) +
+                                        "] is not a pair a < b < n_agents");
+    }
+  }
+  return MACM_OK;
+}
+
 static int copy_state(macm_world* w, const macm_state* st, void* stream, bool to_device) {
   if (!w || !st) return fail(MACM_E_INVALID, "world/state is NULL");
   DeviceGuard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   const size_t E = w->P.n_envs, N = w->P.n_agents, T = w->P.n_targets, C = w->P.max_contacts;
+  if (to_device) {
+    if (const int rc = validate_lists(st->contact_count, st->contact_ab, E, C, (int)N, s)) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    clear_host_status(w->hstat);  // an injected state starts clean
+    HIP_TRY(hipMemsetAsync(w->B.status, 0, E * sizeof(int32_t), s));
+  }
   struct Item {
     void* user;
     void* dev;
@@ -533,6 +647,26 @@ int macm_world_reset_counters(macm_world* w, void* stream) {
   return MACM_OK;
 }
 
+int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream) {
+  if (!w || !env_steps) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  std::vector<uint32_t> h((size_t)w->P.n_envs);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(h.data(), w->B.spill_count, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  int64_t acc = 0;
+  for (uint32_t v : h) acc += v;
+  *env_steps = acc;
+  return MACM_OK;
+}
+
+int macm_world_set_debug(macm_world* w, int32_t flags) {
+  if (!w) return fail(MACM_E_INVALID, "world is NULL");
+  if (flags & ~MACM_DEBUG_FORCE_SPILL) return fail(MACM_E_INVALID, "unknown debug flag");
+  w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
+  return MACM_OK;
+}
+
 // ============================ TDM =============================================
 
 int macm_tdm_config_default(macm_tdm_config* c) {
@@ -570,6 +704,8 @@ int macm_tdm_config_default(macm_tdm_config* c) {
 static void free_tdm(macm_tdm* w) {
   for (void* p : w->allocs) (void)hipFree(p);
   w->allocs.clear();
+  if (w->hstat) (void)hipHostFree(w->hstat);
+  w->hstat = nullptr;
 }
 
 int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, macm_tdm** out) {
@@ -647,11 +783,16 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
       (rc = dalloc(A, &B.time_passed, E)) || (rc = dalloc(A, &B.done, E)) || (rc = dalloc(A, &B.status, E)) ||
       (rc = dalloc(A, &B.env_counters, E * 4)) || (rc = dalloc(A, &TB.health, EN)) ||
       (rc = dalloc(A, &TB.cd_atk, EN)) || (rc = dalloc(A, &TB.cd_mov, EN)) || (rc = dalloc(A, &TB.alive, EN)) ||
-      (rc = dalloc(A, &TB.listener, E)) || (rc = dalloc(A, &TB.winner, E)) ||
+      (rc = dalloc(A, &TB.listener, E)) || (rc = dalloc(A, &TB.winner, E)) || (rc = dalloc(A, &w->bad, 1)) ||
       (rc = dalloc(A, &w->mt, E * kMtStride)) || (rc = dalloc(A, &w->rmask, E))) {
     free_tdm(w);
     delete w;
     return rc;
+  }
+  if (hipError_t he = alloc_host_status(&w->hstat, &B.host_status); he != hipSuccess) {
+    free_tdm(w);
+    delete w;
+    return fail(MACM_E_OOM, std::string("hipHostMalloc (status word): ") + hipGetErrorString(he));
   }
   hipError_t e = hipMemset(B.env_counters, 0, E * 4 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * E);
@@ -686,6 +827,8 @@ static TdmBuffers tdm_with_outputs(const macm_tdm* w, const macm_tdm_outputs* ou
 }
 
 static int tdm_init(macm_tdm* w, const macm_tdm_outputs* out, hipStream_t s) {
+  HIP_TRY(hipStreamSynchronize(s));  // earlier steps' status stores land before the word is cleared
+  clear_host_status(w->hstat);
   w->cur = 0;
   const TdmBuffers TB = tdm_with_outputs(w, out);
   HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
@@ -762,7 +905,12 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
 
 int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream) {
   if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
   DeviceGuard g(w->device);
+  if (w->cfg.validate_actions) {
+    const int rc = check_actions(w->bad, actions, 2, w->TB.alive, w->P.n_envs, w->P.n_agents, (hipStream_t)stream);
+    if (rc) return rc;
+  }
   const TdmBuffers TB = tdm_with_outputs(w, out);
   HIP_TRY(launch_tdm_step_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
                               w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream));
@@ -812,6 +960,12 @@ static int tdm_copy_state(macm_tdm* w, const macm_tdm_state* st, void* stream, b
       {st->done, w->B.done, E},
       {st->winner, w->TB.winner, E * sizeof(int32_t)},
   };
+  if (to_device) {
+    if (const int rc = validate_lists(st->contact_count, st->contact_ab, E, C, (int)N, s)) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    clear_host_status(w->hstat);
+    HIP_TRY(hipMemsetAsync(w->B.status, 0, E * sizeof(int32_t), s));
+  }
   for (const Item& it : items) {
     if (!it.user) continue;
     if (to_device) HIP_TRY(hipMemcpyAsync(it.dev, it.user, it.bytes, hipMemcpyDefault, s));

@@ -14,7 +14,9 @@ ACTION_DISCRETE, ACTION_CONTINUOUS = 0, 1
 REWARD_BINARY, REWARD_LINEAR = 0, 1
 COORD_POLAR, COORD_CARTESIAN = 0, 1
 
-ST_CONTACT_OVERFLOW, ST_TOUCH_OVERFLOW, ST_DEGREE_OVERFLOW = 1, 2, 4
+ST_CONTACT_OVERFLOW, ST_TOUCH_OVERFLOW, ST_DEGREE_OVERFLOW, ST_INVALID_ACTION = 1, 2, 4, 8
+DEBUG_FORCE_SPILL = 1
+E_INVALID, E_OVERFLOW = -1, -5
 
 _ERRORS = {
     -1: "MACM_E_INVALID",
@@ -36,7 +38,7 @@ class MacmConfig(Structure):
         ("position_iterations", c_int32),
         ("warm_starting", c_int32),
         ("obs_f64", c_int32),
-        ("_pad0", c_int32),
+        ("validate_actions", c_int32),
         ("hz", c_double),
         ("start_spread", c_double),
         ("start_point", c_double * 2),
@@ -93,6 +95,8 @@ class MacmTdmConfig(Structure):
         ("obs_f64", c_int32),
         ("fresh_raycast", c_int32),
         ("decay_mov_penalty", c_int32),
+        ("validate_actions", c_int32),
+        ("_pad", c_int32),
         ("hz", c_double),
         ("world_width", c_double),
         ("world_height", c_double),
@@ -143,13 +147,26 @@ def tdm_config_from_defaults() -> "MacmTdmConfig":
 
 
 class MacmLibraryError(RuntimeError):
-    """The HIP library could not be loaded: the product path refuses to run."""
+    """The HIP library failed: it could not be loaded (the product path refuses to run without
+    it), or one of its calls returned an error (MacmError)."""
 
 
-class MacmError(RuntimeError):
+class MacmError(MacmLibraryError):
+    """A C-ABI call returned a negative MACM_E_* status; ``code`` holds it."""
+
     def __init__(self, code: int, fn: str, msg: str):
         super().__init__(f"{fn} failed: {_ERRORS.get(code, code)}: {msg}")
         self.code = code
+
+
+class MacmOverflowError(MacmError):
+    """MACM_E_OVERFLOW: an env outgrew a capacity in an earlier step, so the results since then
+    are not the reference's (the step refuses to continue until reset / place / set_state)."""
+
+
+class MacmInvalidActionError(MacmError):
+    """MACM_E_INVALID from a step with validate_actions: an action outside the action space
+    (the reference's ``assert self.action_space.contains(actions)``); no env was stepped."""
 
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # gym-macm_amd/
@@ -175,6 +192,8 @@ SIGNATURES = {
     "macm_world_status": (c_int, [c_void_p, POINTER(c_int32), c_void_p]),
     "macm_world_counters": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_world_reset_counters": (c_int, [c_void_p, c_void_p]),
+    "macm_world_spilled": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
+    "macm_world_set_debug": (c_int, [c_void_p, c_int32]),
     "macm_tdm_config_default": (c_int, [POINTER(MacmTdmConfig)]),
     "macm_tdm_create": (c_int, [POINTER(MacmTdmConfig), c_int32, c_int32, POINTER(c_void_p)]),
     "macm_tdm_destroy": (c_int, [c_void_p]),
@@ -222,4 +241,9 @@ def lib():
 def check(code: int, fn: str) -> None:
     if code != 0:
         msg = lib().macm_last_error()
-        raise MacmError(code, fn, msg.decode() if msg else "")
+        msg = msg.decode() if msg else ""
+        if code == E_OVERFLOW:
+            raise MacmOverflowError(code, fn, msg)
+        if code == E_INVALID and fn.endswith("_step") and "action space" in msg:
+            raise MacmInvalidActionError(code, fn, msg)
+        raise MacmError(code, fn, msg)

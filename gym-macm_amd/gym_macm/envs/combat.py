@@ -205,6 +205,7 @@ class TDM(object):
             a[0, k] = actions[agent.id] if agent.alive else (1, 1, 1, 0)
         self.world.step(self._act)
         self._sync()
+        self.world.check_status()  # a TDM capacity overflow raises right here
         self._cache = None
         alive_before = [agent.alive for agent in self.agents]
         self.obs = self._obs_dict()

@@ -188,6 +188,9 @@ class Flock(object):
         obs_t, nbr_t, rew_t, _ = self.world.step(self._act)
         self._sync()
         self._cache = None
+        # the dict API waits for every step anyway: a capacity overflow (only the contact list
+        # can overflow; dense touching contacts take the spill step) raises right here
+        self.world.check_status()
         obs = obs_t[0].numpy()
         rew = rew_t[0].numpy()
         half = obs.shape[1] // 2

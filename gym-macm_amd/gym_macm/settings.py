@@ -80,7 +80,8 @@ class flockSettings(fwSettings):
         self.reward_radius = self._reward_radius if self.reward_mode == "binary" else 1
 
 
-def to_config(s: fwSettings, n_agents: int, n_targets: int, obs_f64: bool = False) -> _abi.MacmConfig:
+def to_config(s: fwSettings, n_agents: int, n_targets: int, obs_f64: bool = False,
+              validate_actions: bool = False) -> _abi.MacmConfig:
     """Flatten a settings object into ``macm_config``; rejects what the HIP path does not model."""
     if getattr(s, "render", False):
         raise NotImplementedError("render=True (pyglet GUI) is out of scope: headless NoRender only")
@@ -107,6 +108,7 @@ def to_config(s: fwSettings, n_agents: int, n_targets: int, obs_f64: bool = Fals
     c.position_iterations = int(s.positionIterations)
     c.warm_starting = 1 if s.enableWarmStarting else 0
     c.obs_f64 = 1 if obs_f64 else 0
+    c.validate_actions = 1 if validate_actions else 0
     c.hz = float(s.hz)
     c.start_spread = float(s.start_spread)
     c.start_point[0] = float(s.start_point[0])
@@ -148,7 +150,7 @@ class combatSettings(fwSettings):
 
 
 def to_tdm_config(s: combatSettings, n_agents, obs_f64=False, fresh_raycast=False, decay_mov_penalty=False,
-                  world_width=30.0, world_height=30.0):
+                  world_width=30.0, world_height=30.0, validate_actions=False):
     """Flatten combatSettings + TDM/Agent constants (combat.py:13-29,76-77) into macm_tdm_config."""
     sizes = [int(n) for n in n_agents]
     if not 1 <= len(sizes) <= 4:
@@ -162,6 +164,7 @@ def to_tdm_config(s: combatSettings, n_agents, obs_f64=False, fresh_raycast=Fals
     c.position_iterations = int(s.positionIterations)
     c.warm_starting = 1 if s.enableWarmStarting else 0
     c.obs_f64 = 1 if obs_f64 else 0
+    c.validate_actions = 1 if validate_actions else 0
     c.fresh_raycast = 1 if fresh_raycast else 0
     c.decay_mov_penalty = 1 if decay_mov_penalty else 0
     c.hz = float(s.hz)

@@ -16,7 +16,8 @@ from . import _abi
 from .world import _ptr
 
 
-def tdm_config(n_agents=(1, 1), obs_f64=False, fresh_raycast=False, decay_mov_penalty=False, **overrides):
+def tdm_config(n_agents=(1, 1), obs_f64=False, fresh_raycast=False, decay_mov_penalty=False, validate_actions=False,
+               **overrides):
     """macm_tdm_config for TDM(n_agents=[...]) with combatSettings values
     (settings.py:149-177); keyword overrides use the config field names."""
     sizes = [int(n) for n in n_agents]
@@ -30,6 +31,7 @@ def tdm_config(n_agents=(1, 1), obs_f64=False, fresh_raycast=False, decay_mov_pe
     c.obs_f64 = 1 if obs_f64 else 0
     c.fresh_raycast = 1 if fresh_raycast else 0
     c.decay_mov_penalty = 1 if decay_mov_penalty else 0
+    c.validate_actions = 1 if validate_actions else 0
     names = {f for f, _ in _abi.MacmTdmConfig._fields_}
     for k, v in overrides.items():
         if k not in names:
@@ -178,6 +180,14 @@ class TdmWorld:
         v = ctypes.c_int32()
         _abi.check(self.L.macm_tdm_status(self.h, ctypes.byref(v), self._stream()), "macm_tdm_status")
         return int(v.value)
+
+    def check_status(self) -> None:
+        """Raise MacmOverflowError if any env overflowed the TDM kernel's contact capacities
+        (256 touching contacts, 16 per body; synchronises the stream)."""
+        st = self.status()
+        if st:
+            raise _abi.MacmOverflowError(_abi.E_OVERFLOW, "macm_tdm_status",
+                                         f"status bits {st}: an env outgrew the TDM kernel's contact capacities")
 
     def counters(self) -> np.ndarray:
         out = (ctypes.c_int64 * 4)()

@@ -25,14 +25,15 @@ from gym_macm.world import World
 
 class FlockVec(object):
     def __init__(self, num_envs, n_agents=(10,), targets=None, seed=0, env_offset=0, device=None,
-                 obs_dtype=torch.float32, max_contacts=0, autoreset=False, **kwargs):
+                 obs_dtype=torch.float32, max_contacts=0, autoreset=False, validate_actions=False, **kwargs):
         self.settings = flockSettings(**kwargs)
         self.num_envs = int(num_envs)
         self.n_agents = list(n_agents) if not isinstance(n_agents, int) else [n_agents]
         N = int(sum(self.n_agents))
         self.n_targets = 1 if targets is None else len(np.unique(targets))
         self.targets_idx = np.zeros(N, np.int32) if targets is None else np.asarray(targets, np.int32)
-        cfg = to_config(self.settings, N, self.n_targets, obs_f64=(obs_dtype == torch.float64))
+        cfg = to_config(self.settings, N, self.n_targets, obs_f64=(obs_dtype == torch.float64),
+                        validate_actions=validate_actions)
         self.world = World(cfg, self.targets_idx, self.num_envs, device=device, max_contacts=max_contacts)
         self.device = self.world.device
         self.N = N
@@ -55,7 +56,12 @@ class FlockVec(object):
         """One step of every env. With ``autoreset``, envs whose episode ended in this
         step start their next episode right away (reset_envs on the done flags, on
         the device): the returned done marks them and obs already holds the new
-        episode's initial observation for those envs."""
+        episode's initial observation for those envs.
+
+        Raises MacmOverflowError (a MacmLibraryError) once an earlier step has overflowed a
+        capacity (the contact list's max_contacts; dense touching contacts never overflow: the
+        spill step takes them), MacmInvalidActionError with ``validate_actions=True`` and an
+        action outside the action space (no env is stepped, as the reference asserts first)."""
         out = self.world.step(actions)
         if self.autoreset:
             self.world.reset_envs(self.world.done)
@@ -76,6 +82,14 @@ class FlockVec(object):
 
     def status(self):
         return self.world.status()
+
+    def check_status(self):
+        """Raise MacmOverflowError if any env overflowed a capacity (synchronises)."""
+        self.world.check_status()
+
+    def spilled(self):
+        """Env-steps taken by the spill step (dense envs) since creation."""
+        return self.world.spilled()
 
     def counters(self):
         return self.world.counters()

@@ -162,11 +162,18 @@ class World:
         return s
 
     def set_state(self, s: dict) -> None:
+        """Inject a state (get_state's layout). Contact lists saved from a world with a different
+        max_contacts are re-padded; a list longer than this world's capacity raises ValueError
+        (truncating it would change the physics). The library validates the pairs too."""
         ref = self.state_buffers()
+        counts = np.asarray(s["contact_count"], dtype=np.int32)
+        if counts.shape == (self.E,) and (counts.max(initial=0) > self.C or counts.min(initial=0) < 0):
+            raise ValueError(f"contact_count must lie in [0, {self.C}] (this world's max_contacts); "
+                             f"got [{int(counts.min())}, {int(counts.max())}]")
         arrs = {}
         for k, v in ref.items():
             a = np.ascontiguousarray(np.asarray(s[k], dtype=v.dtype))
-            if k in ("contact_ab", "contact_imp") and a.shape[1] != self.C:
+            if k in ("contact_ab", "contact_imp") and a.ndim >= 2 and a.shape[1] != self.C:
                 pad = np.zeros_like(v)
                 n = min(a.shape[1], self.C)
                 pad[:, :n] = a[:, :n]
@@ -190,3 +197,21 @@ class World:
 
     def reset_counters(self) -> None:
         _abi.check(self.L.macm_world_reset_counters(self.h, self._stream()), "macm_world_reset_counters")
+
+    def spilled(self) -> int:
+        """Env-steps taken by the spill step (dense envs beyond the fast kernels' LDS capacities)."""
+        v = ctypes.c_int64()
+        _abi.check(self.L.macm_world_spilled(self.h, ctypes.byref(v), self._stream()), "macm_world_spilled")
+        return int(v.value)
+
+    def set_debug(self, flags: int) -> None:
+        """Test hooks (macm_world_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the
+        spill step."""
+        _abi.check(self.L.macm_world_set_debug(self.h, int(flags)), "macm_world_set_debug")
+
+    def check_status(self) -> None:
+        """Raise MacmOverflowError if any env has a status bit set (synchronises the stream)."""
+        st = self.status()
+        if st:
+            raise _abi.MacmOverflowError(_abi.E_OVERFLOW, "macm_world_status",
+                                         f"status bits {st}: an env outgrew a capacity (max_contacts={self.C})")

@@ -36,26 +36,39 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 2
+#define MACM_ABI_VERSION 3
 
 enum {
   MACM_OK = 0,
-  MACM_E_INVALID = -1,     /* bad argument / config                          */
+  MACM_E_INVALID = -1,     /* bad argument / config / action (validate_actions) */
   MACM_E_OOM = -2,         /* device allocation failed                       */
   MACM_E_HIP = -3,         /* HIP runtime error                              */
   MACM_E_UNSUPPORTED = -4, /* config valid for the reference, not built here */
-  MACM_E_OVERFLOW = -5     /* a per-env capacity (contacts/islands) overflowed */
+  MACM_E_OVERFLOW = -5     /* a per-env capacity overflowed in an earlier step: results since
+                              then are not the reference's (reset / place / set_state clear it) */
 };
 
 enum { MACM_ACTION_DISCRETE = 0, MACM_ACTION_CONTINUOUS = 1 };
 enum { MACM_REWARD_BINARY = 0, MACM_REWARD_LINEAR = 1 };
 enum { MACM_COORD_POLAR = 0, MACM_COORD_CARTESIAN = 1 };
 
-/* Status bits accumulated per env on the device (macm_world_status). */
+/*
+ * Status bits accumulated per env on the device (macm_world_status). Flock never sets
+ * TOUCH/DEGREE: an env whose touching contacts exceed a fast kernel's LDS capacity is stepped
+ * by the spill step (HBM working set sized by max_contacts) instead. CONTACT_OVERFLOW (the
+ * fat-AABB pair list itself outgrew max_contacts) and TDM's TOUCH/DEGREE caps remain; once any
+ * bit is set, the next step call returns MACM_E_OVERFLOW.
+ */
 enum {
-  MACM_ST_CONTACT_OVERFLOW = 1, /* Ov(F_t) list exceeded max_contacts            */
-  MACM_ST_TOUCH_OVERFLOW = 2,   /* touching contacts exceeded the solver capacity */
-  MACM_ST_DEGREE_OVERFLOW = 4   /* a body touched more bodies than the adjacency cap */
+  MACM_ST_CONTACT_OVERFLOW = 1, /* Ov(F_t) list exceeded max_contacts                   */
+  MACM_ST_TOUCH_OVERFLOW = 2,   /* TDM: touching contacts exceeded the solver capacity   */
+  MACM_ST_DEGREE_OVERFLOW = 4,  /* TDM: a body touched more bodies than the adjacency cap */
+  MACM_ST_INVALID_ACTION = 8    /* validate_actions: an action outside the action space  */
+};
+
+/* macm_world_set_debug flags (test hooks; 0 = product behaviour). */
+enum {
+  MACM_DEBUG_FORCE_SPILL = 1 /* every env takes the spill step (parity tests of that path) */
 };
 
 /*
@@ -73,7 +86,10 @@ typedef struct macm_config {
   int32_t position_iterations; /* 3                                 settings.py:32   */
   int32_t warm_starting;       /* enableWarmStarting = True         settings.py:34   */
   int32_t obs_f64;             /* 0: obs written as float32, 1: float64              */
-  int32_t _pad0;
+  int32_t validate_actions;    /* 1: macm_world_step checks every action against the
+                                  action space first (assert action_space.contains,
+                                  mvmnt.py:94) and returns MACM_E_INVALID without
+                                  stepping; synchronises the stream. 0 (default): no check */
   double hz;                   /* 60.0                              settings.py:30   */
   double start_spread;         /* 20                                settings.py:119  */
   double start_point[2];       /* [0, 0]                            settings.py:120  */
@@ -111,6 +127,10 @@ typedef struct macm_tdm_config {
   int32_t decay_mov_penalty;    /* 0 (reference): cooldown_mov_penalty is never
                                    decremented (combat.py:151,155). 1: decremented by
                                    1/hz alongside cooldown_atk.                        */
+  int32_t validate_actions;     /* 1: macm_tdm_step checks the alive agents' actions
+                                   (assert action_space.contains, combat.py:118) first,
+                                   MACM_E_INVALID without stepping; synchronises          */
+  int32_t _pad;
   double hz;                    /* 60                                                 */
   double world_width;           /* 30                                 combat.py:76    */
   double world_height;          /* 30                                 combat.py:77    */
@@ -235,7 +255,12 @@ int macm_config_default(macm_config* cfg);
 /*
  * Create E envs of one Flock configuration on `device`.
  *   targets_idx: host int32[N], agent -> target index (mvmnt.py:43), or NULL = all 0.
- *   max_contacts: per-env ordered contact list capacity, 0 = N(N-1)/2 (never overflows).
+ *   max_contacts: per-env capacity C of the ordered fat-AABB pair list (and of the spill
+ *   step's HBM working set, 80 B per entry and env with the list). 0 = the default:
+ *   N(N-1)/2 (every pair: the list can never overflow) when N <= 64 or when E * N(N-1)/2 * 80 B
+ *   fits in 8 GiB; otherwise the largest C with E * C * 80 B <= 8 GiB (at least 32 N).
+ *   macm_world_info reports the value chosen. Overflow of the list sets
+ *   MACM_ST_CONTACT_OVERFLOW and the next macm_world_step returns MACM_E_OVERFLOW.
  * Replaces: Flock.__init__ world + body creation (mvmnt.py:35-79,
  * cm_framework.py:155-167). State is undefined until macm_world_reset.
  */
@@ -280,13 +305,23 @@ int macm_world_reset_envs(macm_world* w, const uint8_t* env_mask, const macm_out
  *   actions: device pointer. Discrete: uint8/int8 [E, N, 3] in {0,1,2}
  *   (MultiDiscrete([3,3,3]), mvmnt.py:143-145). Continuous: float32 [E, N, 2] in [-1,1].
  * Replaces Flock.step (mvmnt.py:81-140) incl. b2World.Step(1/hz, 8, 3) + ClearForces.
+ * Returns MACM_E_OVERFLOW (and launches nothing) if an earlier step or reset set a status bit
+ * (read from a host-mapped word the kernels write; no synchronisation). With
+ * cfg.validate_actions, returns MACM_E_INVALID and steps no env if any action is outside the
+ * action space (reference: AssertionError before any agent acts, mvmnt.py:94).
  */
 int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream);
 
 /* Observation of the current state without stepping (Flock.get_obs, mvmnt.py:181-222). */
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream);
 
-/* Copy state out / in (synchronous w.r.t. `stream`). */
+/*
+ * Copy state out / in (synchronous w.r.t. `stream`). set_state validates the contact lists
+ * it is given (when contact_count is non-NULL): 0 <= count <= C and, for every entry below the
+ * count, a < b < N (host copies of contact_ab are checked on the host, device copies after a
+ * staging copy); otherwise MACM_E_INVALID and nothing is copied. contact_ab and contact_count
+ * must be given together. Clears the status bits.
+ */
 int macm_world_get_state(macm_world* w, const macm_state* dst, void* stream);
 int macm_world_set_state(macm_world* w, const macm_state* src, void* stream);
 
@@ -301,6 +336,12 @@ int macm_world_status(macm_world* w, int32_t* status_or, void* stream);
  */
 int macm_world_counters(macm_world* w, int64_t out[4], void* stream);
 int macm_world_reset_counters(macm_world* w, void* stream);
+
+/* Env-steps taken by the spill step since creation (dense worlds; synchronises `stream`). */
+int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream);
+
+/* Test hooks: MACM_DEBUG_* flags (0 = product behaviour). */
+int macm_world_set_debug(macm_world* w, int32_t flags);
 
 /* ---- TDM (gym_macm:cm-tdm-v0, combat.py:57-264) -------------------------- */
 
@@ -336,7 +377,8 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
 /*
  * One TDM.step for all E envs (combat.py:104-184). actions: device uint8
  * [E, N, 4] (MultiDiscrete([3,3,3,2]): forward, lateral, rotation, attack);
- * rows of dead agents are ignored.
+ * rows of dead agents are ignored. Returns MACM_E_OVERFLOW if a capacity (256 touching
+ * contacts, 16 per body) overflowed in an earlier step; MACM_E_INVALID with validate_actions.
  */
 int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream);
 

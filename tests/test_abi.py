@@ -30,15 +30,30 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, name), name
 
 
-def test_struct_layouts_match_header():
-    # sizes fixed by the header's field order (no implicit padding surprises)
-    assert ctypes.sizeof(_abi.MacmConfig) == 10 * 4 + 10 * 8 + 4 * 4
-    assert ctypes.sizeof(_abi.MacmOutputs) == 5 * 8
-    assert ctypes.sizeof(_abi.MacmState) == 11 * 8
-    assert ctypes.sizeof(_abi.MacmWorldInfo) == 8 * 4
-    assert ctypes.sizeof(_abi.MacmTdmConfig) == 12 * 4 + 12 * 8 + 4 * 4
-    assert ctypes.sizeof(_abi.MacmTdmOutputs) == 6 * 8
-    assert ctypes.sizeof(_abi.MacmTdmState) == 17 * 8
+def test_struct_layouts_match_header(tmp_path):
+    """Every field offset and struct size of the ctypes mirror equals what a C compiler lays
+    out from include/macm.h (gcc, no GPU needed)."""
+    import subprocess
+    structs = {"macm_config": _abi.MacmConfig, "macm_outputs": _abi.MacmOutputs, "macm_state": _abi.MacmState,
+               "macm_world_info": _abi.MacmWorldInfo, "macm_tdm_config": _abi.MacmTdmConfig,
+               "macm_tdm_outputs": _abi.MacmTdmOutputs, "macm_tdm_state": _abi.MacmTdmState}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'  printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    r = subprocess.run(["gcc", "-std=c99", "-o", str(exe), str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                               check=True).stdout.split("\n") if line)
+    for cname, cls in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, f"{cname}.{f}"
 
 
 def test_tdm_defaults_match_python_mirror():
@@ -57,7 +72,7 @@ def test_tdm_defaults_match_python_mirror():
 
 def test_version_and_defaults_without_gpu():
     L = _abi.lib()
-    assert L.macm_abi_version() == 2
+    assert L.macm_abi_version() == 3
     assert b"gfx950" in L.macm_version()
     c = _abi.MacmConfig()
     assert L.macm_config_default(ctypes.byref(c)) == 0

@@ -157,12 +157,6 @@ def test_determinism_two_runs_identical():
     assert_state_equal(outs[0], outs[1], "second run")
 
 
-def test_contact_overflow_is_reported():
-    v = FlockVec(4, n_agents=[64], seed=3, device="cuda:0", start_spread=4, max_contacts=8)
-    v.step(torch.ones((4, 64, 3), dtype=torch.uint8, device="cuda:0"))
-    assert v.status() & 1
-
-
 def test_counters():
     v = FlockVec(8, n_agents=[32], seed=1, device="cuda:0")
     v.world.reset_counters()

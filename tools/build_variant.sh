@@ -5,7 +5,7 @@ set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; shift
 mkdir -p ab/build_$NAME
-SRC="flock_step_w64 flock_step_wg bots env_reset macm_capi"
+SRC="flock_step_w64 flock_step_wg bots env_reset actions_check macm_capi"
 for f in $SRC; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-result "$@" \
     -c -o ab/build_$NAME/$f.o gym-macm_amd/csrc/$f.hip &

@@ -36,7 +36,7 @@ __global__ void check(uint32_t end, unsigned long long* bad, uint32_t* first) {
   for (int i = 0; i < kNCount; ++i) atomicAdd(&bad[i], nb[i]);
 }
 
-// div_by_invariant(n, K) == n / K for every float32 n in {0} u [2^-40, 0.2] (the position solve's
+// div_by_invariant(n, K) == n / K for every float32 n in {-0, +0} u [2^-40, 0.2] (the position solve's
 // -C: 0 or >= 2^-40, at most kMaxLinearCorrection) and K in Ks: the default config's K and random ones.
 __global__ void check_div(const float* Ks, int nK, uint32_t end, unsigned long long* bad) {
   unsigned long long nb[2] = {};  // n = 0 or n >= 2^-40 (what the step can give it), below
@@ -47,6 +47,10 @@ __global__ void check_div(const float* Ks, int nK, uint32_t end, unsigned long l
       const float a = macm::div_by_invariant(n, K), b = n / K;
       if (__float_as_uint(a) != __float_as_uint(b)) ++nb[(n == 0.0f || n >= 0x1p-40f) ? 0 : 1];
     }
+    // n = -0.0 (the step gives it when C = +0: -C), compared bitwise like the rest
+    if (blockIdx.x == 0 && threadIdx.x == 0 &&
+        __float_as_uint(macm::div_by_invariant(-0.0f, K)) != __float_as_uint(-0.0f / K))
+      ++nb[0];
   }
   atomicAdd(&bad[0], nb[0]);
   atomicAdd(&bad[1], nb[1]);
