@@ -33,6 +33,7 @@ struct StepParams {
   int32_t vel_iters, pos_iters, warm_starting;
   int32_t action_mode, reward_mode, coord;
   int32_t force_spill;  // test hook (macm_world_set_debug): every env takes the spill step
+  int32_t sweep;        // workgroup pair sweep: 0 = by N (strip cells at N >= 512), 1 = cells, 2 = all pairs
   float dt;          // fl32(1.0 / hz)                       cm_framework.py:182-185 -> world.Step
   float inv_dt;      // 1.0f / dt                            b2World::Step
   float inv_mass;    // 1 / (density * b2_pi * r * r)        b2CircleShape::ComputeMass
@@ -40,7 +41,6 @@ struct StepParams {
   float radius;      // circle radius
   float friction;    // b2MixFriction = sqrtf(f * f)
   float force_f32;   // (float)agent_force (continuous mode: numpy float32 * int)
-  float _padf;
   double rot_step;   // rotation_speed, multiplied as ((a2-1) * rot) * (1/hz)   mvmnt.py:103-104
   double inv_hz;     // 1 / hz (Python float division)                       mvmnt.py:104,134
   double force;      // agent_force (double)                                 mvmnt.py:113-116

@@ -18,6 +18,7 @@
 // (flock_spill.hpp) inside kernel A, and B and C skip it.
 #include "flock_common.hpp"
 #include "flock_spill.hpp"
+#include "flock_grid.hpp"
 
 namespace macm {
 namespace wg {
@@ -289,7 +290,7 @@ __host__ __device__ inline WgLayoutA wg_layout_a(int N, int tcap) {
 }
 
 struct WgLayoutC {
-  int slp, flags, oldc, scan, misc, recs, total;
+  int slp, flags, oldc, scan, misc, fn, fo, c, gred, gpar, gstart, gent, pk, bjv, total;
 };
 __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
   WgLayoutC L;
@@ -304,7 +305,15 @@ __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
   L.oldc = take(4 * ((N + 31) / 32));
   L.scan = take(4 * 32);
   L.misc = take(4 * 8);
-  L.recs = take((int)sizeof(wg::Rec) * N);
+  L.fn = take(16 * N);  // pair-sweep records, SoA: new fat AABB, old fat AABB, final position
+  L.fo = take(16 * N);
+  L.c = take(8 * N);
+  L.gred = take(4 * 4 * 16);
+  L.gpar = take(4 * 8);
+  L.gstart = take(4 * (grid::buckets(N) + 1) > 2 * N + 4 ? 4 * (grid::buckets(N) + 1) : 2 * N + 4);
+  L.gent = take(16 * N);
+  L.pk = take(4 * N);   // per body: collided bit 31 | new-pair count (sweep)
+  L.bjv = take(2 * N);  // per body: nearest neighbour (sweep); then new-pair segment starts
   L.total = o;
   return L;
 }
@@ -1014,28 +1023,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   uint32_t* s_oldc = (uint32_t*)(lds + L.oldc);
   int* s_scan = (int*)(lds + L.scan);
   int* s_misc = (int*)(lds + L.misc);
-  Rec* s_rec = (Rec*)(lds + L.recs);
+  float4* s_fn = (float4*)(lds + L.fn);
+  float4* s_fo = (float4*)(lds + L.fo);
+  float2* s_c = (float2*)(lds + L.c);
+  uint32_t* s_pk = (uint32_t*)(lds + L.pk);
+  uint16_t* s_bjv = (uint16_t*)(lds + L.bjv);
   const float2* g_lam = B.scratch + (size_t)e * tcap;
   const int IS = wg_isl_stride(N);
   const int nisl = B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
+  WSTAMP(0);
 
   const uint32_t* cab = B.cab[cur] + (size_t)e * C;
   const int step_count = B.step_count[e];
   const int M = B.ccount[cur][e];
-  float2 p = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
-  float ang = 0.0f, slp = 0.0f, cx = 0.0f, cy = 0.0f, vx = 0.0f, vy = 0.0f;
+  float2 p = make_float2(0.0f, 0.0f);
+  float slp = 0.0f, cx = 0.0f, cy = 0.0f, vx = 0.0f, vy = 0.0f;
   float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   bool hasdeg = false;
   if (act) {
     p = B.pos[ag];
-    ang = B.angle[ag];
     fo = B.fat[ag];
     slp = B.sleep[ag];
     const float2 c = B.x_cout[ag], vv = B.x_vout[ag];
     cx = c.x; cy = c.y; vx = vv.x; vy = vv.y;
     hasdeg = B.x_deg[ag] != 0;
-    tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
   }
   for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
   if (tid < 8) s_misc[tid] = 0;
@@ -1057,19 +1069,41 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     s_flag[tid] = (!hasdeg && ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
   }
   __syncthreads();
+  WSTAMP(1);
   {
+    // island sleep (b2Island::Solve's minSleepTime): one thread per island body; the island of
+    // body slot k is found by binary search over the island ranges (copied to LDS), the minimum
+    // by LDS atomicMin on the float bits (sleep clocks are >= 0, so their bit patterns order as
+    // the floats). Scratch: the grid's entry / bucket arrays, not yet in use.
     const uint16_t* ib = B.x_ib + (size_t)e * IS;
     const uint16_t* ibod = B.x_ibod + (size_t)e * N;
     const uint8_t* isolv = B.x_isolv + (size_t)e * IS;
-    for (int I = tid; I < nisl; I += BS) {
-      const int b0 = ib[I], b1 = ib[I + 1];
-      float mn = 3.402823466e+38f;
-      for (int k = b0; k < b1; ++k) mn = bmin(mn, s_slp[ibod[k]]);
-      const uint8_t sl = (mn >= kTimeToSleep && isolv[I]) ? 1 : 0;
-      for (int k = b0; k < b1; ++k) s_flag[ibod[k]] = sl;
+    uint16_t* s_ib = (uint16_t*)(lds + L.gent);     // [nisl + 1] <= N / 2 + 2 (gent: 16 N bytes)
+    uint32_t* s_mn = (uint32_t*)(lds + L.gstart);   // [nisl] <= N / 2 (gstart: >= 8 N bytes)
+    for (int I = tid; I <= nisl; I += BS) s_ib[I] = ib[I];
+    for (int I = tid; I < nisl; I += BS) s_mn[I] = 0x7f7fffffu;  // FLT_MAX, as the serial minimum starts
+    __syncthreads();
+    const int nb = nisl > 0 ? s_ib[nisl] : 0;
+    for (int k = tid; k < nb; k += BS) {
+      int lo = 0, hi = nisl - 1;  // the island I with ib[I] <= k < ib[I + 1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_ib[mid] <= k) lo = mid; else hi = mid - 1;
+      }
+      atomicMin(&s_mn[lo], __float_as_uint(s_slp[ibod[k]]));
+    }
+    __syncthreads();
+    for (int k = tid; k < nb; k += BS) {
+      int lo = 0, hi = nisl - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_ib[mid] <= k) lo = mid; else hi = mid - 1;
+      }
+      s_flag[ibod[k]] = (__uint_as_float(s_mn[lo]) >= kTimeToSleep && isolv[lo]) ? 1 : 0;
     }
   }
   __syncthreads();
+  WSTAMP(2);
 
   // ---- SynchronizeFixtures ----------------------------------------------------------------------
   float4 fn = fo;
@@ -1090,25 +1124,104 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       vy = 0.0f;
       ns = 0.0f;
     }
-    Rec r0;
-    r0.fn = fn;
-    r0.fo = fo;
-    r0.c = make_float2(cx, cy);
-    s_rec[tid] = r0;
+    s_fn[tid] = fn;
+    s_fo[tid] = fo;
+    s_c[tid] = make_float2(cx, cy);
+    // final velocity, sleep clock and fat AABB (nothing below reads them back; frees registers
+    // for the sweep)
+    B.vel[ag] = make_float2(vx, vy);
+    B.fat[ag] = fn;
+    B.sleep[ag] = ns;
   }
   __syncthreads();
+  WSTAMP(3);
 
-  // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour ----------------------------
+  // ---- pair sweep over the spatial hash (flock_grid.hpp): collisions, new-pair counts, nearest
+  //      neighbour. Candidates of a body are the bodies of the 3 x 3 cell block around it; an env
+  //      whose positions or extents the hash cannot bin takes the all-pairs sweep.
+  const grid::Lds G{(float*)(lds + L.gred), (float*)(lds + L.gpar), (uint32_t*)(lds + L.gstart),
+                    (float4*)(lds + L.gent), grid::buckets(N)};
   bool coll = act && ((s_oldc[tid >> 5] >> (tid & 31)) & 1u);
   int newcnt = 0;
   float best = __builtin_inff();
   int bj = tid == 0 ? 1 : 0;
-  if (act) {
+  // strip cells from N = 512 (at C5's 1024 they halve the candidates and match the all-pairs
+  // sweep's time; at 256 the all-pairs sweep is 15% faster: DESIGN.md §3)
+#ifdef MACM_AB_ALL_PAIRS
+  const bool cells = false;
+#else
+  const bool cells = P.sweep == 1 || (P.sweep == 0 && N >= grid::kCellsMinAgents);
+#endif
+  const bool gok = cells && grid::build(G, act, make_float2(cx, cy), fn);
+  WSTAMP(4);
+  // Thread t sweeps the body of strip-sorted entry t (flock_grid.hpp): body i, its wave's tile of
+  // strips [s0, s1], walked with broadcast reads. Results go to LDS per body (s_pk: collided bit
+  // 31 | new-pair count, s_slp: best d2, s_bjv: neighbour), read back by the owning thread.
+  int ti = 0, ts0 = 1, ts1 = 0;
+  if (gok) {
+    const float4 E = act ? G.ent[tid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int i = __float_as_int(E.z);
+    const float px = E.x, py = E.y;
+    const float4 fni = s_fn[i], foi = s_fo[i];
+    int s0, s1;
+    grid::tile(G, act, px, s0, s1);
+    ti = i;
+    ts0 = s0;
+    ts1 = s1;
+    float bst = __builtin_inff();
+    int bjj = i == 0 ? 1 : 0;
+    bool col = false;
+    int nc = 0;
+    const int q0 = s0 <= s1 ? (int)G.start[s0] : 0, q1 = s0 <= s1 ? (int)G.start[s1 + 1] : 0;
+    for (int q = q0; q < q1; ++q) {
+      const float4 Eq = G.ent[q];
+      const int j = __float_as_int(Eq.z);
+      const bool ovn = !(sep_max(fni, s_fn[j]) > 0.0f);
+      const float dx = Eq.x - px, dy = Eq.y - py;
+      const bool other = j != i;
+      if (other) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
+      col |= other && ovn;
+      if (j > i && ovn && sep_max(foi, s_fo[j]) > 0.0f) ++nc;
+    }
+    // nearest neighbours the tile cannot certify: the wave walks the other strips for them
+    const bool need = act && !grid::certified(G, px, s0, s1, bst);
+    if (__ballot(need)) {
+#ifdef MACM_STAMPS
+      if (need) atomicAdd(&s_misc[3], 1);
+#endif
+      const int qn = (int)G.start[G.H];
+      for (int q = 0; q < qn; ++q) {
+        if (q == q0) q = q1;
+        if (q >= qn) break;
+        const float4 Eq = G.ent[q];
+        const int j = __float_as_int(Eq.z);
+        const float dx = Eq.x - px, dy = Eq.y - py;
+        if (need && j != i) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
+      }
+    }
+#ifdef MACM_STAMPS
+    if (act) atomicAdd(&s_misc[2], q1 - q0);
+#endif
+    if (act) {
+      s_slp[i] = bst;
+      s_bjv[i] = (uint16_t)bjj;
+      s_pk[i] = (col ? 0x80000000u : 0u) | (uint32_t)nc;
+    }
+    __syncthreads();
+    if (act) {
+      const uint32_t pk = s_pk[tid];
+      coll |= (pk >> 31) != 0;
+      newcnt = (int)(pk & 0x7fffffffu);
+      best = s_slp[tid];
+      bj = s_bjv[tid];
+    }
+  } else if (act) {
 #pragma unroll 2
     for (int j = 0; j < N; ++j) {
-      const Rec r = s_rec[j];
-      const bool ovn = !(sep_max(fn, r.fn) > 0.0f);
-      const float dx = r.c.x - cx, dy = r.c.y - cy;
+      const float4 rfn = s_fn[j];
+      const float2 rc = s_c[j];
+      const bool ovn = !(sep_max(fn, rfn) > 0.0f);
+      const float dx = rc.x - cx, dy = rc.y - cy;
       const float d2 = dx * dx + dy * dy;
       const bool other = j != tid;
       coll |= other && ovn;
@@ -1116,19 +1229,52 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         best = d2;
         bj = j;
       }
-      if (j > tid && ovn && sep_max(fo, r.fo) > 0.0f) ++newcnt;
+      if (j > tid && ovn && sep_max(fo, s_fo[j]) > 0.0f) ++newcnt;
     }
   }
   // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs ------------------------
+  WSTAMP(5);
   uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
   float2* ocimp = B.cimp[nxt] + (size_t)e * C;
   int excl;
   const int nnew = block_scan_excl(newcnt, excl, s_scan);
-  if (act && newcnt > 0) {
+  if (gok && nnew <= 2 * N) {
+    // The partners again, same mapping and tiles, into each body's segment of an LDS scratch
+    // (the dead sleep-clock array: 2N u16 slots; s_bjv holds the segment starts), then each
+    // owner sorts its segment descending and writes it out.
+    uint16_t* s_np = (uint16_t*)s_slp;
+    if (act) s_bjv[tid] = (uint16_t)excl;
+    __syncthreads();
+    {
+      const int i = ti;
+      const float4 fni = s_fn[i], foi = s_fo[i];
+      const int q0 = ts0 <= ts1 ? (int)G.start[ts0] : 0, q1 = ts0 <= ts1 ? (int)G.start[ts1 + 1] : 0;
+      int w = act ? (int)s_bjv[i] : 0;
+      for (int q = q0; q < q1; ++q) {
+        const int j = __float_as_int(G.ent[q].z);
+        if (j > i && !(sep_max(fni, s_fn[j]) > 0.0f) && sep_max(foi, s_fo[j]) > 0.0f) s_np[w++] = (uint16_t)j;
+      }
+    }
+    __syncthreads();
+    if (act && newcnt > 0) {
+      uint16_t* seg = s_np + excl;
+      for (int a = 1; a < newcnt; ++a) {  // insertion sort, descending
+        const uint16_t x = seg[a];
+        int b = a - 1;
+        for (; b >= 0 && seg[b] < x; --b) seg[b + 1] = seg[b];
+        seg[b + 1] = x;
+      }
+      int w = nnew - excl - newcnt;
+      for (int t = 0; t < newcnt; ++t, ++w)
+        if (w < C) {
+          ocab[w] = (uint32_t)tid | ((uint32_t)seg[t] << 16);
+          ocimp[w] = make_float2(0.0f, 0.0f);
+        }
+    }
+  } else if (act && newcnt > 0) {  // all-pairs (no cells, or more new pairs than the scratch holds)
     int w = nnew - excl - newcnt;
     for (int j = N - 1; j > tid; --j) {
-      const Rec r = s_rec[j];
-      if (overlap(fn, r.fn) && !overlap(fo, r.fo)) {
+      if (!(sep_max(fn, s_fn[j]) > 0.0f) && sep_max(fo, s_fo[j]) > 0.0f) {
         if (w < C) {
           ocab[w] = (uint32_t)tid | ((uint32_t)j << 16);
           ocimp[w] = make_float2(0.0f, 0.0f);
@@ -1138,6 +1284,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     }
   }
   const float rr = (P.radius + P.radius) * (P.radius + P.radius);
+  WSTAMP(6);
   int kept = 0, Tr = 0;
   for (int k0 = 0; k0 < M; k0 += BS) {
     const int k = k0 + tid;
@@ -1146,7 +1293,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     if (k < M) {
       ab = cab[k];
       const int a = ab & 0xffffu, b = ab >> 16;
-      keep = overlap(s_rec[a].fn, s_rec[b].fn);
+      keep = overlap(s_fn[a], s_fn[b]);
       const float2 pa = B.pos[(size_t)e * N + a], pb = B.pos[(size_t)e * N + b];
       const float dx = pb.x - pa.x, dy = pb.y - pa.y;
       touch = !(dx * dx + dy * dy > rr);
@@ -1172,8 +1319,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   }
 
   // ---- rewards + obs -----------------------------------------------------------------------------
+  WSTAMP(7);
   float rew = 0.0f;
   if (act) {
+    const float2 tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
+    const float ang = B.angle[ag];
     const float tdx = tg.x - cx, tdy = tg.y - cy;
     const float td2 = tdx * tdx + tdy * tdy;
     const double d = sqrt((double)td2);
@@ -1185,7 +1335,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     if (nbr_out) nbr_out[ag] = bj;
     if (obs) {
       const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-      const float2 cb = s_rec[bj].c;
+      const float2 cb = s_c[bj];
       write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
     }
   }
@@ -1194,11 +1344,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);
   if (status) atomicOr(&s_misc[1], status);
   __syncthreads();
+  WSTAMP(8);
   if (act) {
     B.pos[ag] = make_float2(cx, cy);
-    B.vel[ag] = make_float2(vx, vy);
-    B.fat[ag] = fn;
-    B.sleep[ag] = ns;
   }
   if (tid == 0) {
     const int nst = s_misc[1];
@@ -1219,6 +1367,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     ec[2] += (unsigned long long)npos;
     ec[3] += (unsigned long long)dn;
   }
+  WSTAMP(9);
+#ifdef MACM_STAMPS
+  if (tid == 0) {  // strip diagnostics: tile candidates per body (x1000), bodies walking all strips, strip width
+    B.stamps[(size_t)e * 16 + 10] = (unsigned long long)s_misc[2] * 1000ull / N;
+    B.stamps[(size_t)e * 16 + 11] = (unsigned long long)s_misc[3];
+    B.stamps[(size_t)e * 16 + 12] = (unsigned long long)__float_as_uint(G.par[2]);
+  }
+#endif
 }
 
 // ---- launchers -------------------------------------------------------------------------------------

@@ -317,6 +317,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   P.reward_mode = c.reward_mode;
   P.coord = c.coord;
   P.force_spill = 0;
+  P.sweep = 0;
   fill_body_params(P, c.hz, c.radius, c.density, c.friction, c.linear_damping, c.agent_force,
                    c.agent_rotation_speed);
   P.reward_radius = c.reward_radius;
@@ -662,8 +663,12 @@ int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream) {
 
 int macm_world_set_debug(macm_world* w, int32_t flags) {
   if (!w) return fail(MACM_E_INVALID, "world is NULL");
-  if (flags & ~MACM_DEBUG_FORCE_SPILL) return fail(MACM_E_INVALID, "unknown debug flag");
+  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SWEEP_CELLS | MACM_DEBUG_SWEEP_ALL_PAIRS))
+    return fail(MACM_E_INVALID, "unknown debug flag");
+  if ((flags & MACM_DEBUG_SWEEP_CELLS) && (flags & MACM_DEBUG_SWEEP_ALL_PAIRS))
+    return fail(MACM_E_INVALID, "SWEEP_CELLS and SWEEP_ALL_PAIRS exclude each other");
   w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
+  w->P.sweep = (flags & MACM_DEBUG_SWEEP_CELLS) ? 1 : (flags & MACM_DEBUG_SWEEP_ALL_PAIRS) ? 2 : 0;
   return MACM_OK;
 }
 

@@ -16,6 +16,8 @@ COORD_POLAR, COORD_CARTESIAN = 0, 1
 
 ST_CONTACT_OVERFLOW, ST_TOUCH_OVERFLOW, ST_DEGREE_OVERFLOW, ST_INVALID_ACTION = 1, 2, 4, 8
 DEBUG_FORCE_SPILL = 1
+DEBUG_SWEEP_CELLS = 2
+DEBUG_SWEEP_ALL_PAIRS = 4
 E_INVALID, E_OVERFLOW = -1, -5
 
 _ERRORS = {

@@ -206,7 +206,8 @@ class World:
 
     def set_debug(self, flags: int) -> None:
         """Test hooks (macm_world_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the
-        spill step."""
+        spill step; DEBUG_SWEEP_CELLS / DEBUG_SWEEP_ALL_PAIRS pick the workgroup path's pair sweep
+        regardless of N (default: strip cells at N >= 512)."""
         _abi.check(self.L.macm_world_set_debug(self.h, int(flags)), "macm_world_set_debug")
 
     def check_status(self) -> None:

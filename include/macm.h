@@ -68,7 +68,9 @@ enum {
 
 /* macm_world_set_debug flags (test hooks; 0 = product behaviour). */
 enum {
-  MACM_DEBUG_FORCE_SPILL = 1 /* every env takes the spill step (parity tests of that path) */
+  MACM_DEBUG_FORCE_SPILL = 1,     /* every env takes the spill step (parity tests of that path)  */
+  MACM_DEBUG_SWEEP_CELLS = 2,     /* N > 64: pair sweep over strip cells at any N (else N >= 512) */
+  MACM_DEBUG_SWEEP_ALL_PAIRS = 4  /* N > 64: all-pairs pair sweep at any N                        */
 };
 
 /*

@@ -101,7 +101,7 @@ def test_metric_config_full_size_deterministic():
 
 def test_c3_full_size_4096x256_four_flocks():
     tg = [i // 64 for i in range(256)]
-    flock_full(4096, 256, 12, targets=tg, max_contacts=4096, n_sample=2)
+    flock_full(4096, 256, 40, targets=tg, max_contacts=4096, n_sample=2)
 
 
 def test_c5_shard_full_size_2048x1024():

@@ -13,7 +13,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MACM_LIB"] = os.path.join(REPO, "gym-macm_amd", "build", "libmacm_hip_stamps.so")
+os.environ["MACM_LIB"] = os.environ.get("MACM_STAMPS_LIB",
+                                        os.path.join(REPO, "gym-macm_amd", "build", "libmacm_hip_stamps.so"))
 sys.path.insert(0, os.path.join(REPO, "gym-macm_amd"))
 
 import numpy as np  # noqa: E402
@@ -26,6 +27,10 @@ PHASES = ["actions", "collide", "adjacency", "dfs+integrate+normals", "velocity_
           "position_solve+sleepclk", "sleep_decision", "sync_fixtures", "pairs+nearest", "list_build",
           "reward+obs+writeback", "bookkeeping"]
 # flock_step_wg (N > 64): WSTAMP(0..12) in csrc/flock_step_wg.hip
+# split step: flock_step_wg_c stamps 0..9, flock_solve_wg stamps 13..15
+PHASES_C = ["oldc+sleep_clock", "island_sleep", "sync_fixtures", "grid_build", "pair_sweep+nearest",
+            "new_pairs", "old_list", "reward+obs", "writeback"]
+PHASES_B = ["solve_velocity", "solve_position"]
 PHASES_WG = ["loads+actions", "collide", "csr+sort", "dfs", "integrate+records", "velocity_solve",
              "impulses+integrate+position", "sleep", "sync_fixtures", "pairs+nearest", "list_build",
              "reward+obs+writeback"]
@@ -51,7 +56,7 @@ def main():
     gen = torch.Generator(device="cuda:0")
     gen.manual_seed(1)
     buf = np.zeros((E, 16), np.uint64)
-    deltas, stats, walls = [], [], []
+    deltas, stats, walls, stats_wg = [], [], [], []
     for s in range(args.warmup + args.steps):
         if args.policy == "bots":
             from gym_macm.bots import flock_actions
@@ -69,13 +74,17 @@ def main():
             walls.append(ev0.elapsed_time(ev1))
             _abi.check(L.macm_debug_stamps(vec.world.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))),
                        "stamps")
-            t = buf[:, :14].astype(np.int64)
-            deltas.append(np.diff(t, axis=1))
+            if N > 64:
+                t = np.concatenate([buf[:, :10], buf[:, 13:16]], 1).astype(np.int64)
+                dd = np.diff(t, axis=1)
+                deltas.append(np.concatenate([dd[:, :9], dd[:, 10:]], 1))
+            else:
+                t = buf[:, :14].astype(np.int64)
+                deltas.append(np.diff(t, axis=1))
             stats.append(buf[:, 14:].copy())
+            stats_wg.append(buf[:, 10:13].copy())
     d = np.concatenate(deltas)  # [steps*E, 13]
-    phases = PHASES if N <= 64 else PHASES_WG
-    if N > 64:
-        d = d[:, :12]
+    phases = PHASES if N <= 64 else PHASES_C + PHASES_B
     st = np.concatenate(stats)
     total = d.sum(axis=1)
     out = {"envs": E, "agents": N, "spread": args.spread, "policy": args.policy, "kernel_ms_stamped": float(np.mean(walls)),
@@ -85,7 +94,11 @@ def main():
         col = d[:, k]
         out["phases"][name] = {"mean": float(col.mean()), "p95": float(np.percentile(col, 95)),
                                "max": float(col.max()), "share": float(col.sum() / total.sum())}
-    if N > 64:  # the workgroup kernel records no size statistics
+    if N > 64:  # grid diagnostics of the stamp build (flock_step_wg_c, slots 10..12)
+        g = np.concatenate(stats_wg)
+        out["grid"] = {"tile_candidates_per_body": float(g[:, 0].mean() / 1000),
+                       "bodies_walking_all_strips": float(g[:, 1].mean()),
+                       "strip_width": float((g[:, 2] & 0xFFFFFFFF).astype(np.uint32).view(np.float32).mean())}
         print(json.dumps(out, indent=1))
         if args.json:
             with open(args.json, "w") as f:
