@@ -68,10 +68,11 @@ struct WorldBuffers {
   unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
   float2* scratch;               // [E, tcap] list-order impulses (workgroup kernel only)
   // Workgroup path, split step (flock_step_wg_a -> flock_solve_wg -> flock_step_wg_c), per env:
-  float4* x_cst;                 // [E, tcap] island-ordered touching contacts (ab bits, nx, ny, 0)
-  float2* x_cimp;                // [E, tcap] their impulses (normal, tangent), island order
-  uint16_t* x_ord;               // [E, tcap] island order -> touching (list) rank
+  float4* x_cst;                 // [E, tcap] touching contacts in level order (ab bits, nx, ny, level << 16 | island)
+  float2* x_cimp;                // [E, tcap] their impulses (normal, tangent), level order
+  uint16_t* x_ord;               // [E, tcap] level order -> touching (list) rank
   uint16_t* x_ic;                // [E, IS]   island contact ranges (IS = N/2 + 2)
+  int32_t* x_nlvl;               // [E]       number of Gauss-Seidel levels (diagnostics)
   uint16_t* x_ib;                // [E, IS]   island body ranges
   uint16_t* x_ibod;              // [E, N]    island bodies
   int32_t* x_nisl;               // [E]

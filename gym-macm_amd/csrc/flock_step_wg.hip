@@ -33,7 +33,7 @@ constexpr int W = 64;
   do {                                                                  \
     __builtin_amdgcn_s_waitcnt(0);                                      \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();         \
-    if (tid == 0) B.stamps[(size_t)e * 16 + (k)] = _t;                  \
+    if (tid == 0) B.stamps[(size_t)e * 32 + (k)] = _t;                  \
   } while (0)
 #else
 #define WSTAMP(k) \
@@ -86,6 +86,19 @@ struct __align__(16) Rec {  // per-agent record for the pair sweep (48 B with fl
   float2 c;                // final position
 };
 
+
+// Inclusive prefix maximum over the 64 lanes of a wave in lane order, by DPP row shifts and row
+// broadcasts (no LDS crossbar round trips). Values must be > -2^30 (the identity used).
+__device__ __forceinline__ int wave_prefix_max(int v) {
+  constexpr int kId = -0x40000000;
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return v;
+}
 
 // Exclusive scan over the block in thread order; returns the block total.
 __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
@@ -284,7 +297,7 @@ __host__ __device__ inline WgLayoutA wg_layout_a(int N, int tcap) {
   L.scan = take(4 * 32);
   L.misc = take(4 * 8);
   L.tab = take(4 * tcap);
-  L.adj = take(4 * tcap);
+  L.adj = take(6 * tcap + 8);  // CSR edges (2 tcap u16), then level counts (tcap + 1 u32); levels (tcap u16) at 4 tcap + 8
   L.total = o;
   return L;
 }
@@ -320,7 +333,7 @@ __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
 
 __host__ __device__ inline int wg_isl_stride(int N) { return N / 2 + 2; }
 // solver LDS: velocities + positions (16 B per body), record/impulse/ab rings, big-island list
-__host__ __device__ inline int wg_solve_lds(int N) { return 16 * N + 2 * 64 * (16 + 8 + 4) + 4 * (64 + 1); }
+__host__ __device__ inline int wg_solve_lds(int N) { return 16 * N + 5 * wg_isl_stride(N) + 16; }
 
 template <typename OT>
 __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffers B, int cur, int tcap,
@@ -376,6 +389,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   }
   for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0;
   if (tid < 8) s_misc[tid] = 0;
+  WSTAMP(16);
 
   // ---- actions -> angle, force (mvmnt.py:97-129) ---------------------------------
   float Fx = 0.0f, Fy = 0.0f;
@@ -407,6 +421,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     Fy = 0.0f + Fy;
   }
   __syncthreads();
+  WSTAMP(17);
 
   // ---- Collide: ordered compaction of the touching contacts -----------------------
   const float rr = (P.radius + P.radius) * (P.radius + P.radius);
@@ -443,6 +458,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   }
   if (act) B.angle[ag] = ang;  // kernel C reads it for the observation
   __syncthreads();
+  WSTAMP(18);
 
   // ---- CSR touching edges, each body's segment in list (= Box2D edge) order ---------
 #define DEG_WORD(i) ((unsigned int*)(s_deg + ((i) & ~1)))
@@ -479,6 +495,11 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 #undef DEG_INC
 #undef DEG_GET
   __syncthreads();
+  // Gauss-Seidel levels are computed during the DFS (below): s_last[b] = 1 + level of the last
+  // contact, in island order, that touches body b (0 = none). s_deg is free from here on.
+  uint16_t* s_last = s_deg;
+  uint16_t* s_lvl = (uint16_t*)(lds + L.adj + 4 * tcap + 8);  // [tcap] level of island-ordered contact k
+  if (act) s_last[tid] = 0;
   if (act && deg > 1) {
     const int o0 = s_off[tid];
     for (int x = o0 + 1; x < o0 + deg; ++x) {
@@ -492,11 +513,16 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     }
   }
   __syncthreads();
+  WSTAMP(19);
 
   // ---- island DFS in Box2D order (as in flock_step_wg) ---------------------------------
+#ifdef MACM_AB_PAR_DFS_ALWAYS
+  const bool par_dfs = true;
+#else
   const bool par_dfs = 2 * T >= 4 * N;
+#endif
   if (!par_dfs && tid == 0) {
-    int nord = 0, nisl = 0, nb = 0;
+    int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
       const unsigned long long m = s_todo[w];
       if (m == 0ull) {
@@ -518,8 +544,15 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
           const uint32_t ab = s_tab[t];
           if (ab & 0x80000000u) continue;
           s_tab[t] = ab | 0x80000000u;
-          s_ord[nord++] = (uint16_t)t;
           const int a = ab & 0xffffu, bb = ab >> 16;
+          {  // level: 1 + the level of the last earlier contact touching a or bb
+            const int l = max((int)s_last[a], (int)s_last[bb]);
+            s_last[a] = (uint16_t)(l + 1);
+            s_last[bb] = (uint16_t)(l + 1);
+            s_lvl[nord] = (uint16_t)l;
+            dmax = max(dmax, l + 1);
+          }
+          s_ord[nord++] = (uint16_t)t;
           const int o = (a == b) ? bb : a;
           const unsigned long long ob = 1ull << (o & 63);
           const unsigned long long tw = s_todo[o >> 6];
@@ -533,11 +566,12 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     s_ic[nisl] = (uint16_t)nord;
     s_ib[nisl] = (uint16_t)nb;
     s_misc[0] = nisl;
+    s_misc[1] = dmax;
   }
   if (par_dfs && tid < W) {
     const int lane = tid;
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    int nord = 0, nisl = 0, nb = 0;
+    int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
       const unsigned long long m = s_todo[w];
       if (m == 0ull) {
@@ -559,6 +593,11 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
         if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
         ++nb;
         const int e0 = s_off[bdy], e1 = s_off[bdy + 1];
+        // Levels of the new contacts c_1..c_m of bdy, in order (all touch bdy; their other bodies
+        // o_i are distinct): with X_0 = s_last[bdy] and y_i = s_last[o_i], the serial rule
+        // X_i = max(X_{i-1}, y_i) + 1 gives X_i = i + max(X_0, max_{j<=i}(y_j - j + 1)),
+        // a prefix maximum over the lanes; level(c_i) = X_i - 1.
+        int xcur = s_last[bdy];
         for (int q0 = e0; q0 < e1; q0 += W) {
           const int q = q0 + lane;
           bool newc = false, push = false;
@@ -570,14 +609,25 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
             newc = !(ab & 0x80000000u);
           }
           const unsigned long long mc = __ballot(newc);
+          int rank = 0, z = -0x3fffffff;
           if (newc) {
             s_tab[t] = ab | 0x80000000u;
-            s_ord[nord + __popcll(mc & lt)] = (uint16_t)t;
+            rank = __popcll(mc & lt) + 1;
+            s_ord[nord + rank - 1] = (uint16_t)t;
             const int a = ab & 0xffffu, bb = ab >> 16;
             o = (a == bdy) ? bb : a;
             push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
+            z = (int)s_last[o] - rank + 1;
           }
-          nord += __popcll(mc);
+          z = wave_prefix_max(z);
+          if (newc) {
+            const int xi = rank + max(xcur, z);
+            s_last[o] = (uint16_t)xi;
+            s_lvl[nord + rank - 1] = (uint16_t)(xi - 1);
+          }
+          const int mnew = __popcll(mc);
+          if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
+          nord += mnew;
           const unsigned long long mp = __ballot(push);
           if (push) {
             atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
@@ -586,6 +636,9 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
           sp += __popcll(mp);
           __builtin_amdgcn_wave_barrier();
         }
+        if (lane == 0) s_last[bdy] = (uint16_t)xcur;
+        dmax = max(dmax, xcur);
+        __builtin_amdgcn_wave_barrier();
       }
       ++nisl;
     }
@@ -593,13 +646,47 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       s_ic[nisl] = (uint16_t)nord;
       s_ib[nisl] = (uint16_t)nb;
       s_misc[0] = nisl;
+      s_misc[1] = dmax;
     }
   }
   __syncthreads();
   const int nisl = s_misc[0];
+  WSTAMP(20);
   const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
 
-  // ---- integrate velocities; island-ordered contact records with normals -> HBM --------
+  // ---- Gauss-Seidel levels (computed by the DFS): level-order positions ----------------------
+  // Contacts of one level share no body, so kernel B solves a level's contacts at once and every
+  // body still sees Box2D's sequence of updates (b2ContactSolver walks the island in DFS order).
+  uint32_t* s_lst = (uint32_t*)(lds + L.adj);  // [levels + 1] counts, then starts (edges are dead)
+  const int nlvl = s_misc[1];
+  for (int q = tid; q <= nlvl; q += BS) s_lst[q] = 0u;
+  __syncthreads();
+  constexpr int kPer = 5;  // tcap <= 5 * blockDim: at most 5 contacts per thread
+  int slot[kPer];
+#pragma unroll
+  for (int m = 0; m < kPer; ++m) {
+    const int k = tid + m * BS;
+    slot[m] = k < nord ? (int)atomicAdd(&s_lst[s_lvl[k]], 1u) : 0;
+  }
+  __syncthreads();
+  {  // exclusive scan of the level counts in place; thread t owns levels [t*per, (t+1)*per)
+    const int per = (nlvl + BS - 1) / BS;
+    const int l0 = tid * per, l1 = min(nlvl, l0 + per);
+    int sum = 0;
+    for (int l = l0; l < l1; ++l) sum += (int)s_lst[l];
+    int run;
+    block_scan_excl(sum, run, s_scan);
+    for (int l = l0; l < l1; ++l) {
+      const int c = (int)s_lst[l];
+      s_lst[l] = (uint32_t)run;
+      run += c;
+    }
+    if (tid == 0) s_lst[nlvl] = (uint32_t)nord;
+  }
+  __syncthreads();
+  WSTAMP(21);
+
+  // ---- integrate velocities; level-ordered contact records with normals -> HBM ------------
   const int IS = wg_isl_stride(N);
   if (act) {
     const float vx = v.x + P.dt * (0.0f + P.inv_mass * Fx);
@@ -611,7 +698,10 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   float4* xc = B.x_cst + (size_t)e * tcap;
   float2* xi = B.x_cimp + (size_t)e * tcap;
   uint16_t* xo = B.x_ord + (size_t)e * tcap;
-  for (int k = tid; k < nord; k += BS) {
+#pragma unroll
+  for (int m = 0; m < kPer; ++m) {
+    const int k = tid + m * BS;
+    if (k >= nord) continue;
     const int t = s_ord[k];
     const uint32_t ab = s_tab[t] & 0x7fffffffu;
     const int a = ab & 0xffffu, b = ab >> 16;
@@ -623,10 +713,21 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       ny = pb.y - pa.y;
       normalize(nx, ny);
     }
-    xc[k] = make_float4(__uint_as_float(ab), nx, ny, 0.0f);
-    xi[k] = g_lam[t];
-    xo[k] = (uint16_t)t;
+    // the island of contact k (kernel B's per-island position-pass exit): binary search of the
+    // island contact ranges
+    int lo = 0, hi = nisl - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int)s_ic[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    const int lv = s_lvl[k];
+    const int pos = (int)s_lst[lv] + slot[m];
+    xc[pos] = make_float4(__uint_as_float(ab), nx, ny, __int_as_float((lv << 16) | lo));
+    xi[pos] = g_lam[t];
+    xo[pos] = (uint16_t)t;
   }
+  if (tid == 0) B.x_nlvl[e] = nlvl;
+  WSTAMP(22);
   for (int q = tid; q <= nisl; q += BS) {
     B.x_ic[(size_t)e * IS + q] = s_ic[q];
     B.x_ib[(size_t)e * IS + q] = s_ib[q];
@@ -692,29 +793,41 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
 
 }  // namespace wg
 
+__device__ __forceinline__ int sep_key(float f) {  // order-preserving int of a float (atomicMin)
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : (i ^ 0x7fffffff);
+}
+__device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0 ? k : (k ^ 0x7fffffff)); }
+
+// Kernel B: one wave per env solves all its islands together, level by level (kernel A's
+// Gauss-Seidel levels): a level's contacts touch disjoint bodies, so lanes solve them at once
+// and each body gets Box2D's sequence of updates (b2Island::Solve -> b2ContactSolver). The
+// passes are Box2D's: warm start, vel_iters velocity passes, StoreImpulses, position
+// integration, up to pos_iters position passes with each island leaving after the first pass
+// whose minimum separation is >= -3 linearSlop.
 __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
   const int e = blockIdx.x, lane = threadIdx.x, N = P.n_agents;
+  const int IS = wg_isl_stride(N);
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
-  float4* s_rr = (float4*)(s_c + N);               // [2][64] record ring (big islands)
-  float2* s_ri = (float2*)(s_rr + 2 * W);          // [2][64] impulse ring
-  uint32_t* s_ra = (uint32_t*)(s_ri + 2 * W);      // [2][64] ab ring (position passes)
-  int* s_big = (int*)(s_ra + 2 * W);               // [W] islands with >= kBig contacts, [W] = count
+  int* s_mins = (int*)(s_c + N);              // [IS] per island: minimum separation of the pass (key)
+  uint8_t* s_done = (uint8_t*)(s_mins + IS);  // [IS] per island: position-solved
   const size_t en = (size_t)e * N;
-  const int IS = wg_isl_stride(N);
-  const float4* cst = B.x_cst + (size_t)e * tcap;
-  const uint32_t* cab = (const uint32_t*)cst;  // .x of each record, stride 4 words
-  float2* cimp = B.x_cimp + (size_t)e * tcap;
-  const uint16_t* ic = B.x_ic + (size_t)e * IS;
   const int nisl = B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
+  const int nc = nisl > 0 ? (int)B.x_ic[(size_t)e * IS + nisl] : 0;
+  const int nch = (nc + W - 1) / W;
+  const float4* cst = B.x_cst + (size_t)e * tcap;
+  float2* cimp = B.x_cimp + (size_t)e * tcap;
+  const uint16_t* xord = B.x_ord + (size_t)e * tcap;
+  float2* g_lam = B.scratch + (size_t)e * tcap;
   for (int i = lane; i < N; i += W) {
     s_c[i] = B.pos[en + i];
     s_v[i] = B.x_vmid[en + i];
   }
-  if (lane == 0) s_big[W] = 0;
+  for (int I = lane; I < nisl; I += W) s_done[I] = 0;
   __syncthreads();
   const int tid = lane;  // for WSTAMP (slots 13..15, diagnostic build)
   (void)tid;
@@ -723,180 +836,78 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
   const float friction = P.friction;
 
-  // ---- warm start + velocity iterations, one lane per island ------------------------------------
-  // Islands of >= kBig contacts (dense worlds: one island of thousands) are set aside for the
-  // chunked path below; the rest run one lane per island.
-  constexpr int kBig = 128;
-  bool len_overflow = false;
-  for (int I = lane; I < nisl; I += W) {
-    const int c0 = ic[I], c1 = ic[I + 1];
-    const int len = c1 - c0;
-    if (len >= kBig) {  // solved below by the whole wave, one island at a time
-      const int slot = atomicAdd(&s_big[W], 1);
-      if (slot < W) s_big[slot] = I;
-      else len_overflow = true;
-    }
-    if (len >= kBig && !len_overflow) continue;
-    len_overflow = false;
-    if (len <= 2) {  // records and impulses in registers
-      const float4 r0 = cst[c0], r1 = len == 2 ? cst[c0 + 1] : r0;
-      float2 i0 = cimp[c0], i1 = len == 2 ? cimp[c0 + 1] : i0;
-      const uint32_t ab0 = __float_as_uint(r0.x), ab1 = __float_as_uint(r1.x);
-      const int a0 = ab0 & 0xffffu, b0 = ab0 >> 16, a1 = ab1 & 0xffffu, b1 = ab1 >> 16;
-      if (P.warm_starting) {
-        float2 va = s_v[a0], vb = s_v[b0];
-        gs_warm(va, vb, r0.y, r0.z, i0.x, i0.y, mA, mB);
-        s_v[a0] = va;
-        s_v[b0] = vb;
-        if (len == 2) {
-          va = s_v[a1];
-          vb = s_v[b1];
-          gs_warm(va, vb, r1.y, r1.z, i1.x, i1.y, mA, mB);
-          s_v[a1] = va;
-          s_v[b1] = vb;
-        }
-      }
-      for (int it = 0; it < P.vel_iters; ++it) {
-        float2 va = s_v[a0], vb = s_v[b0];
-        gs_velocity(va, vb, r0.y, r0.z, i0.x, i0.y, mA, mB, kmass, friction);
-        s_v[a0] = va;
-        s_v[b0] = vb;
-        if (len == 2) {
-          va = s_v[a1];
-          vb = s_v[b1];
-          gs_velocity(va, vb, r1.y, r1.z, i1.x, i1.y, mA, mB, kmass, friction);
-          s_v[a1] = va;
-          s_v[b1] = vb;
-        }
-      }
-      cimp[c0] = i0;
-      if (len == 2) cimp[c0 + 1] = i1;
-      continue;
-    }
-    if (P.warm_starting) {
-      float4 rn = cst[c0];
-      float2 in = cimp[c0];
-      for (int k = c0; k < c1; ++k) {
-        const float4 r = rn;
-        const float2 im = in;
-        if (k + 1 < c1) {
-          rn = cst[k + 1];
-          in = cimp[k + 1];
-        }
-        const uint32_t ab = __float_as_uint(r.x);
-        const int a = ab & 0xffffu, b = ab >> 16;
-        float2 va = s_v[a], vb = s_v[b];
-        gs_warm(va, vb, r.y, r.z, im.x, im.y, mA, mB);
-        s_v[a] = va;
-        s_v[b] = vb;
-      }
-    }
-    // Velocity passes flattened into one stream of nq = iters * len contact solves. The record
-    // for solve q + 2 is loaded at solve q; with len >= 3 it is a different contact from
-    // solves q and q + 1, so its impulses are final when loaded (their store came one pass
-    // earlier from this lane).
-    const int nq = P.vel_iters * len;
-    int k0 = c0, k1 = c0 + 1, k2 = c0 + 2;
-    float4 r0 = cst[k0], r1 = cst[k1], r2;
-    float2 i0 = cimp[k0], i1 = cimp[k1], i2;
-#define VSTEP(X, Y, Z)                                              \
-  {                                                                 \
-    if (q == nq) break;                                             \
-    k##Z = k##Y + 1 < c1 ? k##Y + 1 : c0;                           \
-    r##Z = cst[k##Z];                                               \
-    i##Z = cimp[k##Z];                                              \
-    const uint32_t ab = __float_as_uint(r##X.x);                    \
-    const int a = ab & 0xffffu, b = ab >> 16;                       \
-    float2 va = s_v[a], vb = s_v[b];                                \
-    gs_velocity(va, vb, r##X.y, r##X.z, i##X.x, i##X.y, mA, mB, kmass, friction); \
-    s_v[a] = va;                                                    \
-    s_v[b] = vb;                                                    \
-    cimp[k##X] = i##X;                                              \
-    ++q;                                                            \
-  }
-    for (int q = 0;;) {
-      VSTEP(0, 1, 2)
-      VSTEP(1, 2, 0)
-      VSTEP(2, 0, 1)
-    }
-#undef VSTEP
-  }
-  __syncthreads();
+  // The records are in level order (record.w = level << 16 | island). The wave walks them in
+  // chunks of 64, one record per lane, loaded a chunk ahead; inside a chunk it steps through the
+  // chunk's levels, the lanes of the current level solving together. A level that continues into
+  // the next chunk is finished there (its contacts share no body, so the split is harmless).
+  // Between level steps the next lanes must see this step's body updates: a wave's LDS accesses
+  // are performed in issue order, so waiting for its own LDS writes (lgkmcnt) is enough.
+  auto level_sync = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt / expcnt not waited
+    __builtin_amdgcn_wave_barrier();
+  };
+  // Chunk loads are branch-free (lanes past the end re-read the last record) and waited for
+  // explicitly at the end of the chunk before: the compiler then places no memory wait inside the
+  // level loop.
+  auto wait_vm = [&]() { __builtin_amdgcn_s_waitcnt(0x0f70); };  // vmcnt(0)
+  struct Slot {
+    float4 r;
+    float2 m;
+    int o;
+  };
+  auto load = [&](int c, Slot& x) {
+    const int k = min(c * W + lane, nc - 1);
+    x.r = cst[k];
+    x.m = cimp[k];
+    x.o = xord[k];
+  };
+  // a lane's level (past the end: a level no chunk walks) and the chunk's first / last level
+  auto chunk_levels = [&](int c, const Slot& x, int& mylv, int& lv0, int& lv1) {
+    mylv = c * W + lane < nc ? __float_as_int(x.r.w) >> 16 : 0x7fff;
+    const int last = min(W, nc - c * W) - 1;
+    lv0 = __builtin_amdgcn_readfirstlane(mylv);
+    lv1 = __builtin_amdgcn_readlane(mylv, last);
+  };
 
-  // Big islands, one at a time: the solve stream (warm-start pass, then vel_iters passes) is cut
-  // into chunks of 64 solves. The wave loads chunk c + 2 (one record per lane, coalesced) while
-  // lane 0 solves chunk c out of an LDS ring, and writes chunk c's impulses back after it. A
-  // contact recurs len >= kBig = 2 * 64 solves later, i.e. at least two chunks on, whose loads
-  // are issued after this chunk's write-back.
-  const int nbig = __builtin_amdgcn_readfirstlane(s_big[W] < W ? s_big[W] : W);
-  for (int bi = 0; bi < nbig; ++bi) {
-    const int I = __builtin_amdgcn_readfirstlane(s_big[bi]);
-    const int c0 = __builtin_amdgcn_readfirstlane((int)ic[I]);
-    const int c1 = __builtin_amdgcn_readfirstlane((int)ic[I + 1]);
-    const int len = c1 - c0;
-    const int nw = P.warm_starting ? len : 0;
-    const int ns = nw + P.vel_iters * len;
-    const int nch = (ns + W - 1) / W;
-    // contact of this lane's solve in chunk c: c0 + (64 c + lane) mod len, kept incrementally
-    int kl = c0 + lane % len;
-    float4 vr = cst[kl];
-    float2 vi = cimp[kl];
-    s_rr[lane] = vr;
-    s_ri[lane] = vi;
-    int kl1 = kl + W % len;
-    if (kl1 >= c1) kl1 -= len;
-    if (nch > 1) {
-      vr = cst[kl1];
-      vi = cimp[kl1];
-    }
-    __syncthreads();
+  // Warm start and velocity passes. last: the final impulses go straight to list order (g_lam).
+  auto vel_pass = [&](bool warm, bool last) {
+    if (nch == 0) return;
+    Slot cur, nxt;
+    load(0, cur);
+    wait_vm();
     for (int c = 0; c < nch; ++c) {
-      const int slot = (c & 1) * W;
-      if (lane == 0) {
-        const int s0 = c * W;
-        const int tn = ns - s0 < W ? ns - s0 : W;
-        for (int t = 0; t < tn; ++t) {
-          const float4 r = s_rr[slot + t];
-          const uint32_t ab = __float_as_uint(r.x);
-          const int a = ab & 0xffffu, b = ab >> 16;
+      load(c + 1, nxt);
+      int mylv, lv0, lv1;
+      chunk_levels(c, cur, mylv, lv0, lv1);
+      const uint32_t ab = __float_as_uint(cur.r.x);
+      const int a = ab & 0xffffu, b = ab >> 16;
+      float2 im = cur.m;
+      for (int lv = lv0; lv <= lv1; ++lv) {
+        if (mylv == lv) {
           float2 va = s_v[a], vb = s_v[b];
-          float2 im = s_ri[slot + t];
-          if (s0 + t < nw) {
-            gs_warm(va, vb, r.y, r.z, im.x, im.y, mA, mB);
-          } else {
-            gs_velocity(va, vb, r.y, r.z, im.x, im.y, mA, mB, kmass, friction);
-            s_ri[slot + t] = im;
-          }
+          if (warm) gs_warm(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB);
+          else gs_velocity(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB, kmass, friction);
           s_v[a] = va;
           s_v[b] = vb;
         }
+        level_sync();
       }
-      __syncthreads();
-      if (c * W + lane < ns) cimp[kl] = s_ri[slot + lane];  // this chunk's impulses back
-      int kl2 = kl1 + W % len;
-      if (kl2 >= c1) kl2 -= len;
-      if (c + 1 < nch) {  // ring <- chunk c + 1 (loaded a chunk ago), then load chunk c + 2
-        s_rr[(W - slot) + lane] = vr;
-        s_ri[(W - slot) + lane] = vi;
-        if (c + 2 < nch) {
-          vr = cst[kl2];
-          vi = cimp[kl2];
-        }
+      const int k = c * W + lane;
+      if (!warm && k < nc) {
+        if (last) g_lam[cur.o] = im;
+        else cimp[k] = im;
       }
-      kl = kl1;
-      kl1 = kl2;
-      __syncthreads();
+      wait_vm();
+      cur = nxt;
     }
-  }
+  };
+  if (P.warm_starting) vel_pass(true, false);
+  for (int it = 0; it < P.vel_iters; ++it) vel_pass(false, it + 1 == P.vel_iters);
+  if (P.vel_iters == 0)  // StoreImpulses of the (warm-started) impulses as they are
+    for (int k = lane; k < nc; k += W) g_lam[xord[k]] = cimp[k];
 
   WSTAMP(14);
-  // ---- StoreImpulses back in list order; integrate positions ----------------------------------
-  const int nord = nisl > 0 ? (int)ic[nisl] : 0;
-  {
-    const uint16_t* ord = B.x_ord + (size_t)e * tcap;
-    float2* g_lam = B.scratch + (size_t)e * tcap;
-    for (int k = lane; k < nord; k += W) g_lam[ord[k]] = cimp[k];
-  }
+  // ---- integrate positions ---------------------------------------------------------------------
   for (int i = lane; i < N; i += W) {
     const float2 vv = s_v[i];
     float vx = vv.x, vy = vv.y;
@@ -912,93 +923,52 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   }
   __syncthreads();
 
-  // ---- position iterations, one lane per island ---------------------------------------------
-  uint8_t* isolv = B.x_isolv + (size_t)e * IS;
-  for (int I = lane; I < nisl; I += W) {
-    const int c0 = ic[I], c1 = ic[I + 1];
-    if (c1 - c0 >= kBig) {
-      bool listed = false;
-      for (int q = 0; q < nbig; ++q) listed |= s_big[q] == I;
-      if (listed) continue;
-    }
-    int solved = 0;
-    uint32_t abn = cab[4 * c0];
-    for (int it = 0; it < P.pos_iters; ++it) {
-      float min_sep = 0.0f;
-      for (int k = c0; k < c1; ++k) {
-        const uint32_t ab = abn;
-        abn = cab[4 * (k + 1 < c1 ? k + 1 : c0)];
-        const int a = ab & 0xffffu, b = ab >> 16;
-        float2 ca = s_c[a], cb = s_c[b];
-        const float sep = gs_position(ca, cb, P.radius, mA, mB);
-        min_sep = bmin(min_sep, sep);
-        s_c[a] = ca;
-        s_c[b] = cb;
-      }
-      if (min_sep >= -3.0f * kLinearSlop) {
-        solved = 1;
-        break;
-      }
-    }
-    isolv[I] = (uint8_t)solved;
-  }
-  __syncthreads();
-  // Big islands: position passes (read-only records) through the same chunked ring; lane 0
-  // decides the early exit at each pass end.
-  for (int bi = 0; bi < nbig; ++bi) {
-    const int I = __builtin_amdgcn_readfirstlane(s_big[bi]);
-    const int c0 = __builtin_amdgcn_readfirstlane((int)ic[I]);
-    const int c1 = __builtin_amdgcn_readfirstlane((int)ic[I + 1]);
-    const int len = c1 - c0;
-    const int ns = P.pos_iters * len;
-    const int nch = (ns + W - 1) / W;
-    int kl = c0 + lane % len;
-    s_ra[lane] = cab[4 * kl];
-    int kl1 = kl + W % len;
-    if (kl1 >= c1) kl1 -= len;
-    uint32_t va = nch > 1 ? cab[4 * kl1] : 0u;
+  // ---- position passes: every island not yet solved, level by level; an island is solved after
+  //      the first pass whose minimum separation (starting at 0) is >= -3 linearSlop ------------
+  for (int it = 0; it < P.pos_iters; ++it) {
+    for (int I = lane; I < nisl; I += W) s_mins[I] = sep_key(0.0f);
     __syncthreads();
-    int solved = 0, done = 0;
-    float min_sep = 0.0f;
-    for (int c = 0; c < nch && !done; ++c) {
-      const int slot = (c & 1) * W;
-      if (lane == 0) {
-        const int s0 = c * W;
-        const int tn = ns - s0 < W ? ns - s0 : W;
-        int j = s0 % len;
-        for (int t = 0; t < tn; ++t) {
-          const uint32_t ab = s_ra[slot + t];
-          const int a = ab & 0xffffu, b = ab >> 16;
+    Slot cur, nxt;
+    if (nch > 0) load(0, cur);
+    wait_vm();
+    for (int c = 0; c < nch; ++c) {
+      load(c + 1, nxt);
+      int mylv, lv0, lv1;
+      chunk_levels(c, cur, mylv, lv0, lv1);
+      const int I = __float_as_int(cur.r.w) & 0xffff;
+      const uint32_t ab = __float_as_uint(cur.r.x);
+      const int a = ab & 0xffffu, b = ab >> 16;
+      const bool live = !s_done[I];
+      for (int lv = lv0; lv <= lv1; ++lv) {
+        if (live && mylv == lv) {
           float2 ca = s_c[a], cb = s_c[b];
           const float sep = gs_position(ca, cb, P.radius, mA, mB);
-          min_sep = bmin(min_sep, sep);
           s_c[a] = ca;
           s_c[b] = cb;
-          if (++j == len) {
-            j = 0;
-            if (min_sep >= -3.0f * kLinearSlop) {
-              solved = 1;
-              done = 1;
-              break;
-            }
-            min_sep = 0.0f;
-          }
+          atomicMin(&s_mins[I], sep_key(sep));
         }
+        level_sync();
       }
-      done = __builtin_amdgcn_readfirstlane(done);
-      int kl2 = kl1 + W % len;
-      if (kl2 >= c1) kl2 -= len;
-      if (!done && c + 1 < nch) {
-        s_ra[(W - slot) + lane] = va;
-        if (c + 2 < nch) va = cab[4 * kl2];
-      }
-      kl1 = kl2;
-      __syncthreads();
+      wait_vm();
+      cur = nxt;
     }
-    if (lane == 0) isolv[I] = (uint8_t)solved;
+    __syncthreads();
+    bool open = false;
+    for (int I = lane; I < nisl; I += W) {
+      if (s_done[I]) continue;
+      if (sep_unkey(s_mins[I]) >= -3.0f * kLinearSlop) s_done[I] = 1;
+      else open = true;
+    }
+    const bool any_open = __ballot(open) != 0ull;
+    __syncthreads();
+    if (!any_open) break;
   }
-  __syncthreads();
+  uint8_t* isolv = B.x_isolv + (size_t)e * IS;
+  for (int I = lane; I < nisl; I += W) isolv[I] = s_done[I];
   WSTAMP(15);
+#ifdef MACM_STAMPS
+  if (lane == 0) B.stamps[(size_t)e * 32 + 12] = (unsigned long long)B.x_nlvl[e] | ((unsigned long long)nc << 32);
+#endif
   for (int i = lane; i < N; i += W) B.x_cout[en + i] = s_c[i];
 }
 
@@ -1369,10 +1339,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   }
   WSTAMP(9);
 #ifdef MACM_STAMPS
-  if (tid == 0) {  // strip diagnostics: tile candidates per body (x1000), bodies walking all strips, strip width
-    B.stamps[(size_t)e * 16 + 10] = (unsigned long long)s_misc[2] * 1000ull / N;
-    B.stamps[(size_t)e * 16 + 11] = (unsigned long long)s_misc[3];
-    B.stamps[(size_t)e * 16 + 12] = (unsigned long long)__float_as_uint(G.par[2]);
+  if (tid == 0) {  // strip diagnostics: tile candidates per body (x1000), bodies walking all strips
+    B.stamps[(size_t)e * 32 + 10] = (unsigned long long)s_misc[2] * 1000ull / N;
+    B.stamps[(size_t)e * 32 + 11] = (unsigned long long)s_misc[3];
   }
 #endif
 }

@@ -337,13 +337,14 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       (rc = dalloc(w, &B.done, (size_t)n_envs)) || (rc = dalloc(w, &B.status, (size_t)n_envs)) ||
       (rc = dalloc(w, &B.env_counters, (size_t)n_envs * 4))
 #ifdef MACM_STAMPS
-      || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 16))
+      || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 32))
 #endif
       || (!w->wave && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap))) ||
       (!w->wave && ((rc = dalloc(w, &B.x_cst, (size_t)n_envs * w->tcap)) ||
                     (rc = dalloc(w, &B.x_cimp, (size_t)n_envs * w->tcap)) ||
                     (rc = dalloc(w, &B.x_ord, (size_t)n_envs * w->tcap)) ||
                     (rc = dalloc(w, &B.x_ic, (size_t)n_envs * (N / 2 + 2))) ||
+                    (rc = dalloc(w, &B.x_nlvl, (size_t)n_envs)) ||
                     (rc = dalloc(w, &B.x_ib, (size_t)n_envs * (N / 2 + 2))) ||
                     (rc = dalloc(w, &B.x_ibod, EN)) || (rc = dalloc(w, &B.x_nisl, (size_t)n_envs)) ||
                     (rc = dalloc(w, &B.x_vmid, EN)) || (rc = dalloc(w, &B.x_cout, EN)) ||
@@ -1034,11 +1035,12 @@ int macm_bots_combat(const void* obs, const uint8_t* mask, int32_t obs_f64, int3
 }
 
 #ifdef MACM_STAMPS
-// Diagnostic build only: copy the per-env phase stamps [E, 16] of the last step.
+// Diagnostic build only: copy the per-env phase stamps [E, 32] of the last step (the wave kernel
+// uses rows of 16).
 int macm_debug_stamps(macm_world* w, unsigned long long* out) {
   if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
   DeviceGuard g(w->device);
-  HIP_TRY(hipMemcpy(out, w->B.stamps, (size_t)w->P.n_envs * 16 * sizeof(unsigned long long),
+  HIP_TRY(hipMemcpy(out, w->B.stamps, (size_t)w->P.n_envs * 32 * sizeof(unsigned long long),
                     hipMemcpyDeviceToHost));
   return MACM_OK;
 }

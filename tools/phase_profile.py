@@ -31,6 +31,7 @@ PHASES = ["actions", "collide", "adjacency", "dfs+integrate+normals", "velocity_
 PHASES_C = ["oldc+sleep_clock", "island_sleep", "sync_fixtures", "grid_build", "pair_sweep+nearest",
             "new_pairs", "old_list", "reward+obs", "writeback"]
 PHASES_B = ["solve_velocity", "solve_position"]
+PHASES_A = ["A:actions", "A:collide", "A:csr+sort", "A:dfs+levels", "A:level_sort", "A:records"]
 PHASES_WG = ["loads+actions", "collide", "csr+sort", "dfs", "integrate+records", "velocity_solve",
              "impulses+integrate+position", "sleep", "sync_fixtures", "pairs+nearest", "list_build",
              "reward+obs+writeback"]
@@ -55,7 +56,7 @@ def main():
     vec = FlockVec(E, n_agents=[N], targets=targets, seed=0x6D61636D, device="cuda:0", start_spread=args.spread)
     gen = torch.Generator(device="cuda:0")
     gen.manual_seed(1)
-    buf = np.zeros((E, 16), np.uint64)
+    buf = np.zeros((E, 32), np.uint64)
     deltas, stats, walls, stats_wg = [], [], [], []
     for s in range(args.warmup + args.steps):
         if args.policy == "bots":
@@ -77,14 +78,16 @@ def main():
             if N > 64:
                 t = np.concatenate([buf[:, :10], buf[:, 13:16]], 1).astype(np.int64)
                 dd = np.diff(t, axis=1)
-                deltas.append(np.concatenate([dd[:, :9], dd[:, 10:]], 1))
+                da = np.diff(buf[:, 16:23].astype(np.int64), axis=1)
+                deltas.append(np.concatenate([da, dd[:, :9], dd[:, 10:]], 1))
             else:
-                t = buf[:, :14].astype(np.int64)
+                b16 = buf.reshape(-1)[:E * 16].reshape(E, 16)
+                t = b16[:, :14].astype(np.int64)
                 deltas.append(np.diff(t, axis=1))
-            stats.append(buf[:, 14:].copy())
+            stats.append(buf.reshape(-1)[:E * 16].reshape(E, 16)[:, 14:].copy())
             stats_wg.append(buf[:, 10:13].copy())
     d = np.concatenate(deltas)  # [steps*E, 13]
-    phases = PHASES if N <= 64 else PHASES_C + PHASES_B
+    phases = PHASES if N <= 64 else PHASES_A + PHASES_C + PHASES_B
     st = np.concatenate(stats)
     total = d.sum(axis=1)
     out = {"envs": E, "agents": N, "spread": args.spread, "policy": args.policy, "kernel_ms_stamped": float(np.mean(walls)),
@@ -98,7 +101,10 @@ def main():
         g = np.concatenate(stats_wg)
         out["grid"] = {"tile_candidates_per_body": float(g[:, 0].mean() / 1000),
                        "bodies_walking_all_strips": float(g[:, 1].mean()),
-                       "strip_width": float((g[:, 2] & 0xFFFFFFFF).astype(np.uint32).view(np.float32).mean())}
+                       "gs_levels_mean": float((g[:, 2] & 0xFFFFFFFF).mean()),
+                       "gs_levels_max": float((g[:, 2] & 0xFFFFFFFF).max()),
+                       "touching_mean": float((g[:, 2] >> 32).mean()),
+                       "touching_max": float((g[:, 2] >> 32).max())}
         print(json.dumps(out, indent=1))
         if args.json:
             with open(args.json, "w") as f:
