@@ -221,6 +221,23 @@ __device__ __forceinline__ float div_by_invariant(float n, float K) {
 #endif
 }
 
+// Inclusive prefix maximum over the 64 lanes of a wave in lane order, by DPP row shifts and row
+// broadcasts (no LDS crossbar round trips). Values must be > -2^30 (the identity used).
+__device__ __forceinline__ int wave_prefix_max(int v) {
+  constexpr int kId = -0x40000000;
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ int wave_max(int v) {  // over all 64 lanes, wave-uniform
+  return __builtin_amdgcn_readlane(wave_prefix_max(v), 63);
+}
+
 // Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).
 constexpr int kMtStride = 640;  // words per env: 624 state words, [624] = position
 

@@ -71,6 +71,18 @@ constexpr bool kMergeSingletons = false;
 #else
 constexpr bool kMergeSingletons = KREC > 1;
 #endif
+// Gauss-Seidel levels (T <= 64 touching contacts): the scalar DFS also gives each contact its
+// level, 1 + the level of the last earlier contact (island order) sharing a body with it; lane k
+// holds the k-th contact's record and the wave solves a level's contacts together (they share no
+// body, so every body keeps Box2D's sequence of updates). -DMACM_NO_LEVELS: the per-island lanes.
+#ifndef MACM_LEVELS_MIN_ISLAND  // the level path runs when an island has more contacts than this
+#define MACM_LEVELS_MIN_ISLAND 4
+#endif
+#ifdef MACM_NO_LEVELS
+constexpr bool kLevels = false;
+#else
+constexpr bool kLevels = true;
+#endif
 #ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
 #define MACM_PRIO2_T 3
 #endif
@@ -934,6 +946,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // Seeds in body-list order (reverse creation); bodies without touching
   // edges are singleton islands and contribute no contact order, so only
   // bodies in `hasdeg` are walked.
+  uint32_t ordv = 0u, lvlv = 0u, kislv = 0u;  // lane k: the k-th contact in island order, its level, island
+  bool lvl_path = kLevels && fast_dfs && T <= 64;  // narrowed after the DFS (largest island)
   if (fast_dfs) {
     // Wave-uniform (scalar) DFS: bodies' edge masks and contacts' pairs are read from the
     // owning lanes' registers (v_readlane), visited sets are 64-bit masks, and the outputs
@@ -944,7 +958,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     const uint32_t tabv1 = (TMW == 2 && 64 + lane < T) ? s_tab[64 + lane] : 0u;  // contact 64 + lane's
     const uint32_t tm_lo = (uint32_t)tmask, tm_hi = (uint32_t)(tmask >> 32);
     const uint32_t tm1_lo = (uint32_t)tmask1, tm1_hi = (uint32_t)(tmask1 >> 32);
-    uint32_t ordv = 0u, ordv1 = 0u, bodv = 0u, islv = 0u, icv = 0u, ibv = 0u, stk = 0u;
+    uint32_t ordv1 = 0u, bodv = 0u, islv = 0u, icv = 0u, ibv = 0u, stk = 0u;
     int nord = 0, nisl = 0, nb = 0;
     // one instantiation per width so that the common T <= 64 walk carries no second word
     auto dfs = [&](auto wide) {
@@ -970,9 +984,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
             m &= m - 1ull;
             if (!W2 || nord < 64) ordv = writelane_m0(base + t, nord, ordv);  // s_ord[nord]
             else ordv1 = writelane_m0(base + t, nord - 64, ordv1);
-            ++nord;
             const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tab, t);
             const int a = ab & 0xffffu, bb = ab >> 16;
+            ++nord;
             const int o = (a == b) ? bb : a;
             if ((vis >> o) & 1ull) continue;
             vis |= 1ull << o;
@@ -1088,7 +1102,81 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // any 2..KREC-contact island in this wave (wave-uniform; nisl <= ICAP < W, one island per lane)
   const int lsz = lane < nisl ? s_ic[lane + 1] - s_ic[lane] : 0;
   const bool krec_wave = kMergeSingletons && __builtin_amdgcn_ballot_w64(lsz >= 2 && lsz <= KREC) != 0ull;
-  for (int I = lane; I < nisl; I += W) {
+  // levels pay off once an island is longer than the register-record path takes (KREC): islands
+  // of up to KREC contacts run faster one lane each. Only then are the levels computed: a scalar
+  // walk of the contacts in island order (lane b of lastv: 1 + the level of the last contact
+  // touching body b).
+  lvl_path = lvl_path && __builtin_amdgcn_ballot_w64(lsz > MACM_LEVELS_MIN_ISLAND) != 0ull;
+  if (lvl_path) {
+    const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
+    uint32_t lastv = 0u;
+    for (int k = 0; k < T; ++k) {
+      const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
+      const int a = ab & 0xffffu, bb = ab >> 16;
+      const int l = max(__builtin_amdgcn_readlane(lastv, a), __builtin_amdgcn_readlane(lastv, bb));
+      lastv = writelane_m0(l + 1, a, lastv);
+      lastv = writelane_m0(l + 1, bb, lastv);
+      lvlv = writelane_m0(l, k, lvlv);
+    }
+    int isl = 0;  // island of contact `lane`: the islands whose first contact is at or before it
+    for (int I = 1; I < nisl; ++I) isl += (int)s_ic[I] <= lane ? 1 : 0;
+    kislv = (uint32_t)isl;
+  }
+  // level path: lane k holds contact k (island order) for the whole solve
+  const bool lhas = lvl_path && lane < T;
+  const int lvl = (int)lvlv, lisl = (int)kislv;
+  int dmulti = 0;  // levels of the islands with >= 2 contacts (0: only single-contact islands)
+  int lt_ = 0, la = 0, lb = 0;
+  float lnx = 0.0f, lny = 0.0f, lln = 0.0f, llt = 0.0f;
+  if (lvl_path) {
+    const int c0 = lhas ? (int)s_ic[lisl] : 0, c1 = lhas ? (int)s_ic[lisl + 1] : 0;
+    dmulti = wave_max(lhas && c1 - c0 >= 2 ? lvl + 1 : 0);
+    if (lhas) {
+      lt_ = (int)ordv;
+      const uint32_t ab = s_tab[lt_];
+      la = ab & 0xffffu;
+      lb = ab >> 16;
+      lnx = s_tnx[lt_];
+      lny = s_tny[lt_];
+      lln = s_tln[lt_];
+      llt = s_tlt[lt_];
+    }
+  }
+  // between level steps: this wave's own LDS writes done (LDS performs a wave's accesses in order)
+  auto level_sync = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (lvl_path && dmulti == 0) {  // single-contact islands only: every pass in registers
+    if (lhas) {
+      const float2 vA0 = s_v[la], vB0 = s_v[lb];
+      float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+      if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
+      for (int it = 0; it < P.vel_iters; ++it)
+        solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
+      s_v[la] = make_float2(vAx, vAy);
+      s_v[lb] = make_float2(vBx, vBy);
+    }
+  } else if (lvl_path) {
+    for (int it = P.warm_starting ? -1 : 0; it < P.vel_iters; ++it) {
+      for (int l = 0; l < dmulti; ++l) {
+        if (lhas && lvl == l) {
+          const float2 vA0 = s_v[la], vB0 = s_v[lb];
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+          if (it < 0) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
+          else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
+          s_v[la] = make_float2(vAx, vAy);
+          s_v[lb] = make_float2(vBx, vBy);
+        }
+        level_sync();
+      }
+    }
+  }
+  if (lhas) {
+    s_tln[lt_] = lln;
+    s_tlt[lt_] = llt;
+  }
+  for (int I = lvl_path ? W : lane; I < nisl; I += W) {
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
     if (c1 - c0 == 1 && !krec_wave) {
       const int t = s_ord[c0];
@@ -1207,7 +1295,59 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   STAMP(6);
 
   // ---- position iterations, one lane per island ------------------------------
-  for (int I = lane; I < nisl; I += W) {
+  if (lvl_path) {
+    // per island: the pass's minimum separation (order-preserving int keys); s_imin holds them
+    // until the island sleep decision below re-initialises it (one LDS array fewer keeps 17
+    // waves' LDS per CU: 4096 envs stay a single dispatch round with slack)
+    int* s_pmin = reinterpret_cast<int*>(s_imin);
+    if (dmulti == 0) {  // single-contact islands: lane k runs island k's passes in registers
+      if (lhas) {
+        int solved = 0;
+        const float2 cA0 = s_c[la], cB0 = s_c[lb];
+        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+        for (int it = 0; it < P.pos_iters; ++it) {
+          const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+          if (bmin(0.0f, sep) >= -3.0f * kLinearSlop) {
+            solved = 1;
+            break;
+          }
+        }
+        s_c[la] = make_float2(cAx, cAy);
+        s_c[lb] = make_float2(cBx, cBy);
+        s_isolved[lisl] = (uint8_t)solved;
+      }
+    } else {
+      // passes over the levels; an island leaves after the first pass whose minimum separation
+      // (from 0) is >= -3 linearSlop (b2Island::Solve)
+      const unsigned long long islm = nisl >= 64 ? ~0ull : ((1ull << nisl) - 1ull);
+      unsigned long long done = 0ull;
+      for (int it = 0; it < P.pos_iters && done != islm; ++it) {
+        if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
+        level_sync();
+        for (int l = 0; l < dmulti; ++l) {
+          if (lhas && lvl == l && !((done >> lisl) & 1ull)) {
+            const float2 cA0 = s_c[la], cB0 = s_c[lb];
+            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+            s_c[la] = make_float2(cAx, cAy);
+            s_c[lb] = make_float2(cBx, cBy);
+            // order-preserving int of the float for atomicMin
+            const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
+            atomicMin(&s_pmin[lisl], key);
+          }
+          level_sync();
+        }
+        int km = lane < nisl ? s_pmin[lane] : 0;
+        km = km >= 0 ? km : (km ^ 0x7fffffff);
+        done |= __builtin_amdgcn_ballot_w64(lane < nisl && !((done >> lane) & 1ull) &&
+                                            __int_as_float(km) >= -3.0f * kLinearSlop);
+      }
+      if (lane < nisl) s_isolved[lane] = (uint8_t)((done >> lane) & 1ull);
+    }
+    level_sync();
+    if (lane < nisl) s_imin[lane] = 0xffffffffu;  // island sleep decision below
+  }
+  for (int I = lvl_path ? W : lane; I < nisl; I += W) {
     s_imin[I] = 0xffffffffu;  // island sleep decision below
     const int c0 = s_ic[I], c1 = s_ic[I + 1];
     int solved = 0;

@@ -87,19 +87,6 @@ struct __align__(16) Rec {  // per-agent record for the pair sweep (48 B with fl
 };
 
 
-// Inclusive prefix maximum over the 64 lanes of a wave in lane order, by DPP row shifts and row
-// broadcasts (no LDS crossbar round trips). Values must be > -2^30 (the identity used).
-__device__ __forceinline__ int wave_prefix_max(int v) {
-  constexpr int kId = -0x40000000;
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return v;
-}
-
 // Exclusive scan over the block in thread order; returns the block total.
 __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
   const int tid = threadIdx.x, lane = tid & (W - 1), wid = tid / W, nw = blockDim.x / W;
