@@ -47,7 +47,15 @@
 namespace macm {
 
 constexpr int W = 64;       // wavefront = one env's agent lanes
-constexpr int TCAP = 256;   // touching contacts per env held in LDS (indices fit uint8)
+// touching contacts per env held in LDS (indices fit uint8); more take the spill step. With s_adj
+// aliased onto s_tm and the sweep records over s_tn + s_tab the Flock kernel needs 8.3 KB of LDS:
+// 19 waves per CU, so a 4096-env launch (16 per CU) has slack (at 16 per CU, -4% per step at M
+// and -7% in the bots closed loop; TCAP 224 fits 20 per CU but sends dense bots envs to the
+// spill step: profiles/r02/wave_levels)
+#ifndef MACM_TCAP
+#define MACM_TCAP 256
+#endif
+constexpr int TCAP = MACM_TCAP;
 constexpr int DEG = 16;     // touching contacts per body
 constexpr int ICAP = W / 2; // islands with >= 1 contact (>= 2 bodies each)
 constexpr int RCH = 2;      // list chunks (of 64 entries) cached in registers
@@ -591,8 +599,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   // The contact arrays in one block, which the spill step (flock_spill.hpp) reuses as its
   // per-body LDS when an env's touching contacts overflow TCAP / DEG.
   struct __align__(32) Pool {
-    // contact normals live until the velocity solve ends; the all-pairs records are
-    // written after it, so both share one LDS region
+    // contact normals live until the velocity solve ends and the pairs until the position
+    // solve ends; the all-pairs records are written after it over both
     float tn[2 * TCAP];
     uint32_t tab[TCAP];
     float tln[TCAP], tlt[TCAP];
@@ -608,10 +616,16 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   float* const s_tnx = s_tn;
   float* const s_tny = s_tn + TCAP;
   PairRec* const s_pj = reinterpret_cast<PairRec*>(s_tn);
-  static_assert(sizeof(PairRec) * W <= sizeof(float) * 2 * TCAP, "s_pj must fit in s_tn");
+  // s_pj spans s_tn and s_tab (adjacent in Pool): both are dead once the position solve ends
+  static_assert(offsetof(Pool, tab) == sizeof(float) * 2 * TCAP, "tab must follow tn");
+  static_assert(sizeof(PairRec) * W <= sizeof(float) * 2 * TCAP + sizeof(uint32_t) * TCAP, "s_pj must fit in s_tn + s_tab");
   uint32_t* const s_tm = s_pool.tm;
   uint32_t* const s_oldm = s_pool.oldm;
-  __shared__ uint8_t s_adj[W * DEG];
+  // per-body touching edges when T > 64 TMW (no scalar DFS); Flock: in s_tm's words, which only
+  // the scalar DFS reads
+  __shared__ uint8_t s_adj_tdm[kT ? W * DEG : 1];
+  uint8_t* const s_adj = kT ? s_adj_tdm : reinterpret_cast<uint8_t*>(s_pool.tm);
+  static_assert(kT || sizeof(uint32_t) * 2 * 2 * W >= W * DEG, "s_adj must fit in s_tm");
   __shared__ uint8_t s_ord[TCAP];
   __shared__ uint32_t s_cvis[TCAP / 32];
   __shared__ uint8_t s_deg[W], s_stack[W], s_ibodies[W], s_bisl[W];
