@@ -39,46 +39,57 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096):
-    """Time the CPU oracle on this host (OpenMP over envs) on a bounded sample of the
-    same workload: the same E envs x N agents, as many steps as fit the budget."""
+def _cpu_window(step_fn, acts, warmup, steps, budget_s):
+    """Run `warmup` untimed steps, then time up to `steps` steps (the GPU leg's window),
+    fewer if they would exceed the budget. Returns (timed steps, seconds, warmup run)."""
+    t0 = time.perf_counter()
+    step_fn(acts[0])
+    per_step = time.perf_counter() - t0
+    w_run = 1
+    for s in range(1, warmup):
+        if (s + 1) * per_step > budget_s:  # warm-up alone would exceed the budget
+            break
+        step_fn(acts[s % len(acts)])
+        w_run += 1
+    n = int(max(3, min(steps, budget_s / max(per_step, 1e-6))))
+    t0 = time.perf_counter()
+    for s in range(n):
+        step_fn(acts[(w_run + s) % len(acts)])
+    return n, time.perf_counter() - t0, w_run
+
+
+def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20, n_targets=1, tidx=None):
+    """Time the CPU oracle on this host (OpenMP over envs) on the same workload as the GPU
+    leg: the same E envs x N agents from reset, `warmup` untimed steps, then the GPU leg's
+    `steps` timed (fewer if they would exceed the budget)."""
     from oracle import OracleFlock
     from gym_macm.settings import flockSettings, to_config
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     E = n_envs
-    cfg = to_config(flockSettings(), n_agents, 1, obs_f64=True)
-    orc = OracleFlock(cfg, None, E, seed)
+    cfg = to_config(flockSettings(), n_agents, n_targets, obs_f64=True)
+    orc = OracleFlock(cfg, tidx, E, seed)
     rng = np.random.default_rng(seed + 1)
     bufs = dict(obs=np.zeros((E, n_agents, 4), np.float64), nbr_id=np.zeros((E, n_agents), np.int32),
                 reward=np.zeros((E, n_agents), np.float64))
-    pre = [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(8)]
-    t0 = time.perf_counter()
-    for a in pre[:3]:
-        orc.step_raw(a, bufs, threads)
-    per_step = (time.perf_counter() - t0) / 3
-    steps = int(max(5, budget_s / max(per_step, 1e-6)))
     acts = [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(16)]
-    t0 = time.perf_counter()
-    for s in range(steps):
-        orc.step_raw(acts[s % 16], bufs, threads)
-    dt = time.perf_counter() - t0
-    return dict(value=E * n_agents * steps / dt, unit="agent·steps/s", cores=threads, kind="port",
-                sample=f"oracle/ C restatement, {E} envs x {n_agents} agents x {steps} steps (after 3 "
-                       f"warm-up steps) from reset, uniform random discrete actions, OpenMP {threads} threads, "
-                       f"{dt:.1f} s")
+    n, dt, w_run = _cpu_window(lambda a: orc.step_raw(a, bufs, threads), acts, warmup, steps, budget_s)
+    return dict(value=E * n_agents * n / dt, unit="agent·steps/s", cores=threads, kind="port",
+                sample=f"oracle/ C restatement, {E} envs x {n_agents} agents, steps {w_run + 1}..{w_run + n} from "
+                       f"reset (the GPU leg times steps {warmup + 1}..{warmup + steps}), uniform random discrete "
+                       f"actions, OpenMP {threads} threads, {dt:.2f} s timed")
 
 
-def b_alg_tdm(n_agents):
-    """Algorithmic bytes per TDM agent-step (float32 obs): state r+w 2 x 40 (as Flock),
-    action 4, health/cd_atk/cd_mov f64 + alive u8 r+w 2 x 25, obs (N-1) x 16, mask N-1,
+def b_alg_tdm(n_agents, obs_f64=False):
+    """Algorithmic bytes per TDM agent-step: state r+w 2 x 40 (as Flock), action 4,
+    health/cd_atk/cd_mov f64 + alive u8 r+w 2 x 25, obs (N-1) x 16 (float64: x 32), mask N-1,
     health/alive outputs 9."""
-    return 80 + 4 + 50 + (n_agents - 1) * 16 + (n_agents - 1) + 9
+    return 80 + 4 + 50 + (n_agents - 1) * (32 if obs_f64 else 16) + (n_agents - 1) + 9
 
 
-def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0, n_envs=4096):
-    """Time the CPU TDM oracle (oracle/tdm_oracle.c, OpenMP over envs) on a bounded
-    sample of the same workload (same E envs, as many steps as fit the budget)."""
+def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20):
+    """Time the CPU TDM oracle (oracle/tdm_oracle.c, OpenMP over envs) on the GPU leg's window
+    (same E envs from reset, `warmup` untimed steps, then up to `steps` timed)."""
     from oracle import OracleTDM
     from gym_macm.tdm_world import tdm_config
 
@@ -88,19 +99,11 @@ def cpu_baseline_tdm(team_sizes, seed, budget_s=15.0, n_envs=4096):
     orc = OracleTDM(tdm_config(team_sizes, obs_f64=True), E, seed)
     rng = np.random.default_rng(seed + 1)
     acts = [tdm_random_actions_np(rng, E, N) for _ in range(16)]
-    t0 = time.perf_counter()
-    for a in acts[:3]:
-        orc.step(a, threads)
-    per_step = (time.perf_counter() - t0) / 3
-    steps = int(max(5, budget_s / max(per_step, 1e-6)))
-    t0 = time.perf_counter()
-    for s in range(steps):
-        orc.step(acts[s % 16], threads)
-    dt = time.perf_counter() - t0
-    return dict(value=E * N * steps / dt, unit="agent·steps/s", cores=threads, kind="port",
-                sample=f"oracle/ C restatement of TDM, {E} envs x {N} agents x {steps} steps (after 3 warm-up "
-                       f"steps) from reset, uniform random actions (attack p=0.5), OpenMP {threads} threads, "
-                       f"{dt:.1f} s")
+    n, dt, w_run = _cpu_window(lambda a: orc.step(a, threads), acts, warmup, steps, budget_s)
+    return dict(value=E * N * n / dt, unit="agent·steps/s", cores=threads, kind="port",
+                sample=f"oracle/ C restatement of TDM, {E} envs x {N} agents, steps {w_run + 1}..{w_run + n} from "
+                       f"reset (the GPU leg times steps {warmup + 1}..{warmup + steps}), uniform random actions "
+                       f"(attack p=0.5), OpenMP {threads} threads, {dt:.2f} s timed")
 
 
 def tdm_random_actions_np(rng, E, N):
@@ -134,6 +137,8 @@ def main():
     ap.add_argument("--policy", choices=("random", "bots"), default="random",
                     help="random: pre-generated uniform actions (the metric); bots: closed loop with the "
                          "device bots.flock / bots.combat kernels inside the timed region")
+    ap.add_argument("--obs-f64", action="store_true",
+                    help="float64 observations (the reference's own width, mvmnt.py:197-220); default float32")
     ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
     if args.traffic_json is None:
@@ -161,7 +166,7 @@ def main():
         N = args.agents
         targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
         vec = FlockVec(E, n_agents=[N], targets=targets, seed=args.seed, env_offset=gdist.env_offset(rank, E),
-                       device=dev)
+                       device=dev, obs_dtype=torch.float64 if args.obs_f64 else torch.float32)
         world_h = vec.world
         acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
         stride = E * N * 3
@@ -169,7 +174,7 @@ def main():
         from gym_macm.tdm_world import TdmWorld, tdm_config
         teams = [int(x) for x in args.teams.split(",")]
         N = sum(teams)
-        world_h = TdmWorld(tdm_config(teams), E, device=dev)
+        world_h = TdmWorld(tdm_config(teams, obs_f64=args.obs_f64), E, device=dev)
         world_h.reset(args.seed, gdist.env_offset(rank, E))
         acts = torch.randint(0, 3, (W + K, E, N, 4), dtype=torch.uint8, device=dev, generator=gen)
         acts[..., 3] = torch.randint(0, 2, (W + K, E, N), dtype=torch.uint8, device=dev, generator=gen)
@@ -227,7 +232,8 @@ def main():
     value = total_agent_steps / elapsed
 
     if rank == 0:
-        b_alg = B_ALG if args.env == "flock" else b_alg_tdm(N)
+        # float64 obs: the 4 obs values take 8 B each (Flock +16 B; TDM +16 B per observed agent)
+        b_alg = (B_ALG + (16 if args.obs_f64 else 0)) if args.env == "flock" else b_alg_tdm(N, args.obs_f64)
         achieved_gbs = b_alg * E * N / (kernel_ms * 1e-3) / 1e9
         ncap = 32 if N <= 32 else 64
         if args.env == "tdm":
@@ -241,6 +247,8 @@ def main():
                      else "flock_step_wg_a + flock_solve_wg + flock_step_wg_c<float>")
         traffic = None
         tj = load_traffic(args.traffic_json)
+        if args.obs_f64:
+            kname = kname.replace("float", "double")
         if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
                 and tj.get("policy", "random") == args.policy):
             traffic = tj.get("hbm_bytes_per_launch")
@@ -269,12 +277,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32",  # the physics; observations per config.obs
             "data": "synthetic",
             "config": {
                 "workload": workload,
                 "envs_per_gpu": E, "n_agents": N, "total_envs": E * world,
                 "parallelism": f"env-sharded x{world} (no data-path collective)",
+                "obs": "float64" if args.obs_f64 else "float32",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -292,9 +301,11 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
             if args.env == "flock":
-                out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget, E)
+                out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget, E, W, K,
+                                                   n_targets=args.flocks if args.flocks > 1 else 1,
+                                                   tidx=None if targets is None else np.asarray(targets, np.int32))
             else:
-                out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget, E)
+                out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget, E, W, K)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
