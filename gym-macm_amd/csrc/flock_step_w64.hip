@@ -324,6 +324,44 @@ __device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __r
   }
 }
 
+// The same slots in memory order: lane q of each pass writes slot q of the env's [N, N-1] block,
+// so one store instruction covers 64 consecutive slots (1 KB: whole 128-B lines; an env's block is
+// N (N-1) 16 B, a multiple of 128 B for N = 32) and the mask 64 consecutive bytes. Each slot
+// computes its own atan2 (no sharing between the two directions of a pair).
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_linear(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
+                                               unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                               const float* sa) {
+  const int S = N - 1, ns = N * S;
+  int i = lane / S, k = lane - i * S;  // slot q = i * S + k, advanced by 64 per pass
+  for (int q = lane; q < ns; q += W) {
+    const int j = k < i ? k : k + 1;
+    const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
+    double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
+    if (m) {
+      const float2 ci = sc[i], cj = sc[j];
+      const float rx = cj.x - ci.x, ry = cj.y - ci.y;
+      r = obs_sqrt<OT>(rx * rx + ry * ry);
+      t = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)sa[i]);
+      p = wrap_pi((double)sa[j] - (double)sa[i]);
+      ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
+    }
+    if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
+    if (mask) mask[q] = m ? 1 : 0;
+    k += W;
+    while (k >= S) {
+      k -= S;
+      ++i;
+    }
+  }
+}
+
+#ifdef MACM_TDM_OBS_LINEAR
+#define MACM_TDM_OBS tdm_obs_linear
+#else
+#define MACM_TDM_OBS tdm_obs_pairs
+#endif
+
 // b2ContactSolver, one circle contact (fixedRotation: no angular terms). Shared by
 // the LDS path and the single-contact register path, so both round identically.
 __device__ __forceinline__ void warm_start_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
@@ -1636,7 +1674,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     s_ang[lane] = ang;
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
-    tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+    MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
                      s_c, s_ang);
   }
   STAMP(12);
@@ -1864,7 +1902,7 @@ __global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, 
   const unsigned long long livem = __ballot(act);
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
-  tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+  MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
                    s_p, s_a);
   if (lane == 0) {
     B.ccount[cur][e] = total;
@@ -1899,7 +1937,7 @@ __global__ __launch_bounds__(W) void tdm_observe_w64(StepParams P, WorldBuffers 
   const unsigned long long livem = __ballot(live);
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
-  tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+  MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
                    s_p, s_a);
 }
 
