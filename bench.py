@@ -139,6 +139,9 @@ def main():
                          "device bots.flock / bots.combat kernels inside the timed region")
     ap.add_argument("--obs-f64", action="store_true",
                     help="float64 observations (the reference's own width, mvmnt.py:197-220); default float32")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo: host-side counters, ranks "
+                         "may share a GPU (multi-process test of the sharded path on a 1-GPU box)")
     ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
     if args.traffic_json is None:
@@ -148,13 +151,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and args.dist_backend == "nccl":
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif world > 1:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    red_dev = dev if args.dist_backend == "nccl" else None  # gloo reduces host tensors
 
     from gym_macm import dist as gdist
 
@@ -221,9 +228,9 @@ def main():
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / K  # per launch, on the launch stream
     # one small RCCL all-reduce of counters after the timed region (no data-path collective)
-    status = int(gdist.reduce_counters([world_h.status()], device=dev, op="max")[0])
-    cnt = gdist.reduce_counters(world_h.counters(), device=dev)
-    elapsed = gdist.reduce_max(elapsed, device=dev)
+    status = int(gdist.reduce_counters([world_h.status()], device=red_dev, op="max")[0])
+    cnt = gdist.reduce_counters(world_h.counters(), device=red_dev)
+    elapsed = gdist.reduce_max(elapsed, device=red_dev)
     total_agent_steps = world * E * N * K
     if args.env == "flock":
         assert int(cnt[0]) == total_agent_steps, (cnt, total_agent_steps)
@@ -282,7 +289,8 @@ def main():
             "config": {
                 "workload": workload,
                 "envs_per_gpu": E, "n_agents": N, "total_envs": E * world,
-                "parallelism": f"env-sharded x{world} (no data-path collective)",
+                "parallelism": f"env-sharded x{world} (no data-path collective)"
+                               + ("" if world == 1 or args.dist_backend == "nccl" else ", gloo counters (test mode)"),
                 "obs": "float64" if args.obs_f64 else "float32",
             },
             "roofline": {

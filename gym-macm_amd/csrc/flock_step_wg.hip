@@ -24,6 +24,11 @@ namespace macm {
 namespace wg {
 
 constexpr int W = 64;
+#ifdef MACM_NO_DFS_PRIORITY
+constexpr bool kDfsPriority = false;
+#else
+constexpr bool kDfsPriority = true;
+#endif
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
 // block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
@@ -508,6 +513,10 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 #else
   const bool par_dfs = 2 * T >= 4 * N;
 #endif
+  // The DFS is one latency chain on one wave while the block's other waves wait at the barrier
+  // and other blocks' waves share the SIMD: raise its issue priority for the walk (as the wave
+  // kernel does for its chain).
+  if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(3);
   if (!par_dfs && tid == 0) {
     int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
@@ -522,10 +531,21 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       s_ib[nisl] = (uint16_t)nb;
       int sp = 0;
       s_stk[sp++] = (uint16_t)s;
+      int top_b = -1, top_e0 = 0, top_e1 = 0;  // the last push of the previous pop (see par DFS)
       while (sp > 0) {
-        const int b = s_stk[--sp];
+        --sp;
+        int b, e0, e1;
+        if (top_b >= 0) {
+          b = top_b;
+          e0 = top_e0;
+          e1 = top_e1;
+        } else {
+          b = s_stk[sp];
+          e0 = s_off[b];
+          e1 = s_off[b + 1];
+        }
+        top_b = -1;
         s_ibod[nb++] = (uint16_t)b;
-        const int e0 = s_off[b], e1 = s_off[b + 1];
         for (int q = e0; q < e1; ++q) {
           const int t = s_adj[q];
           const uint32_t ab = s_tab[t];
@@ -543,9 +563,13 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
           const int o = (a == b) ? bb : a;
           const unsigned long long ob = 1ull << (o & 63);
           const unsigned long long tw = s_todo[o >> 6];
+          const int oe0 = s_off[o], oe1 = s_off[o + 1];
           if (!(tw & ob)) continue;
           s_todo[o >> 6] = tw & ~ob;
           s_stk[sp++] = (uint16_t)o;
+          top_b = o;
+          top_e0 = oe0;
+          top_e1 = oe1;
         }
       }
       ++nisl;
@@ -574,17 +598,32 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
         s_stk[0] = (uint16_t)sd;
       }
       int sp = 1;
+      // the top of the stack when the previous pop pushed (its last push), with its CSR range
+      // and level, read by the pushing lane alongside its other reads: the next pop then waits
+      // on no LDS read
+      int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;
       __builtin_amdgcn_wave_barrier();
       while (sp > 0) {
-        const int bdy = s_stk[--sp];
+        int bdy, e0, e1, xcur;
+        --sp;
+        if (top_b >= 0) {
+          bdy = top_b;
+          e0 = top_e0;
+          e1 = top_e1;
+          xcur = top_last;
+        } else {
+          bdy = s_stk[sp];
+          e0 = s_off[bdy];
+          e1 = s_off[bdy + 1];
+          xcur = s_last[bdy];
+        }
+        top_b = -1;
         if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
         ++nb;
-        const int e0 = s_off[bdy], e1 = s_off[bdy + 1];
         // Levels of the new contacts c_1..c_m of bdy, in order (all touch bdy; their other bodies
         // o_i are distinct): with X_0 = s_last[bdy] and y_i = s_last[o_i], the serial rule
         // X_i = max(X_{i-1}, y_i) + 1 gives X_i = i + max(X_0, max_{j<=i}(y_j - j + 1)),
         // a prefix maximum over the lanes; level(c_i) = X_i - 1.
-        int xcur = s_last[bdy];
         for (int q0 = e0; q0 < e1; q0 += W) {
           const int q = q0 + lane;
           bool newc = false, push = false;
@@ -596,7 +635,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
             newc = !(ab & 0x80000000u);
           }
           const unsigned long long mc = __ballot(newc);
-          int rank = 0, z = -0x3fffffff;
+          int rank = 0, z = -0x3fffffff, oe0 = 0, oe1 = 0, xi = 0;
           if (newc) {
             s_tab[t] = ab | 0x80000000u;
             rank = __popcll(mc & lt) + 1;
@@ -605,10 +644,12 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
             o = (a == bdy) ? bb : a;
             push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
             z = (int)s_last[o] - rank + 1;
+            oe0 = s_off[o];
+            oe1 = s_off[o + 1];
           }
           z = wave_prefix_max(z);
           if (newc) {
-            const int xi = rank + max(xcur, z);
+            xi = rank + max(xcur, z);
             s_last[o] = (uint16_t)xi;
             s_lvl[nord + rank - 1] = (uint16_t)(xi - 1);
           }
@@ -621,6 +662,13 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
             s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
           }
           sp += __popcll(mp);
+          if (mp) {  // the new top: the highest pushing lane
+            const int hl = 63 - __clzll(mp);
+            top_b = __builtin_amdgcn_readlane(o, hl);
+            top_e0 = __builtin_amdgcn_readlane(oe0, hl);
+            top_e1 = __builtin_amdgcn_readlane(oe1, hl);
+            top_last = __builtin_amdgcn_readlane(xi, hl);
+          }
           __builtin_amdgcn_wave_barrier();
         }
         if (lane == 0) s_last[bdy] = (uint16_t)xcur;
@@ -636,6 +684,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       s_misc[1] = dmax;
     }
   }
+  if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   const int nisl = s_misc[0];
   WSTAMP(20);
