@@ -24,6 +24,7 @@ namespace macm {
 namespace wg {
 
 constexpr int W = 64;
+constexpr int kNewSlots = 8;  // kernel C, all-pairs sweep: new partners kept per body (16 B of LDS)
 #ifdef MACM_NO_DFS_PRIORITY
 constexpr bool kDfsPriority = false;
 #else
@@ -1222,20 +1223,40 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       bj = s_bjv[tid];
     }
   } else if (act) {
+    // The new partners j > tid come out of this ascending sweep; the first kNewSlots of them go to
+    // this body's slots of an LDS scratch (the cells' entry array, unused on this path), so the
+    // list build below writes them back in descending order without a second sweep.
+    uint16_t* np = (uint16_t*)(lds + L.gent) + tid * kNewSlots;
+#ifdef MACM_WG_PACKED_SWEEP
+    // the AABB separations and the distance as packed pairs (v_pk_add / v_pk_mul: each lane of a
+    // packed op rounds as the scalar op)
+    typedef float fv2 __attribute__((ext_vector_type(2)));
+    const fv2 flo = {fn.x, fn.y}, fhi = {fn.z, fn.w}, cc2 = {cx, cy};
+#endif
 #pragma unroll 2
     for (int j = 0; j < N; ++j) {
       const float4 rfn = s_fn[j];
       const float2 rc = s_c[j];
+#ifdef MACM_WG_PACKED_SWEEP
+      const fv2 s1 = (fv2){rfn.x, rfn.y} - fhi, s2 = flo - (fv2){rfn.z, rfn.w};
+      const bool ovn = !(fmaxf(fmaxf(s1.x, s1.y), fmaxf(s2.x, s2.y)) > 0.0f);
+      const fv2 dv = (fv2){rc.x, rc.y} - cc2, dq = dv * dv;
+      const float d2 = dq.x + dq.y;
+#else
       const bool ovn = !(sep_max(fn, rfn) > 0.0f);
       const float dx = rc.x - cx, dy = rc.y - cy;
       const float d2 = dx * dx + dy * dy;
+#endif
       const bool other = j != tid;
       coll |= other && ovn;
       if (other && d2 < best) {
         best = d2;
         bj = j;
       }
-      if (j > tid && ovn && sep_max(fo, s_fo[j]) > 0.0f) ++newcnt;
+      if (j > tid && ovn && sep_max(fo, s_fo[j]) > 0.0f) {
+        if (newcnt < kNewSlots) np[newcnt] = (uint16_t)j;
+        ++newcnt;
+      }
     }
   }
   // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs ------------------------
@@ -1277,7 +1298,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           ocimp[w] = make_float2(0.0f, 0.0f);
         }
     }
-  } else if (act && newcnt > 0) {  // all-pairs (no cells, or more new pairs than the scratch holds)
+  } else if (act && newcnt > 0 && !gok && newcnt <= kNewSlots) {  // all-pairs: from the slots, reversed
+    const uint16_t* np = (const uint16_t*)(lds + L.gent) + tid * kNewSlots;
+    int w = nnew - excl - newcnt;
+    for (int t = newcnt - 1; t >= 0; --t, ++w)
+      if (w < C) {
+        ocab[w] = (uint32_t)tid | ((uint32_t)np[t] << 16);
+        ocimp[w] = make_float2(0.0f, 0.0f);
+      }
+  } else if (act && newcnt > 0) {  // more new pairs than the scratch holds: a descending sweep
     int w = nnew - excl - newcnt;
     for (int j = N - 1; j > tid; --j) {
       if (!(sep_max(fn, s_fn[j]) > 0.0f) && sep_max(fo, s_fo[j]) > 0.0f) {
