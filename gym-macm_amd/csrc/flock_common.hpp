@@ -221,6 +221,22 @@ __device__ __forceinline__ float div_by_invariant(float n, float K) {
 #endif
 }
 
+// Between the level steps of a one-wave Gauss-Seidel solve: the next step's lanes read the body
+// updates this step's lanes wrote to LDS. A wave's LDS accesses are performed in issue order, so
+// wavefront-scope release/acquire fences (no wait) are enough: the reads are issued after the
+// writes and cannot pass them. Waiting for the writes to complete (lgkmcnt(0), the round-2
+// first version: -DMACM_LEVEL_WAIT) adds an LDS round trip to every level step.
+__device__ __forceinline__ void wave_lds_sync() {
+#ifdef MACM_LEVEL_WAIT
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+  __builtin_amdgcn_wave_barrier();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
 // Inclusive prefix maximum over the 64 lanes of a wave in lane order, by DPP row shifts and row
 // broadcasts (no LDS crossbar round trips). Values must be > -2^30 (the identity used).
 __device__ __forceinline__ int wave_prefix_max(int v) {

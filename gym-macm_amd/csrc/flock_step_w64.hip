@@ -1194,11 +1194,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       llt = s_tlt[lt_];
     }
   }
-  // between level steps: this wave's own LDS writes done (LDS performs a wave's accesses in order)
-  auto level_sync = [&]() {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
-    __builtin_amdgcn_wave_barrier();
-  };
+  // between level steps: the next lanes see this step's LDS writes (wave_lds_sync)
+  auto level_sync = [&]() { wave_lds_sync(); };
   if (lvl_path && dmulti == 0) {  // single-contact islands only: every pass in registers
     if (lhas) {
       const float2 vA0 = s_v[la], vB0 = s_v[lb];

@@ -877,12 +877,9 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   // chunks of 64, one record per lane, loaded a chunk ahead; inside a chunk it steps through the
   // chunk's levels, the lanes of the current level solving together. A level that continues into
   // the next chunk is finished there (its contacts share no body, so the split is harmless).
-  // Between level steps the next lanes must see this step's body updates: a wave's LDS accesses
-  // are performed in issue order, so waiting for its own LDS writes (lgkmcnt) is enough.
-  auto level_sync = [&]() {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt / expcnt not waited
-    __builtin_amdgcn_wave_barrier();
-  };
+  // Between level steps the next lanes must see this step's body updates (wave_lds_sync: a wave's
+  // LDS accesses are performed in issue order).
+  auto level_sync = [&]() { wave_lds_sync(); };
   // Chunk loads are branch-free (lanes past the end re-read the last record) and waited for
   // explicitly at the end of the chunk before: the compiler then places no memory wait inside the
   // level loop.
