@@ -25,6 +25,16 @@ namespace wg {
 
 constexpr int W = 64;
 constexpr int kNewSlots = 8;  // kernel C, all-pairs sweep: new partners kept per body (16 B of LDS)
+// Kernel A's island DFS in sparse worlds (average touching degree < 4): the islands are found
+// first (union-find over the touching contacts, in parallel), each gets its contact and body
+// ranges from its size and seed order, and then one thread walks each island, all islands at
+// once, with the serial walk's code: the same order, levels and records as one thread walking
+// them all in turn. -DMACM_NO_ISLAND_DFS: thread 0 walks every island.
+#ifdef MACM_NO_ISLAND_DFS
+constexpr bool kIslandDfs = false;
+#else
+constexpr bool kIslandDfs = true;
+#endif
 #ifdef MACM_NO_DFS_PRIORITY
 constexpr bool kDfsPriority = false;
 #else
@@ -514,11 +524,123 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 #else
   const bool par_dfs = 2 * T >= 4 * N;
 #endif
+  // Sparse worlds: islands first, then one thread per island (see kIslandDfs).
+  const bool isl_dfs = kIslandDfs && !par_dfs && 2 * tcap >= 4 * N;
+  if (isl_dfs) {
+    // Union-find labels, hooking the lower root under the higher and jumping to the roots after
+    // every round, so each component's root is its highest body: the seed the serial walk would
+    // take (it seeds at the highest unvisited body with edges and consumes whole islands).
+    uint32_t* s_lab = (uint32_t*)(lds + L.ord);  // [N]; s_ord is written only by the walks
+    if (act) s_lab[tid] = (uint32_t)tid;
+    __syncthreads();
+    for (;;) {
+      bool hooked = false;
+      for (int t = tid; t < T; t += BS) {
+        const uint32_t ab = s_tab[t];
+        const uint32_t ra = s_lab[ab & 0xffffu], rb = s_lab[ab >> 16];
+        if (ra != rb) {
+          hooked = true;
+          if (ra < rb) atomicMax(&s_lab[ra], rb);
+          else atomicMax(&s_lab[rb], ra);
+        }
+      }
+      if (!__syncthreads_or(hooked)) break;
+      if (act) {  // labels only grow along a chain, so the walk ends at the root
+        uint32_t l = s_lab[tid], n;
+        while ((n = s_lab[l]) != l) l = n;
+        s_lab[tid] = l;
+      }
+      __syncthreads();
+    }
+    // islands in seed order = roots in descending order; rank per root in s_last (free until
+    // the walks), island sizes (contacts | bodies << 16) in s_stk, island seeds in s_ibod
+    uint32_t* s_isz = (uint32_t*)(lds + L.stk);
+    uint16_t* s_seed = s_ibod;
+    const bool root = act && deg > 0 && s_lab[tid] == (uint32_t)tid;
+    int rexcl;
+    const int nisl = block_scan_excl(root ? 1 : 0, rexcl, s_scan);
+    if (tid < nisl) s_isz[tid] = 0u;
+    if (root) {
+      const int I = nisl - 1 - rexcl;
+      s_last[tid] = (uint16_t)I;
+      s_seed[I] = (uint16_t)tid;
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += BS) atomicAdd(&s_isz[s_last[s_lab[s_tab[t] & 0xffffu]]], 1u);
+    if (act && deg > 0) atomicAdd(&s_isz[s_last[s_lab[tid]]], 1u << 16);
+    __syncthreads();
+    const uint32_t sz = tid < nisl ? s_isz[tid] : 0u;
+    const int seed = tid < nisl ? (int)s_seed[tid] : 0;
+    int off;
+    const int tot = block_scan_excl((int)sz, off, s_scan);  // contacts <= tcap, bodies <= N: no carry
+    if (tid < nisl) {
+      s_ic[tid] = (uint16_t)(off & 0xffff);
+      s_ib[tid] = (uint16_t)(off >> 16);
+    }
+    if (tid == 0) {
+      s_ic[nisl] = (uint16_t)(tot & 0xffff);
+      s_ib[nisl] = (uint16_t)(tot >> 16);
+      s_misc[0] = nisl;
+    }
+    if (act) s_last[tid] = 0;
+    __syncthreads();
+    if (tid < nisl) {
+      // the serial walk of island `tid` from its seed; its bodies, contacts and stack live in its
+      // own ranges, its bodies' todo bits share words with other islands' (atomicAnd)
+      int nord = off & 0xffff, nb = off >> 16, dmax = 0;
+      const int sb = nb;
+      int sp = sb;
+      atomicAnd(&s_todo[seed >> 6], ~(1ull << (seed & 63)));
+      s_stk[sp++] = (uint16_t)seed;
+      int top_b = -1, top_e0 = 0, top_e1 = 0;
+      while (sp > sb) {
+        --sp;
+        int b, e0, e1;
+        if (top_b >= 0) {
+          b = top_b;
+          e0 = top_e0;
+          e1 = top_e1;
+        } else {
+          b = s_stk[sp];
+          e0 = s_off[b];
+          e1 = s_off[b + 1];
+        }
+        top_b = -1;
+        s_ibod[nb++] = (uint16_t)b;
+        for (int q = e0; q < e1; ++q) {
+          const int t = s_adj[q];
+          const uint32_t ab = s_tab[t];
+          if (ab & 0x80000000u) continue;
+          s_tab[t] = ab | 0x80000000u;
+          const int a = ab & 0xffffu, bb = ab >> 16;
+          {
+            const int l = max((int)s_last[a], (int)s_last[bb]);
+            s_last[a] = (uint16_t)(l + 1);
+            s_last[bb] = (uint16_t)(l + 1);
+            s_lvl[nord] = (uint16_t)l;
+            dmax = max(dmax, l + 1);
+          }
+          s_ord[nord++] = (uint16_t)t;
+          const int o = (a == b) ? bb : a;
+          const unsigned long long ob = 1ull << (o & 63);
+          const unsigned long long tw = s_todo[o >> 6];
+          const int oe0 = s_off[o], oe1 = s_off[o + 1];
+          if (!(tw & ob)) continue;
+          atomicAnd(&s_todo[o >> 6], ~ob);
+          s_stk[sp++] = (uint16_t)o;
+          top_b = o;
+          top_e0 = oe0;
+          top_e1 = oe1;
+        }
+      }
+      atomicMax(&s_misc[1], dmax);
+    }
+  }
   // The DFS is one latency chain on one wave while the block's other waves wait at the barrier
   // and other blocks' waves share the SIMD: raise its issue priority for the walk (as the wave
   // kernel does for its chain).
   if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(3);
-  if (!par_dfs && tid == 0) {
+  if (!par_dfs && !isl_dfs && tid == 0) {
     int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
       const unsigned long long m = s_todo[w];
