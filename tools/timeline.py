@@ -40,7 +40,7 @@ def main():
     vec = FlockVec(E, n_agents=[N], seed=0x6D61636D, device="cuda:0")
     gen = torch.Generator(device="cuda:0")
     gen.manual_seed(1)
-    buf = np.zeros((E, 16), np.uint64)
+    buf = np.zeros((E, 32), np.uint64)  # macm_debug_stamps copies 32 words per env
     steps = []
     for s in range(args.warmup + args.steps):
         if args.policy == "bots":
@@ -57,7 +57,7 @@ def main():
         if s < args.warmup:
             continue
         _abi.check(L.macm_debug_stamps(vec.world.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))), "stamps")
-        b = buf.astype(np.int64)
+        b = buf.reshape(-1)[:E * 16].reshape(E, 16).astype(np.int64)  # the wave kernel's stride is 16
         rt0, c0, hw, rt1, c1 = b[:, 0], b[:, 1], b[:, 2], b[:, 3], b[:, 4]
         t0 = rt0 - rt0.min()
         life = c1 - c0
