@@ -250,6 +250,43 @@ __device__ __forceinline__ int wave_prefix_max(int v) {
   return v;
 }
 
+// Stores of the Flock step's per-agent outputs (obs, reward, neighbour id, collided): nontemporal
+// (the policy reads them, the step does not): driver window 34.0 -> 33.5 us, steady 21.6 -> 21.4 us
+// (profiles/r02/nt_stores). Not for TDM's [E, N, N-1, 4] obs: its 16-byte pair-tile stores then
+// stop combining in L2 (C4 32.3 -> 62.5 us). Nor for the state and contact list the next step
+// reads (no gain). A/B knobs: -DMACM_PLAIN_OUT, -DMACM_NT_STATE.
+template <int KIND, typename T>
+__device__ __forceinline__ void st_g(T* p, const T& v) {
+#ifdef MACM_NT_STATE
+  constexpr bool nt = true;
+#elif defined(MACM_PLAIN_OUT)
+  constexpr bool nt = false;
+#else
+  constexpr bool nt = KIND == 0;
+#endif
+  if constexpr (nt) {
+    if constexpr (sizeof(T) == 16) {
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      v4u x;
+      __builtin_memcpy(&x, &v, 16);
+      __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
+    } else if constexpr (sizeof(T) == 8) {
+      unsigned long long x;
+      __builtin_memcpy(&x, &v, 8);
+      __builtin_nontemporal_store(x, reinterpret_cast<unsigned long long*>(p));
+    } else if constexpr (sizeof(T) == 4) {
+      unsigned int x;
+      __builtin_memcpy(&x, &v, 4);
+      __builtin_nontemporal_store(x, reinterpret_cast<unsigned int*>(p));
+    } else {
+      __builtin_nontemporal_store(v, p);
+    }
+    return;
+  }
+  *p = v;
+}
+constexpr int kOut = 0, kState = 1;
+
 __device__ __forceinline__ int wave_max(int v) {  // over all 64 lanes, wave-uniform
   return __builtin_amdgcn_readlane(wave_prefix_max(v), 63);
 }

@@ -217,12 +217,10 @@ __device__ __forceinline__ void write_obs_row(OT* o, int coord, double r0, doubl
     o[4] = (OT)cos(t1);
     o[5] = (OT)sin(t1);
   } else if constexpr (sizeof(OT) == 4) {
-    *reinterpret_cast<float4*>(o) = make_float4((float)r0, (float)t0, (float)r1, (float)t1);
+    st_g<kOut>(reinterpret_cast<float4*>(o), make_float4((float)r0, (float)t0, (float)r1, (float)t1));
   } else {
-    o[0] = (OT)r0;
-    o[1] = (OT)t0;
-    o[2] = (OT)r1;
-    o[3] = (OT)t1;
+    st_g<kOut>(reinterpret_cast<double2*>(o), make_double2(r0, t0));
+    st_g<kOut>(reinterpret_cast<double2*>(o) + 1, make_double2(r1, t1));
   }
 }
 
@@ -594,8 +592,8 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
     const int j = 63 - __clzll(m);
     m &= ~(1ull << j);
     if (w < C) {
-      ocab[w] = (uint32_t)lane | ((uint32_t)j << 16);
-      ocimp[w] = make_float2(0.0f, 0.0f);
+      st_g<kState>(ocab + w, (uint32_t)lane | ((uint32_t)j << 16));
+      st_g<kState>(ocimp + w, make_float2(0.0f, 0.0f));
     }
     ++w;
   }
@@ -1611,8 +1609,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       if (w < C) {
         float2 l = make_float2(0.0f, 0.0f);
         if (touch && trank < TCAP) l = make_float2(s_tln[trank], s_tlt[trank]);
-        ocab[w] = ab;
-        ocimp[w] = l;
+        st_g<kState>(ocab + w, ab);
+        st_g<kState>(ocimp + w, l);
       }
     }
   }
@@ -1633,9 +1631,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       if (coll) rew = -1.0f;
       else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
       else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
-      rew_out[ag] = rew;
-      if (coll_out) coll_out[ag] = coll ? 1 : 0;
-      if (nbr_out) nbr_out[ag] = bj;
+      st_g<kOut>(rew_out + ag, rew);
+      if (coll_out) st_g<kOut>(coll_out + ag, (uint8_t)(coll ? 1 : 0));
+      if (nbr_out) st_g<kOut>(nbr_out + ag, (int32_t)bj);
       if (obs) {
         const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
         const float2 cn = s_c[bj];
@@ -1643,11 +1641,11 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         write_obs<OT>(obs + ag * od, P.coord, ang, best, rx, ry, tdx, tdy, td2);
       }
       // ---- state write-back ----
-      B.pos[ag] = make_float2(cx, cy);
-      B.vel[ag] = make_float2(vx, vy);
-      B.angle[ag] = ang;
-      B.fat[ag] = fn;
-      B.sleep[ag] = ns;
+      st_g<kState>(B.pos + ag, make_float2(cx, cy));
+      st_g<kState>(B.vel + ag, make_float2(vx, vy));
+      st_g<kState>(B.angle + ag, ang);
+      st_g<kState>(B.fat + ag, fn);
+      st_g<kState>(B.sleep + ag, ns);
     }
   } else {
     // ---- TDM state write-back + TDM.get_obs (combat.py:166-167, 206-227) -------
