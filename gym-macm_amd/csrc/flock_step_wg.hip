@@ -7,9 +7,10 @@
 //   * ordered compaction of the contact list by block-wide scans;
 //   * touching edges as CSR (counts -> scan -> LDS-atomic fill -> per-body
 //     insertion sort back into list order), no per-body degree cap;
-//   * island DFS serial on thread 0 over a bitmask of bodies with edges, then
-//     the touching contacts are permuted into island order so every Gauss-Seidel
-//     sweep reads consecutive records (one lane per island, as in Box2D);
+//   * island DFS in Box2D order: sparse worlds find the islands first (union-find)
+//     and walk them one thread per island, dense ones walk a popped body's edges
+//     wave-parallel; the touching contacts are then written in Gauss-Seidel level
+//     order for the solver;
 //   * all-pairs sweep over per-agent records in LDS (broadcast reads); new
 //     contacts = Ov(F_t) \ Ov(F_{t-1}) by testing the old fat AABBs, counted per
 //     agent then written in descending (a, b) order after a descending scan.
