@@ -30,7 +30,12 @@ constexpr int kNewSlots = 8;  // kernel C, all-pairs sweep: new partners kept pe
 // first (union-find over the touching contacts, in parallel), each gets its contact and body
 // ranges from its size and seed order, and then one thread walks each island, all islands at
 // once, with the serial walk's code: the same order, levels and records as one thread walking
-// them all in turn. -DMACM_NO_ISLAND_DFS: thread 0 walks every island.
+// them all in turn. -DMACM_NO_ISLAND_DFS: thread 0 walks every island. Islands of more than
+// kBigIsland contacts get a whole wave each (the dense path's wave-parallel walk).
+#ifndef MACM_BIG_ISLAND
+#define MACM_BIG_ISLAND 48
+#endif
+constexpr int kBigIsland = MACM_BIG_ISLAND;
 #ifdef MACM_NO_ISLAND_DFS
 constexpr bool kIslandDfs = false;
 #else
@@ -525,6 +530,94 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 #else
   const bool par_dfs = 2 * T >= 4 * N;
 #endif
+  // One island walked by a whole wave from seed sd (its todo bit already cleared): a popped
+  // body's edges one per lane, levels by a prefix maximum (below). Appends to s_ord / s_lvl at
+  // nord and s_ibod at nb; the stack lives at s_stk[sbase...]. Every lane of the wave calls it.
+  auto par_walk = [&](int sd, int& nord, int& nb, int sbase, int& dmax) {
+    const int lane = tid & (W - 1);
+    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint16_t* stk = s_stk + sbase;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) stk[0] = (uint16_t)sd;
+    int sp = 1;
+    // the top of the stack when the previous pop pushed (its last push), with its CSR range
+    // and level, read by the pushing lane alongside its other reads: the next pop then waits
+    // on no LDS read
+    int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;
+    __builtin_amdgcn_wave_barrier();
+    while (sp > 0) {
+      int bdy, e0, e1, xcur;
+      --sp;
+      if (top_b >= 0) {
+        bdy = top_b;
+        e0 = top_e0;
+        e1 = top_e1;
+        xcur = top_last;
+      } else {
+        bdy = stk[sp];
+        e0 = s_off[bdy];
+        e1 = s_off[bdy + 1];
+        xcur = s_last[bdy];
+      }
+      top_b = -1;
+      if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
+      ++nb;
+      // Levels of the new contacts c_1..c_m of bdy, in order (all touch bdy; their other bodies
+      // o_i are distinct): with X_0 = s_last[bdy] and y_i = s_last[o_i], the serial rule
+      // X_i = max(X_{i-1}, y_i) + 1 gives X_i = i + max(X_0, max_{j<=i}(y_j - j + 1)),
+      // a prefix maximum over the lanes; level(c_i) = X_i - 1.
+      for (int q0 = e0; q0 < e1; q0 += W) {
+        const int q = q0 + lane;
+        bool newc = false, push = false;
+        int t = 0, o = 0;
+        uint32_t ab = 0u;
+        if (q < e1) {
+          t = s_adj[q];
+          ab = s_tab[t];
+          newc = !(ab & 0x80000000u);
+        }
+        const unsigned long long mc = __ballot(newc);
+        int rank = 0, z = -0x3fffffff, oe0 = 0, oe1 = 0, xi = 0;
+        if (newc) {
+          s_tab[t] = ab | 0x80000000u;
+          rank = __popcll(mc & lt) + 1;
+          s_ord[nord + rank - 1] = (uint16_t)t;
+          const int a = ab & 0xffffu, bb = ab >> 16;
+          o = (a == bdy) ? bb : a;
+          push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
+          z = (int)s_last[o] - rank + 1;
+          oe0 = s_off[o];
+          oe1 = s_off[o + 1];
+        }
+        z = wave_prefix_max(z);
+        if (newc) {
+          xi = rank + max(xcur, z);
+          s_last[o] = (uint16_t)xi;
+          s_lvl[nord + rank - 1] = (uint16_t)(xi - 1);
+        }
+        const int mnew = __popcll(mc);
+        if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
+        nord += mnew;
+        const unsigned long long mp = __ballot(push);
+        if (push) {
+          atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
+          stk[sp + __popcll(mp & lt)] = (uint16_t)o;
+        }
+        sp += __popcll(mp);
+        if (mp) {  // the new top: the highest pushing lane
+          const int hl = 63 - __clzll(mp);
+          top_b = __builtin_amdgcn_readlane(o, hl);
+          top_e0 = __builtin_amdgcn_readlane(oe0, hl);
+          top_e1 = __builtin_amdgcn_readlane(oe1, hl);
+          top_last = __builtin_amdgcn_readlane(xi, hl);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) s_last[bdy] = (uint16_t)xcur;
+      dmax = max(dmax, xcur);
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
   // Sparse worlds: islands first, then one thread per island (see kIslandDfs).
   const bool isl_dfs = kIslandDfs && !par_dfs && 2 * tcap >= 4 * N;
   if (isl_dfs) {
@@ -534,7 +627,14 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     uint32_t* s_lab = (uint32_t*)(lds + L.ord);  // [N]; s_ord is written only by the walks
     if (act) s_lab[tid] = (uint32_t)tid;
     __syncthreads();
+#ifdef MACM_STAMPS
+    const unsigned long long lab_t0 = __builtin_amdgcn_s_memtime();
+    int lab_rounds = 0;
+#endif
     for (;;) {
+#ifdef MACM_STAMPS
+      ++lab_rounds;
+#endif
       bool hooked = false;
       for (int t = tid; t < T; t += BS) {
         const uint32_t ab = s_tab[t];
@@ -553,6 +653,12 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       }
       __syncthreads();
     }
+#ifdef MACM_STAMPS
+    if (tid == 0) {  // diagnostics: labeling cycles and rounds (tools/phase_profile.py)
+      B.stamps[(size_t)e * 32 + 24] = __builtin_amdgcn_s_memtime() - lab_t0;
+      B.stamps[(size_t)e * 32 + 25] = (unsigned long long)lab_rounds;
+    }
+#endif
     // islands in seed order = roots in descending order; rank per root in s_last (free until
     // the walks), island sizes (contacts | bodies << 16) in s_stk, island seeds in s_ibod
     uint32_t* s_isz = (uint32_t*)(lds + L.stk);
@@ -584,11 +690,34 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       s_misc[0] = nisl;
     }
     if (act) s_last[tid] = 0;
-    __syncthreads();
+    // Islands of more than kBigIsland contacts are walked by a whole wave each (par_walk), the
+    // rest one per thread of the other waves. Work list (seed, contact | body offsets) in s_lab's
+    // words (the labels are dead): the wave-walked islands first. nbw leaves a thread per island.
+    const int nw = BS / W, wid = tid / W;
+    const bool big = tid < nisl && (int)(sz & 0xffffu) > kBigIsland;
+    int bexcl;
+    const int nbig = block_scan_excl(big ? 1 : 0, bexcl, s_scan);
+    const int nbw = min(nbig, min(nw - 1, (BS - nisl) / W));
+    uint2* s_work = (uint2*)(lds + L.ord);
     if (tid < nisl) {
-      // the serial walk of island `tid` from its seed; its bodies, contacts and stack live in its
+      const bool wv = big && bexcl < nbw;
+      s_work[wv ? bexcl : nbw + tid - min(bexcl, nbw)] = make_uint2((uint32_t)seed, (uint32_t)off);
+    }
+    __syncthreads();
+    const int slot = wid < nbw ? wid : nbw + tid - nbw * W;
+    const uint2 job = slot < nisl ? s_work[slot] : make_uint2(0u, 0u);
+    __syncthreads();
+    if (wid < nbw) {
+      const int sd = (int)job.x;
+      int nord = (int)(job.y & 0xffffu), nb = (int)(job.y >> 16), dmax = 0;
+      if ((tid & (W - 1)) == 0) atomicAnd(&s_todo[sd >> 6], ~(1ull << (sd & 63)));
+      par_walk(sd, nord, nb, nb, dmax);
+      if ((tid & (W - 1)) == 0) atomicMax(&s_misc[1], dmax);
+    } else if (slot < nisl) {
+      // the serial walk of island `slot` from its seed; its bodies, contacts and stack live in its
       // own ranges, its bodies' todo bits share words with other islands' (atomicAnd)
-      int nord = off & 0xffff, nb = off >> 16, dmax = 0;
+      const int seed = (int)job.x;
+      int nord = (int)(job.y & 0xffffu), nb = (int)(job.y >> 16), dmax = 0;
       const int sb = nb;
       int sp = sb;
       atomicAnd(&s_todo[seed >> 6], ~(1ull << (seed & 63)));
@@ -704,8 +833,6 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     s_misc[1] = dmax;
   }
   if (par_dfs && tid < W) {
-    const int lane = tid;
-    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
       const unsigned long long m = s_todo[w];
@@ -715,92 +842,15 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       }
       const int sd = w * 64 + 63 - __clzll(m);
       __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
+      if (tid == 0) {
         s_todo[w] = m & ~(1ull << (sd & 63));
         s_ic[nisl] = (uint16_t)nord;
         s_ib[nisl] = (uint16_t)nb;
-        s_stk[0] = (uint16_t)sd;
       }
-      int sp = 1;
-      // the top of the stack when the previous pop pushed (its last push), with its CSR range
-      // and level, read by the pushing lane alongside its other reads: the next pop then waits
-      // on no LDS read
-      int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;
-      __builtin_amdgcn_wave_barrier();
-      while (sp > 0) {
-        int bdy, e0, e1, xcur;
-        --sp;
-        if (top_b >= 0) {
-          bdy = top_b;
-          e0 = top_e0;
-          e1 = top_e1;
-          xcur = top_last;
-        } else {
-          bdy = s_stk[sp];
-          e0 = s_off[bdy];
-          e1 = s_off[bdy + 1];
-          xcur = s_last[bdy];
-        }
-        top_b = -1;
-        if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
-        ++nb;
-        // Levels of the new contacts c_1..c_m of bdy, in order (all touch bdy; their other bodies
-        // o_i are distinct): with X_0 = s_last[bdy] and y_i = s_last[o_i], the serial rule
-        // X_i = max(X_{i-1}, y_i) + 1 gives X_i = i + max(X_0, max_{j<=i}(y_j - j + 1)),
-        // a prefix maximum over the lanes; level(c_i) = X_i - 1.
-        for (int q0 = e0; q0 < e1; q0 += W) {
-          const int q = q0 + lane;
-          bool newc = false, push = false;
-          int t = 0, o = 0;
-          uint32_t ab = 0u;
-          if (q < e1) {
-            t = s_adj[q];
-            ab = s_tab[t];
-            newc = !(ab & 0x80000000u);
-          }
-          const unsigned long long mc = __ballot(newc);
-          int rank = 0, z = -0x3fffffff, oe0 = 0, oe1 = 0, xi = 0;
-          if (newc) {
-            s_tab[t] = ab | 0x80000000u;
-            rank = __popcll(mc & lt) + 1;
-            s_ord[nord + rank - 1] = (uint16_t)t;
-            const int a = ab & 0xffffu, bb = ab >> 16;
-            o = (a == bdy) ? bb : a;
-            push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
-            z = (int)s_last[o] - rank + 1;
-            oe0 = s_off[o];
-            oe1 = s_off[o + 1];
-          }
-          z = wave_prefix_max(z);
-          if (newc) {
-            xi = rank + max(xcur, z);
-            s_last[o] = (uint16_t)xi;
-            s_lvl[nord + rank - 1] = (uint16_t)(xi - 1);
-          }
-          const int mnew = __popcll(mc);
-          if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
-          nord += mnew;
-          const unsigned long long mp = __ballot(push);
-          if (push) {
-            atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
-            s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
-          }
-          sp += __popcll(mp);
-          if (mp) {  // the new top: the highest pushing lane
-            const int hl = 63 - __clzll(mp);
-            top_b = __builtin_amdgcn_readlane(o, hl);
-            top_e0 = __builtin_amdgcn_readlane(oe0, hl);
-            top_e1 = __builtin_amdgcn_readlane(oe1, hl);
-            top_last = __builtin_amdgcn_readlane(xi, hl);
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-        if (lane == 0) s_last[bdy] = (uint16_t)xcur;
-        dmax = max(dmax, xcur);
-        __builtin_amdgcn_wave_barrier();
-      }
+      par_walk(sd, nord, nb, 0, dmax);
       ++nisl;
     }
+    const int lane = tid;
     if (lane == 0) {
       s_ic[nisl] = (uint16_t)nord;
       s_ib[nisl] = (uint16_t)nb;

@@ -85,7 +85,7 @@ def main():
                 t = b16[:, :14].astype(np.int64)
                 deltas.append(np.diff(t, axis=1))
             stats.append(buf.reshape(-1)[:E * 16].reshape(E, 16)[:, 14:].copy())
-            stats_wg.append(buf[:, 10:13].copy())
+            stats_wg.append(np.concatenate([buf[:, 10:13], buf[:, 24:26]], 1).copy())
     d = np.concatenate(deltas)  # [steps*E, 13]
     phases = PHASES if N <= 64 else PHASES_A + PHASES_C + PHASES_B
     st = np.concatenate(stats)
@@ -105,6 +105,11 @@ def main():
                        "gs_levels_max": float((g[:, 2] & 0xFFFFFFFF).max()),
                        "touching_mean": float((g[:, 2] >> 32).mean()),
                        "touching_max": float((g[:, 2] >> 32).max())}
+        isl = g[:, 4] > 0  # envs that took kernel A's islands-first path: union-find cycles and rounds
+        if isl.any():
+            out["island_labeling"] = {"envs_frac": float(isl.mean()), "cycles_mean": float(g[isl, 3].mean()),
+                                      "cycles_max": float(g[isl, 3].max()), "rounds_mean": float(g[isl, 4].mean()),
+                                      "rounds_max": int(g[isl, 4].max())}
         print(json.dumps(out, indent=1))
         if args.json:
             with open(args.json, "w") as f:
