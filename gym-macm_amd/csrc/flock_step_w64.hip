@@ -605,16 +605,15 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
 // relative observation; `TP`/`TB` are unused for Flock.
 // waves_per_eu(4): <= 128 VGPRs, so the 16 envs per CU of a 4096-env launch are
 // resident together (the unrolled sweep would otherwise hoist every LDS record).
+// The body of one step of env blockIdx.x, inlined into the one-step kernel (env_step_w64) and
+// the multi-step kernel (env_rollout_w64); its LDS arrays are the kernel's.
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
-__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_step_w64(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
-                                                  int cur, const void* __restrict__ actions,
-                                                  OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
-                                                  float* __restrict__ rew_out,
-                                                  uint8_t* __restrict__ coll_out,
-                                                  uint8_t* __restrict__ done_out) {
+__device__ __attribute__((always_inline)) inline void step_w64_body(
+    const StepParams& P, const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur,
+    const void* __restrict__ actions, OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
+    float* __restrict__ rew_out, uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out,
+    const int e = blockIdx.x, const int lane = threadIdx.x) {
   constexpr bool kT = MODE == kTdm;
-  const int e = blockIdx.x;
-  const int lane = threadIdx.x;
 #ifdef MACM_TIMELINE
   const unsigned long long tl_rt0 = __builtin_amdgcn_s_memrealtime(), tl_c0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1744,6 +1743,112 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
 #endif
 }
 
+#ifdef MACM_ROLLOUT_TU
+// nsteps consecutive steps of env blockIdx.x in one launch (macm_world_rollout): actions of step k
+// at actions + k * astride bytes ([K, E, N, A]), outputs overwritten each step (the last step's
+// remain), counters accumulated. Each env's wave runs its own steps back to back, so no env waits
+// at a launch boundary for the slowest env of the batch. Every step reads only what this wave
+// wrote in the step before: a workgroup-scope fence completes its stores before the next step's
+// loads; the barrier orders the LDS reuse. This part is compiled in its own translation unit
+// (flock_rollout_w64.hip, -mllvm -disable-machine-licm): with the step inside a loop, machine
+// LICM hoists the f64 polynomial constants of the trig and atan2 code out of it and the
+// register allocator spills them (327 VGPRs of spills; none without the hoisting).
+template <typename OT>
+struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
+  StepParams P;
+  WorldBuffers B;
+  TdmParams TP;
+  TdmBuffers TB;
+  const void* actions;
+  OT* obs;
+  int32_t* nbr_out;
+  float* rew_out;
+  uint8_t* coll_out;
+  uint8_t* done_out;
+  unsigned long long astride;
+  int cur;
+  int nsteps;
+};
+
+template <int MODE, int NCAP, typename OT, bool SCAL = false>
+__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_rollout_w64(RolloutArgs<OT> A0) {
+  const int nsteps = A0.nsteps;
+  for (int k = 0; k < nsteps; ++k) {
+    // each step reads its parameters from the kernel arguments afresh, through a pointer the
+    // compiler cannot see through, so nothing derived from them stays live across the loop
+    const __attribute__((address_space(4))) RolloutArgs<OT>* ka =
+        (const __attribute__((address_space(4))) RolloutArgs<OT>*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const RolloutArgs<OT>& A = *(const RolloutArgs<OT>*)ka;
+    __builtin_amdgcn_s_setprio(0);  // as at a launch: the chain raises it again
+    step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, A.TB, A.cur ^ (k & 1),
+                                        static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
+                                        A.obs, A.nbr_out, A.rew_out, A.coll_out, A.done_out);
+    // the next step reads only what this wave wrote: workgroup scope (this CU's L1 and its XCD's L2)
+    // suffices; agent scope would write back and invalidate the L2 every step (5x slower, measured)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __syncthreads();
+  }
+}
+
+template <int MODE, int NCAP, typename OT, bool SCAL = false>
+static void launch_roll(int nsteps, unsigned long long astride, hipStream_t s, const StepParams& P,
+                        const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
+                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
+  hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s,
+                     RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps});
+}
+
+// the same instantiation choice as launch_step_w64 / launch_tdm_step_w64
+hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
+                              bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
+                              int nsteps, unsigned long long astride) {
+  const TdmParams TP{};
+  const TdmBuffers TB{};
+  const bool small = P.n_agents <= 32;
+  if (obs_f64) {
+    if (small)
+      launch_roll<kFlock, 32, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+    else
+      launch_roll<kFlock, 64, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+  } else {
+    if (small)
+      launch_roll<kFlock, 32, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+    else if (P.n_envs >= kScalarSweepMinEnvs)
+      launch_roll<kFlock, 64, float, true>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+    else
+      launch_roll<kFlock, 64, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                                  const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
+                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride) {
+  const bool small = P.n_agents <= 32;
+  if (obs_f64) {
+    if (small)
+      launch_roll<kTdm, 32, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+    else
+      launch_roll<kTdm, 64, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+  } else {
+    if (small)
+      launch_roll<kTdm, 32, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+    else
+      launch_roll<kTdm, 64, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+  }
+  return hipGetLastError();
+}
+
+#else  // the one-step kernels, reset / observe kernels and their launchers
+template <int MODE, int NCAP, typename OT, bool SCAL = false>
+__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_step_w64(
+    StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB, int cur, const void* __restrict__ actions,
+    OT* __restrict__ obs, int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
+    uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out) {
+  step_w64_body<MODE, NCAP, OT, SCAL>(P, B, TP, TB, cur, actions, obs, nbr_out, rew_out, coll_out, done_out);
+}
+
 // Initial proxies (b2DynamicTree::CreateProxy: fat = tight +- 0.1), the first
 // FindNewContacts' list (all overlapping pairs, descending), zeroed dynamics,
 // and the initial observation (Flock.obs, mvmnt.py:79).
@@ -1937,30 +2042,32 @@ __global__ __launch_bounds__(W) void tdm_observe_w64(StepParams P, WorldBuffers 
 }
 
 // ---- host-side launchers (C++ linkage, used by macm_capi.hip) -----------------
+template <int MODE, int NCAP, typename OT, bool SCAL = false>
+static void launch_w64(hipStream_t s, const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                       const TdmBuffers& TB, int cur, const void* actions, void* obs, int32_t* nbr, float* rew,
+                       uint8_t* coll, uint8_t* done) {
+  hipLaunchKernelGGL((env_step_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s, P, B, TP, TB, cur, actions,
+                     (OT*)obs, nbr, rew, coll, done);
+}
+
 hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions,
                            void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
                            hipStream_t s) {
-  dim3 grid(P.n_envs), block(W);
   const TdmParams TP{};
   const TdmBuffers TB{};
   const bool small = P.n_agents <= 32;
   if (obs_f64) {
     if (small)
-      hipLaunchKernelGGL((env_step_w64<kFlock, 32, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (double*)obs, nbr, rew, coll, done);
+      launch_w64<kFlock, 32, double>(s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else
-      hipLaunchKernelGGL((env_step_w64<kFlock, 64, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (double*)obs, nbr, rew, coll, done);
+      launch_w64<kFlock, 64, double>(s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
   } else {
     if (small)
-      hipLaunchKernelGGL((env_step_w64<kFlock, 32, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (float*)obs, nbr, rew, coll, done);
+      launch_w64<kFlock, 32, float>(s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else if (P.n_envs >= kScalarSweepMinEnvs)
-      hipLaunchKernelGGL((env_step_w64<kFlock, 64, float, true>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (float*)obs, nbr, rew, coll, done);
+      launch_w64<kFlock, 64, float, true>(s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else
-      hipLaunchKernelGGL((env_step_w64<kFlock, 64, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (float*)obs, nbr, rew, coll, done);
+      launch_w64<kFlock, 64, float>(s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
   }
   return hipGetLastError();
 }
@@ -1968,22 +2075,17 @@ hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, 
 hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
                                uint8_t* done, hipStream_t s) {
-  dim3 grid(P.n_envs), block(W);
   const bool small = P.n_agents <= 32;
   if (obs_f64) {
     if (small)
-      hipLaunchKernelGGL((env_step_w64<kTdm, 32, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (double*)obs, nullptr, nullptr, nullptr, done);
+      launch_w64<kTdm, 32, double>(s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
     else
-      hipLaunchKernelGGL((env_step_w64<kTdm, 64, double>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (double*)obs, nullptr, nullptr, nullptr, done);
+      launch_w64<kTdm, 64, double>(s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
   } else {
     if (small)
-      hipLaunchKernelGGL((env_step_w64<kTdm, 32, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (float*)obs, nullptr, nullptr, nullptr, done);
+      launch_w64<kTdm, 32, float>(s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
     else
-      hipLaunchKernelGGL((env_step_w64<kTdm, 64, float>), grid, block, 0, s, P, B, TP, TB, cur, actions,
-                         (float*)obs, nullptr, nullptr, nullptr, done);
+      launch_w64<kTdm, 64, float>(s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
   }
   return hipGetLastError();
 }
@@ -2028,5 +2130,7 @@ hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* 
     hipLaunchKernelGGL(flock_observe_w64<float>, grid, block, 0, s, P, B, (float*)obs, nbr);
   return hipGetLastError();
 }
+
+#endif  // MACM_ROLLOUT_TU
 
 }  // namespace macm

@@ -17,6 +17,9 @@
 namespace macm {
 hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                            bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
+hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
+                              bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
+                              int nsteps, unsigned long long astride);
 hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
                            int32_t* nbr, const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
@@ -31,6 +34,9 @@ hipError_t launch_observe_wg(const StepParams& P, const WorldBuffers& B, void* o
 hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
                                uint8_t* done, hipStream_t s);
+hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                                  const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
+                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride);
 hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                const TdmBuffers& TB, int cur, void* obs, bool obs_f64, const uint8_t* mask,
                                hipStream_t s);
@@ -526,6 +532,36 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
   return MACM_OK;
 }
 
+int macm_world_rollout(macm_world* w, const void* actions, int n_steps, const macm_outputs* out, void* stream) {
+  if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
+  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
+  if (n_steps == 0) return MACM_OK;
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
+  DeviceGuard g(w->device);
+  const int mode = w->cfg.action_mode == MACM_ACTION_DISCRETE ? 0 : 1;
+  if (w->cfg.validate_actions) {  // every step's actions before any env is stepped
+    const long long rows = (long long)n_steps * w->P.n_envs;
+    if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
+    const int rc = check_actions(w->bad, actions, mode, nullptr, (int)rows, w->P.n_agents, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  const unsigned long long astride =
+      (unsigned long long)w->P.n_envs * w->P.n_agents * (mode == 0 ? 3 * sizeof(uint8_t) : 2 * sizeof(float));
+  if (w->wave) {
+    HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
+                               out->reward, out->collided, out->done, (hipStream_t)stream, n_steps, astride));
+    if (n_steps & 1) w->cur ^= 1;
+  } else {  // workgroup path: its three launches per step, in order
+    for (int k = 0; k < n_steps; ++k) {
+      HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, static_cast<const unsigned char*>(actions) + k * astride,
+                             out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward, out->collided, out->done,
+                             (hipStream_t)stream));
+      w->cur ^= 1;
+    }
+  }
+  return MACM_OK;
+}
+
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
   if (!w || !out) return fail(MACM_E_INVALID, "world/out is NULL");
   DeviceGuard g(w->device);
@@ -921,6 +957,26 @@ int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out,
   HIP_TRY(launch_tdm_step_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
                               w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream));
   w->cur ^= 1;
+  return MACM_OK;
+}
+
+int macm_tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
+  if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
+  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
+  if (n_steps == 0) return MACM_OK;
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
+  DeviceGuard g(w->device);
+  if (w->cfg.validate_actions) {  // every agent's actions of every step, alive or not (deaths are not known yet)
+    const long long rows = (long long)n_steps * w->P.n_envs;
+    if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
+    const int rc = check_actions(w->bad, actions, 2, nullptr, (int)rows, w->P.n_agents, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  const TdmBuffers TB = tdm_with_outputs(w, out);
+  const unsigned long long astride = (unsigned long long)w->P.n_envs * w->P.n_agents * 4;
+  HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
+                                 w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream, n_steps, astride));
+  if (n_steps & 1) w->cur ^= 1;
   return MACM_OK;
 }
 

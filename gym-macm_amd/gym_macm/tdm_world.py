@@ -140,6 +140,22 @@ class TdmWorld:
         self.L.macm_tdm_step(self.h, ctypes.c_void_p(actions_ptr), ctypes.byref(self._out),
                              ctypes.c_void_p(stream_handle))
 
+    def rollout(self, actions: torch.Tensor):
+        """K steps with actions given in advance (uint8 [K, E, N, 4] on this device) in one launch
+        (macm_tdm_rollout); same results as K step() calls, the outputs hold the last step's."""
+        if actions.device != self.device or not actions.is_contiguous() or actions.dim() != 4:
+            raise ValueError("actions must be a contiguous [K, E, N, 4] tensor on the world's device")
+        if actions.dtype not in (torch.uint8, torch.int8) or tuple(actions.shape[1:]) != (self.E, self.N, 4):
+            raise ValueError(f"TDM rollout actions must be uint8 [K,{self.E},{self.N},4]")
+        _abi.check(self.L.macm_tdm_rollout(self.h, _ptr(actions), int(actions.shape[0]), ctypes.byref(self._out),
+                                           self._stream()), "macm_tdm_rollout")
+        return self.outputs()
+
+    def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
+        """Minimal-overhead rollout for timed loops (no validation)."""
+        self.L.macm_tdm_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
+                                ctypes.c_void_p(stream_handle))
+
     def observe(self):
         _abi.check(self.L.macm_tdm_observe(self.h, ctypes.byref(self._out), self._stream()), "macm_tdm_observe")
         return self.outputs()

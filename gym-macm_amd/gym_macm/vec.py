@@ -67,6 +67,12 @@ class FlockVec(object):
             self.world.reset_envs(self.world.done)
         return out
 
+    def rollout(self, actions):
+        """K steps of every env with actions given in advance ([K, E, N, 3] on the device, e.g. a
+        random-action rollout), one launch (World.rollout): each env runs its K steps back to back.
+        Same results as K step() calls without autoreset; returns the last step's outputs."""
+        return self.world.rollout(actions)
+
     def reset_envs(self, mask=None):
         """New episodes in the masked envs (see World.reset_envs)."""
         return self.world.reset_envs(mask)

@@ -136,6 +136,25 @@ class World:
         self.L.macm_world_step(self.h, ctypes.c_void_p(actions_ptr), ctypes.byref(self._out),
                                ctypes.c_void_p(stream_handle))
 
+    def rollout(self, actions: torch.Tensor):
+        """K steps with actions given in advance ([K, E, N, 3] uint8/int8 or [K, E, N, 2] float32 on
+        this device), one launch on the wave path (macm_world_rollout). Same results as K step()
+        calls; the outputs hold the last step's values."""
+        if actions.device != self.device or not actions.is_contiguous() or actions.dim() != 4:
+            raise ValueError("actions must be a contiguous [K, E, N, A] tensor on the world's device")
+        A = 3 if self.cfg.action_mode == _abi.ACTION_DISCRETE else 2
+        ok = actions.dtype in (torch.uint8, torch.int8) if A == 3 else actions.dtype == torch.float32
+        if not ok or tuple(actions.shape[1:]) != (self.E, self.N, A):
+            raise ValueError(f"rollout actions must be [K,{self.E},{self.N},{A}] of the step's action dtype")
+        _abi.check(self.L.macm_world_rollout(self.h, _ptr(actions), int(actions.shape[0]), ctypes.byref(self._out),
+                                             self._stream()), "macm_world_rollout")
+        return self.obs, self.nbr_id, self.reward, self.done
+
+    def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
+        """Minimal-overhead rollout for timed loops (no validation)."""
+        self.L.macm_world_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
+                                  ctypes.c_void_p(stream_handle))
+
     def observe(self):
         _abi.check(self.L.macm_world_observe(self.h, ctypes.byref(self._out_obs), self._stream()),
                    "macm_world_observe")

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 3
+#define MACM_ABI_VERSION 4
 
 enum {
   MACM_OK = 0,
@@ -314,6 +314,19 @@ int macm_world_reset_envs(macm_world* w, const uint8_t* env_mask, const macm_out
  */
 int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream);
 
+/*
+ * n_steps consecutive env.steps of all E envs with actions given in advance, e.g. the
+ * reference's random-action loop (`env.step(env.action_space.sample())`, mvmnt.py:271-293),
+ * in one launch on the wave path (N <= 64): each env's wave runs its steps back to back, so no
+ * env waits at a launch boundary for the slowest env of the batch. Results are those of
+ * n_steps macm_world_step calls with the same actions.
+ *   actions: device pointer, [n_steps, E, N, 3] uint8 (discrete) or [n_steps, E, N, 2] float32.
+ *   out: overwritten by every step; the last step's outputs remain. Counters accumulate all steps.
+ * The workgroup path (N > 64) launches its steps one after another. n_steps = 0 does nothing.
+ * With cfg.validate_actions every step's actions are checked before any env is stepped.
+ */
+int macm_world_rollout(macm_world* w, const void* actions, int32_t n_steps, const macm_outputs* out, void* stream);
+
 /* Observation of the current state without stepping (Flock.get_obs, mvmnt.py:181-222). */
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream);
 
@@ -383,6 +396,13 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
  * contacts, 16 per body) overflowed in an earlier step; MACM_E_INVALID with validate_actions.
  */
 int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream);
+
+/*
+ * As macm_world_rollout for TDM: actions [n_steps, E, N, 4] uint8, one launch. With
+ * validate_actions every row is checked, the dead agents' rows included (deaths within the
+ * rollout are not known when the check runs).
+ */
+int macm_tdm_rollout(macm_tdm* w, const void* actions, int32_t n_steps, const macm_tdm_outputs* out, void* stream);
 
 /* TDM.get_obs of the current state without stepping. */
 int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream);
