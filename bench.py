@@ -142,6 +142,11 @@ def main():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo: host-side counters, ranks "
                          "may share a GPU (multi-process test of the sharded path on a 1-GPU box)")
+    ap.add_argument("--launch", choices=("rollout", "step"), default="rollout",
+                    help="rollout: the K timed steps (actions drawn in advance) in one macm_world_rollout launch, "
+                         "each env's wave running its steps back to back (N <= 64; the workgroup path launches "
+                         "per step either way); step: one launch per step. --policy bots is always per step. "
+                         "A rollout run also times the per-step launches on the same window (per_step_launch)")
     ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
     if args.traffic_json is None:
@@ -206,27 +211,42 @@ def main():
         def step(_ptr, sh_):  # noqa: F811
             world_h.step_raw(loop_ptr, sh_)
             policy()
-    log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}")
-    for w in range(W):
-        step(base + w * stride, sh)
-    torch.cuda.synchronize(dev)
-    if args.env == "flock":
-        world_h.reset_counters()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(K):
-        step(base + (W + k) * stride, sh)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    kernel_ms = ev0.elapsed_time(ev1) / K  # per launch, on the launch stream
+    rollout = args.launch == "rollout" and args.policy == "random"
+    log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}, "
+        f"{'one rollout launch' if rollout else 'one launch per step'}")
+
+    def timed_window(roll):
+        """W untimed warm-up steps from the current state, then K timed steps (bracketed by a barrier
+        and synchronisations); returns (host seconds, event ms on the launch stream)."""
+        if roll:
+            if W:
+                world_h.rollout_raw(base, W, sh)
+        else:
+            for w in range(W):
+                step(base + w * stride, sh)
+        torch.cuda.synchronize(dev)
+        if args.env == "flock":
+            world_h.reset_counters()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        if roll:
+            world_h.rollout_raw(base + W * stride, K, sh)
+        else:
+            for k in range(K):
+                step(base + (W + k) * stride, sh)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        return t1 - t0, ev0.elapsed_time(ev1)
+
+    elapsed, ev_ms = timed_window(rollout)
+    kernel_ms = ev_ms / K  # per step on the launch stream (a rollout launch covers all K steps)
     # one small RCCL all-reduce of counters after the timed region (no data-path collective)
     status = int(gdist.reduce_counters([world_h.status()], device=red_dev, op="max")[0])
     cnt = gdist.reduce_counters(world_h.counters(), device=red_dev)
@@ -244,13 +264,13 @@ def main():
         achieved_gbs = b_alg * E * N / (kernel_ms * 1e-3) / 1e9
         ncap = 32 if N <= 32 else 64
         if args.env == "tdm":
-            kname = f"env_step_w64<1, {ncap}, float, false>"
+            kname = f"env_{'rollout' if rollout else 'step'}_w64<1, {ncap}, float, false>"
         else:
             # N > 64: the workgroup path's three launches per step (split step; kernel_ms covers all)
             # N > 32 with >= 2048 envs: the scalar-sweep instantiation (flock_step_w64.hip,
             # kScalarSweepMinEnvs)
             scal = "true" if (ncap == 64 and E >= SCALAR_SWEEP_MIN_ENVS) else "false"
-            kname = (f"env_step_w64<0, {ncap}, float, {scal}>" if N <= 64
+            kname = (f"env_{'rollout' if rollout else 'step'}_w64<0, {ncap}, float, {scal}>" if N <= 64
                      else "flock_step_wg_a + flock_solve_wg + flock_step_wg_c<float>")
         traffic = None
         tj = load_traffic(args.traffic_json)
@@ -258,7 +278,8 @@ def main():
             kname = kname.replace("float", "double")
         if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
                 and tj.get("policy", "random") == args.policy):
-            traffic = tj.get("hbm_bytes_per_launch")
+            # per step (a rollout launch's bytes over its steps), like achieved
+            traffic = tj.get("hbm_bytes_per_launch") / tj.get("steps_per_launch", 1)
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
         if args.env == "tdm":
@@ -292,11 +313,15 @@ def main():
                 "parallelism": f"env-sharded x{world} (no data-path collective)"
                                + ("" if world == 1 or args.dist_backend == "nccl" else ", gloo counters (test mode)"),
                 "obs": "float64" if args.obs_f64 else "float32",
+                "launch": ("one macm_world_rollout launch for the K timed steps" if rollout and N <= 64
+                           else "one step per launch" if not rollout
+                           else "macm_world_rollout, workgroup path: 3 launches per step"),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": kname, "kernel_ms": kernel_ms,
+                "kernel": kname, "kernel_ms": kernel_ms,  # per step
+                "steps_per_launch": K if (rollout and N <= 64) else 1,
                 "bytes_alg_per_launch": b_alg * E * N,
             },
         }
@@ -306,6 +331,15 @@ def main():
         else:
             out["counters"] = {"alive_agent_steps": int(cnt[0]), "melee_attacks": int(cnt[1]),
                                "deaths": int(cnt[2]), "done_env_steps": int(cnt[3])}
+        if rollout and world == 1:
+            # the same window again with one launch per step (what a closed-loop policy needs)
+            if args.env == "flock":
+                vec.reset()
+            else:
+                world_h.reset(args.seed, gdist.env_offset(rank, E))
+            el2, ev2 = timed_window(False)
+            out["per_step_launch"] = {"value": E * N * K / el2, "ms_per_step": el2 / K * 1e3,
+                                      "kernel_ms_per_step": ev2 / K}
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
             if args.env == "flock":

@@ -533,9 +533,9 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
 }
 
 int macm_world_rollout(macm_world* w, const void* actions, int n_steps, const macm_outputs* out, void* stream) {
-  if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
   if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
-  if (n_steps == 0) return MACM_OK;
+  if (n_steps == 0) return MACM_OK;  // nothing is read, so actions may be NULL (an empty tensor)
+  if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
   if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
   DeviceGuard g(w->device);
   const int mode = w->cfg.action_mode == MACM_ACTION_DISCRETE ? 0 : 1;
@@ -961,9 +961,9 @@ int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out,
 }
 
 int macm_tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
-  if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
   if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
   if (n_steps == 0) return MACM_OK;
+  if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
   if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
   DeviceGuard g(w->device);
   if (w->cfg.validate_actions) {  // every agent's actions of every step, alive or not (deaths are not known yet)

@@ -248,6 +248,6 @@ def check(code: int, fn: str) -> None:
         msg = msg.decode() if msg else ""
         if code == E_OVERFLOW:
             raise MacmOverflowError(code, fn, msg)
-        if code == E_INVALID and fn.endswith("_step") and "action space" in msg:
+        if code == E_INVALID and fn.endswith(("_step", "_rollout")) and "action space" in msg:
             raise MacmInvalidActionError(code, fn, msg)
         raise MacmError(code, fn, msg)

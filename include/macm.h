@@ -322,7 +322,8 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
  * n_steps macm_world_step calls with the same actions.
  *   actions: device pointer, [n_steps, E, N, 3] uint8 (discrete) or [n_steps, E, N, 2] float32.
  *   out: overwritten by every step; the last step's outputs remain. Counters accumulate all steps.
- * The workgroup path (N > 64) launches its steps one after another. n_steps = 0 does nothing.
+ * The workgroup path (N > 64) launches its steps one after another. n_steps = 0 does nothing
+ * (actions may then be NULL).
  * With cfg.validate_actions every step's actions are checked before any env is stepped.
  */
 int macm_world_rollout(macm_world* w, const void* actions, int32_t n_steps, const macm_outputs* out, void* stream);

@@ -1,0 +1,137 @@
+"""macm_world_rollout / macm_tdm_rollout: K steps of every env with actions given in advance in
+one launch (include/macm.h). The bar is the per-step path's: a rollout leaves exactly the state,
+outputs and counters that K macm_world_step calls with the same actions leave (and so the
+oracle's), for both parities of K, both observation widths, continuous actions, the spill step
+inside the loop (dense worlds), the workgroup path (a launch sequence per step) and TDM.
+Reference: the random-action loop `env.step(env.action_space.sample())` (mvmnt.py:271-293)."""
+import numpy as np
+import pytest
+import torch
+
+from parity import assert_state_equal
+from test_gpu_parity import make_pair
+
+pytestmark = pytest.mark.gpu
+
+from gym_macm import _abi  # noqa: E402
+from gym_macm.tdm_world import TdmWorld, tdm_config  # noqa: E402
+from gym_macm.vec import FlockVec  # noqa: E402
+
+
+def flock_actions(K, E, N, seed, continuous=False):
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    if continuous:
+        return torch.rand((K, E, N, 2), device="cuda:0", generator=g) * 2 - 1
+    return torch.randint(0, 3, (K, E, N, 3), dtype=torch.uint8, device="cuda:0", generator=g)
+
+
+def outputs(w):
+    return [t.clone() for t in (w.obs, w.nbr_id, w.reward, w.collided, w.done)]
+
+
+def assert_same(a_vec, b_vec, ctx):
+    for x, y, nm in zip(outputs(a_vec.world), outputs(b_vec.world), ("obs", "nbr", "reward", "collided", "done")):
+        assert torch.equal(x, y), f"{ctx}: {nm}"
+    sa, sb = a_vec.get_state(), b_vec.get_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"{ctx}: state[{k}]")
+    np.testing.assert_array_equal(a_vec.counters(), b_vec.counters(), err_msg=f"{ctx}: counters")
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (64, 64, 7, {}),                                   # odd K: the list parity flips
+    (64, 64, 10, {}),
+    (48, 20, 9, {}),                                   # the 32-lane instantiation
+    (32, 64, 6, {"obs_dtype": torch.float64}),
+    (40, 30, 8, {"action_mode": "continuous"}),
+    (8, 64, 12, {"start_spread": 4}),                  # dense: the spill step inside the loop
+    (2100, 64, 5, {}),                                 # >= 2048 envs: the scalar-sweep instantiation
+])
+def test_flock_rollout_equals_per_step(E, N, K, kw):
+    cont = kw.get("action_mode") == "continuous"
+    a = FlockVec(E, n_agents=[N], seed=5, device="cuda:0", **kw)
+    b = FlockVec(E, n_agents=[N], seed=5, device="cuda:0", **kw)
+    acts = flock_actions(2 * K + 3, E, N, 11, cont)
+    for k in range(K):
+        a.step(acts[k])
+    b.rollout(acts[:K])
+    assert_same(a, b, f"after rollout of {K}")
+    # stepping on after the rollout (one step, then a second rollout) stays in lockstep
+    a.step(acts[K])
+    b.step(acts[K])
+    for k in range(K + 1, 2 * K + 3):
+        a.step(acts[k])
+    b.rollout(acts[K + 1:2 * K + 3])
+    assert_same(a, b, "after step + second rollout")
+    assert a.status() == 0 and b.status() == 0
+    if kw.get("start_spread") == 4:
+        assert b.spilled() > 0, "the dense start never reached the spill step"
+
+
+def test_flock_rollout_matches_oracle():
+    """40 steps of 16 envs x 64 agents in one launch against the oracle stepped 40 times."""
+    E, N, K = 16, 64, 40
+    vec, orc = make_pair(E, [N], seed=21, start_spread=8)
+    rng = np.random.default_rng(3)
+    acts = rng.integers(0, 3, size=(K, E, N, 3)).astype(np.uint8)
+    vec.rollout(torch.from_numpy(acts).cuda())
+    for k in range(K):
+        r = orc.step(acts[k])
+    assert_state_equal(vec.get_state(), orc.get_state(vec.world.C), "rollout end")
+    np.testing.assert_array_equal(vec.nbr_id.cpu().numpy(), r["nbr_id"])
+    np.testing.assert_array_equal(vec.world.reward.cpu().numpy(), r["reward"].astype(np.float32))
+    np.testing.assert_array_equal(vec.world.collided.cpu().numpy(), r["collided"])
+    assert vec.status() == 0
+
+
+def test_workgroup_path_rollout_equals_per_step():
+    """N > 64: macm_world_rollout launches the split step K times."""
+    E, N, K = 6, 100, 5
+    a = FlockVec(E, n_agents=[N], seed=8, device="cuda:0", start_spread=12)
+    b = FlockVec(E, n_agents=[N], seed=8, device="cuda:0", start_spread=12)
+    acts = flock_actions(K, E, N, 4)
+    for k in range(K):
+        a.step(acts[k])
+    b.rollout(acts)
+    assert_same(a, b, "workgroup rollout")
+
+
+def test_rollout_zero_steps_and_validation():
+    E, N = 4, 16
+    v = FlockVec(E, n_agents=[N], seed=2, device="cuda:0", validate_actions=True)
+    s0 = v.get_state()
+    acts = flock_actions(3, E, N, 9)
+    v.rollout(acts[:0])  # n_steps = 0: nothing happens
+    acts[2, 1, 5, 0] = 3  # out of MultiDiscrete([3, 3, 3]) in the last step: no env is stepped
+    with pytest.raises(_abi.MacmInvalidActionError):
+        v.rollout(acts)
+    s1 = v.get_state()
+    for k in s0:
+        np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
+    with pytest.raises(ValueError):
+        v.rollout(acts[0])  # not [K, E, N, 3]
+
+
+@pytest.mark.parametrize("teams,K,obs_f64", [([16, 16], 9, False), ([8, 8, 8], 12, True)])
+def test_tdm_rollout_equals_per_step(teams, K, obs_f64):
+    E = 64
+    N = sum(teams)
+    a = TdmWorld(tdm_config(teams, obs_f64=obs_f64), E, device="cuda:0")
+    b = TdmWorld(tdm_config(teams, obs_f64=obs_f64), E, device="cuda:0")
+    a.reset(7, 0)
+    b.reset(7, 0)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(1)
+    acts = torch.randint(0, 3, (K, E, N, 4), dtype=torch.uint8, device="cuda:0", generator=g)
+    acts[..., 3] = torch.randint(0, 2, (K, E, N), dtype=torch.uint8, device="cuda:0", generator=g)
+    for k in range(K):
+        a.step(acts[k])
+    b.rollout(acts)
+    for x, y in zip(a.outputs(), b.outputs()):
+        assert torch.equal(x, y)
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"state[{k}]")
+    np.testing.assert_array_equal(a.counters(), b.counters())
+    assert int(a.counters()[1]) > 0, "no melee attacks: the combat branch was not exercised"

@@ -18,13 +18,19 @@ import json
 import os
 
 
-def kernel_means(path, kernel):
-    agg = collections.defaultdict(list)
+def kernel_means(path, kernel, last=False):
+    """Mean per dispatch of each counter over the kernel's dispatches (last: the last dispatch only,
+    e.g. the timed rollout launch after the warm-up one)."""
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
     with open(path) as f:
         for r in csv.DictReader(f):
             if kernel in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+                agg[r["Counter_Name"]][r.get("Dispatch_Id", "0")] += float(r["Counter_Value"])
+    out = {}
+    for k, per in agg.items():
+        vals = [per[d] for d in sorted(per, key=lambda x: int(x))]
+        out[k] = vals[-1] if last else sum(vals) / len(vals)
+    return out
 
 
 def main():
@@ -34,13 +40,16 @@ def main():
     ap.add_argument("--policy", default="random")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--agents", type=int, default=64)
+    ap.add_argument("--steps-per-launch", type=int, default=1,
+                    help="env steps one launch of the kernel takes (a rollout launch: its K)")
+    ap.add_argument("--last", action="store_true", help="the kernel's last dispatch only")
     ap.add_argument("-o", "--out", default="")
     a = ap.parse_args()
     res = {}
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
         p = os.path.join(a.dir, sub, "run_counter_collection.csv")
         if os.path.exists(p):
-            res.update(kernel_means(p, a.kernel))
+            res.update(kernel_means(p, a.kernel, a.last))
     fetch_b = res["FETCH_SIZE"] * 1024.0
     write_b = res["WRITE_SIZE"] * 1024.0
     agents = a.envs * a.agents
@@ -48,7 +57,8 @@ def main():
         "kernel": a.kernel, "envs": a.envs, "agents": a.agents, "policy": a.policy,
         "fetch_size_kib": res["FETCH_SIZE"], "write_size_kib": res["WRITE_SIZE"],
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
-        "hbm_bytes_per_agent_step": (2.0 * fetch_b + write_b) / agents,
+        "steps_per_launch": a.steps_per_launch,
+        "hbm_bytes_per_agent_step": (2.0 * fetch_b + write_b) / agents / a.steps_per_launch,
         "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE",
         "per_wave": {k: v / res.get("SQ_WAVES", 1.0) for k, v in res.items() if k.startswith("SQ_")},
         "source": a.dir,

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--agents", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--flocks", type=int, default=1)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -34,7 +35,8 @@ def main():
     if args.env == "flock":
         from gym_macm.vec import FlockVec
         N = args.agents
-        w = FlockVec(E, n_agents=[N], seed=seed, device=dev).world
+        targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
+        w = FlockVec(E, n_agents=[N], targets=targets, seed=seed, device=dev).world
         acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
         outs = lambda: (w.obs, w.nbr_id, w.reward, w.collided, w.done)  # noqa: E731
     else:
