@@ -44,6 +44,10 @@ SCENARIOS = [
          policy="random_cont"),
     dict(name="n12_split_3targets", seed=21, n_agents=[5, 7], targets=[0, 1, 2] * 4, steps=120,
          policy="bots"),
+    # random actions with the target drawn 1-3 m from a dense start (start_spread 5): positive
+    # binary rewards and collisions from the first step, without a scripted policy
+    dict(name="n24_near_target_dense", seed=13, n_agents=[24],
+         kwargs=dict(start_spread=5, target_mindist=1, target_maxdist=3), steps=150, policy="random"),
 ]
 
 # TDM (combat.py). Stepped until done or `steps`.
