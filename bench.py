@@ -143,10 +143,11 @@ def main():
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo: host-side counters, ranks "
                          "may share a GPU (multi-process test of the sharded path on a 1-GPU box)")
     ap.add_argument("--launch", choices=("rollout", "step"), default="rollout",
-                    help="rollout: the K timed steps (actions drawn in advance) in one macm_world_rollout launch, "
-                         "each env's wave running its steps back to back (N <= 64; the workgroup path launches "
-                         "per step either way); step: one launch per step. --policy bots is always per step. "
-                         "A rollout run also times the per-step launches on the same window (per_step_launch)")
+                    help="rollout: the K timed steps in one launch, each env's wave running its steps back to "
+                         "back (random: macm_world_rollout over the actions drawn in advance; bots: "
+                         "macm_world_rollout_bots, the bot acting inside the launch; N <= 64, the workgroup path "
+                         "launches per step either way); step: one launch per step (plus the bot's). A rollout run "
+                         "also times the per-step launches on the same window (per_step_launch)")
     ap.add_argument("--traffic-json", default=None)
     args = ap.parse_args()
     if args.traffic_json is None:
@@ -211,14 +212,17 @@ def main():
         def step(_ptr, sh_):  # noqa: F811
             world_h.step_raw(loop_ptr, sh_)
             policy()
-    rollout = args.launch == "rollout" and args.policy == "random"
+    rollout = args.launch == "rollout"
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}, "
         f"{'one rollout launch' if rollout else 'one launch per step'}")
 
     def timed_window(roll):
         """W untimed warm-up steps from the current state, then K timed steps (bracketed by a barrier
         and synchronisations); returns (host seconds, event ms on the launch stream)."""
-        if roll:
+        if roll and args.policy == "bots":  # closed loop in one launch: the bot acts inside it
+            if W:
+                world_h.rollout_bots_raw(loop_ptr, W, sh)
+        elif roll:
             if W:
                 world_h.rollout_raw(base, W, sh)
         else:
@@ -233,7 +237,9 @@ def main():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        if roll:
+        if roll and args.policy == "bots":
+            world_h.rollout_bots_raw(loop_ptr, K, sh)
+        elif roll:
             world_h.rollout_raw(base + W * stride, K, sh)
         else:
             for k in range(K):
@@ -313,7 +319,8 @@ def main():
                 "parallelism": f"env-sharded x{world} (no data-path collective)"
                                + ("" if world == 1 or args.dist_backend == "nccl" else ", gloo counters (test mode)"),
                 "obs": "float64" if args.obs_f64 else "float32",
-                "launch": ("one macm_world_rollout launch for the K timed steps" if rollout and N <= 64
+                "launch": (f"one macm_world_rollout{'_bots' if args.policy == 'bots' else ''} launch for the "
+                           "K timed steps" if rollout and N <= 64
                            else "one step per launch" if not rollout
                            else "macm_world_rollout, workgroup path: 3 launches per step"),
             },
@@ -337,6 +344,8 @@ def main():
                 vec.reset()
             else:
                 world_h.reset(args.seed, gdist.env_offset(rank, E))
+            if args.policy == "bots":
+                policy()  # the first actions from the initial obs again
             el2, ev2 = timed_window(False)
             out["per_step_launch"] = {"value": E * N * K / el2, "ms_per_step": el2 / K * 1e3,
                                       "kernel_ms_per_step": ev2 / K}

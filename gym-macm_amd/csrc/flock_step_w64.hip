@@ -41,6 +41,7 @@
 //     solver is a signed zero; dropping them can change only the sign of a zero
 //     velocity/impulse component, never a nonzero value or any position.
 //   * circles sit at the body origin, so b2Mul(xf, m_p) == position exactly.
+#include "bots.hpp"
 #include "flock_common.hpp"
 #include "flock_spill.hpp"
 
@@ -1768,6 +1769,9 @@ struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   unsigned long long astride;
   int cur;
   int nsteps;
+  // closed loop (macm_world_rollout_bots): every step reads its actions here and the device bot
+  // (bots.hpp) writes the next step's from the observation this step wrote; NULL: actions[k]
+  uint8_t* policy_act;
 };
 
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
@@ -1782,12 +1786,27 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     const RolloutArgs<OT>& A = *(const RolloutArgs<OT>*)ka;
     __builtin_amdgcn_s_setprio(0);  // as at a launch: the chain raises it again
     step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, A.TB, A.cur ^ (k & 1),
-                                        static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
+                                        A.policy_act ? A.policy_act
+                                                     : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
                                         A.obs, A.nbr_out, A.rew_out, A.coll_out, A.done_out);
     // the next step reads only what this wave wrote: workgroup scope (this CU's L1 and its XCD's L2)
     // suffices; agent scope would write back and invalidate the L2 every step (5x slower, measured)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __syncthreads();
+    if (A.policy_act) {  // every agent row, as the bots kernel over all E x N rows
+      const int N = A.P.n_agents, lane = threadIdx.x;
+      if (lane < N) {
+        const size_t row = (size_t)blockIdx.x * N + lane;
+        if constexpr (MODE == kTdm)
+          bot_combat_row(A.obs + row * (N - 1) * 4, A.TB.mask_out + row * (N - 1), N, A.policy_act + row * 4);
+        else {
+          const int od = A.P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+          bot_flock_row(A.obs + row * od, od, A.policy_act + row * 3);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __syncthreads();
+    }
   }
 }
 
@@ -1795,8 +1814,10 @@ template <int MODE, int NCAP, typename OT, bool SCAL = false>
 static void launch_roll(int nsteps, unsigned long long astride, hipStream_t s, const StepParams& P,
                         const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
                         void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
+  // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
+  uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
   hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s,
-                     RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps});
+                     RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol});
 }
 
 // the same instantiation choice as launch_step_w64 / launch_tdm_step_w64

@@ -562,6 +562,35 @@ int macm_world_rollout(macm_world* w, const void* actions, int n_steps, const ma
   return MACM_OK;
 }
 
+int macm_world_rollout_bots(macm_world* w, uint8_t* actions, int n_steps, const macm_outputs* out, void* stream) {
+  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
+  if (n_steps == 0) return MACM_OK;
+  if (!w || !actions || !out || !out->obs || !out->reward)
+    return fail(MACM_E_INVALID, "world/actions/out/obs/reward is NULL");
+  if (w->cfg.action_mode != MACM_ACTION_DISCRETE) return fail(MACM_E_INVALID, "bots.flock acts in discrete mode");
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (w->cfg.validate_actions) {  // the first step's (the caller's); the bot's are in range
+    const int rc = check_actions(w->bad, actions, 0, nullptr, w->P.n_envs, w->P.n_agents, s);
+    if (rc) return rc;
+  }
+  if (w->wave) {  // astride 0: the closed-loop form of the rollout kernel
+    HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
+                               out->reward, out->collided, out->done, s, n_steps, 0));
+    if (n_steps & 1) w->cur ^= 1;
+  } else {
+    const long long rows = (long long)w->P.n_envs * w->P.n_agents;
+    for (int k = 0; k < n_steps; ++k) {
+      HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
+                             out->reward, out->collided, out->done, s));
+      w->cur ^= 1;
+      HIP_TRY(launch_bots_flock(out->obs, w->cfg.obs_f64 != 0, obs_dim(w->cfg), rows, actions, s));
+    }
+  }
+  return MACM_OK;
+}
+
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
   if (!w || !out) return fail(MACM_E_INVALID, "world/out is NULL");
   DeviceGuard g(w->device);
@@ -976,6 +1005,24 @@ int macm_tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm_t
   const unsigned long long astride = (unsigned long long)w->P.n_envs * w->P.n_agents * 4;
   HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
                                  w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream, n_steps, astride));
+  if (n_steps & 1) w->cur ^= 1;
+  return MACM_OK;
+}
+
+int macm_tdm_rollout_bots(macm_tdm* w, uint8_t* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
+  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
+  if (n_steps == 0) return MACM_OK;
+  if (!w || !actions || !out || !out->obs || !out->mask) return fail(MACM_E_INVALID, "tdm/actions/obs/mask is NULL");
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (w->cfg.validate_actions) {
+    const int rc = check_actions(w->bad, actions, 2, w->TB.alive, w->P.n_envs, w->P.n_agents, s);
+    if (rc) return rc;
+  }
+  const TdmBuffers TB = tdm_with_outputs(w, out);
+  HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->done,
+                                 s, n_steps, 0));
   if (n_steps & 1) w->cur ^= 1;
   return MACM_OK;
 }

@@ -189,6 +189,7 @@ SIGNATURES = {
     "macm_world_reset_envs": (c_int, [c_void_p, c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_step": (c_int, [c_void_p, c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_rollout": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmOutputs), c_void_p]),
+    "macm_world_rollout_bots": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmOutputs), c_void_p]),
     "macm_world_observe": (c_int, [c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_get_state": (c_int, [c_void_p, POINTER(MacmState), c_void_p]),
     "macm_world_set_state": (c_int, [c_void_p, POINTER(MacmState), c_void_p]),
@@ -205,6 +206,7 @@ SIGNATURES = {
     "macm_tdm_reset_envs": (c_int, [c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_step": (c_int, [c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_rollout": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_rollout_bots": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_observe": (c_int, [c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_get_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),
     "macm_tdm_set_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),

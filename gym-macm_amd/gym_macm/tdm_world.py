@@ -156,6 +156,20 @@ class TdmWorld:
         self.L.macm_tdm_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
                                 ctypes.c_void_p(stream_handle))
 
+    def rollout_bots(self, actions: torch.Tensor, n_steps: int):
+        """n_steps of the closed loop step -> bots.combat -> step in one launch (macm_tdm_rollout_bots);
+        actions uint8 [E, N, 4]: the first step's on entry, the bot's next on return."""
+        if (actions.device != self.device or not actions.is_contiguous() or actions.dtype != torch.uint8
+                or tuple(actions.shape) != (self.E, self.N, 4)):
+            raise ValueError(f"actions must be a contiguous uint8 [{self.E},{self.N},4] tensor on the world's device")
+        _abi.check(self.L.macm_tdm_rollout_bots(self.h, _ptr(actions), int(n_steps), ctypes.byref(self._out),
+                                                self._stream()), "macm_tdm_rollout_bots")
+        return self.outputs()
+
+    def rollout_bots_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
+        self.L.macm_tdm_rollout_bots(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
+                                     ctypes.c_void_p(stream_handle))
+
     def observe(self):
         _abi.check(self.L.macm_tdm_observe(self.h, ctypes.byref(self._out), self._stream()), "macm_tdm_observe")
         return self.outputs()

@@ -73,6 +73,11 @@ class FlockVec(object):
         Same results as K step() calls without autoreset; returns the last step's outputs."""
         return self.world.rollout(actions)
 
+    def rollout_bots(self, actions, n_steps):
+        """n_steps of the closed loop step -> bots.flock -> step in one launch (World.rollout_bots);
+        ``actions`` (uint8 [E, N, 3]) holds the first step's actions on entry, the next on return."""
+        return self.world.rollout_bots(actions, n_steps)
+
     def reset_envs(self, mask=None):
         """New episodes in the masked envs (see World.reset_envs)."""
         return self.world.reset_envs(mask)

@@ -155,6 +155,21 @@ class World:
         self.L.macm_world_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
                                   ctypes.c_void_p(stream_handle))
 
+    def rollout_bots(self, actions: torch.Tensor, n_steps: int):
+        """n_steps of the closed loop step -> bots.flock -> step in one launch (macm_world_rollout_bots).
+        actions: uint8 [E, N, 3] on this device, the first step's actions on entry (e.g.
+        bots.flock_actions(self.obs)) and the bot's next actions on return."""
+        if (actions.device != self.device or not actions.is_contiguous() or actions.dtype != torch.uint8
+                or tuple(actions.shape) != (self.E, self.N, 3)):
+            raise ValueError(f"actions must be a contiguous uint8 [{self.E},{self.N},3] tensor on the world's device")
+        _abi.check(self.L.macm_world_rollout_bots(self.h, _ptr(actions), int(n_steps), ctypes.byref(self._out),
+                                                  self._stream()), "macm_world_rollout_bots")
+        return self.obs, self.nbr_id, self.reward, self.done
+
+    def rollout_bots_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
+        self.L.macm_world_rollout_bots(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
+                                       ctypes.c_void_p(stream_handle))
+
     def observe(self):
         _abi.check(self.L.macm_world_observe(self.h, ctypes.byref(self._out_obs), self._stream()),
                    "macm_world_observe")

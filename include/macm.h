@@ -328,6 +328,16 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
  */
 int macm_world_rollout(macm_world* w, const void* actions, int32_t n_steps, const macm_outputs* out, void* stream);
 
+/*
+ * n_steps of the closed loop `step -> bots.flock -> step` (test_scripts/bots.py:37-61 acting on every
+ * agent's observation, as macm_bots_flock) in one launch on the wave path: each env's wave steps,
+ * then every lane takes its agent's next action from the observation just written.
+ *   actions: device uint8 [E, N, 3]; in: the first step's actions (e.g. macm_bots_flock on the
+ *   initial obs); out: the bot's actions for the step after the last. out->obs must be set.
+ * Same results as n_steps of (macm_world_step, macm_bots_flock). Workgroup path: those launches.
+ */
+int macm_world_rollout_bots(macm_world* w, uint8_t* actions, int32_t n_steps, const macm_outputs* out, void* stream);
+
 /* Observation of the current state without stepping (Flock.get_obs, mvmnt.py:181-222). */
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream);
 
@@ -404,6 +414,10 @@ int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out,
  * rollout are not known when the check runs).
  */
 int macm_tdm_rollout(macm_tdm* w, const void* actions, int32_t n_steps, const macm_tdm_outputs* out, void* stream);
+
+/* The closed loop `step -> bots.combat -> step` in one launch (as macm_world_rollout_bots);
+ * actions uint8 [E, N, 4] in/out, out->obs and out->mask must be set. */
+int macm_tdm_rollout_bots(macm_tdm* w, uint8_t* actions, int32_t n_steps, const macm_tdm_outputs* out, void* stream);
 
 /* TDM.get_obs of the current state without stepping. */
 int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream);

@@ -135,3 +135,45 @@ def test_tdm_rollout_equals_per_step(teams, K, obs_f64):
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"state[{k}]")
     np.testing.assert_array_equal(a.counters(), b.counters())
     assert int(a.counters()[1]) > 0, "no melee attacks: the combat branch was not exercised"
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (64, 64, 9, {}),
+    (32, 20, 8, {"obs_dtype": torch.float64, "coord": "cartesian"}),
+    (4, 100, 4, {"start_spread": 12}),  # workgroup path: step + bots launches
+])
+def test_flock_closed_loop_rollout_equals_per_step(E, N, K, kw):
+    """macm_world_rollout_bots vs K x (step, bots.flock) launches: same state, outputs and actions."""
+    from gym_macm.bots import flock_actions
+    a = FlockVec(E, n_agents=[N], seed=12, device="cuda:0", start_spread=kw.pop("start_spread", 6), **kw)
+    b = FlockVec(E, n_agents=[N], seed=12, device="cuda:0", start_spread=a.settings.start_spread, **kw)
+    act_a = flock_actions(a.obs)
+    act_b = act_a.clone()
+    for _ in range(K):
+        a.step(act_a)
+        flock_actions(a.obs, out=act_a)
+    b.rollout_bots(act_b, K)
+    assert_same(a, b, "closed-loop rollout")
+    assert torch.equal(act_a, act_b), "the bot's next actions"
+
+
+def test_tdm_closed_loop_rollout_equals_per_step():
+    from gym_macm.bots import combat_actions
+    E, teams, K = 32, [8, 8], 40
+    a = TdmWorld(tdm_config(teams), E, device="cuda:0")
+    b = TdmWorld(tdm_config(teams), E, device="cuda:0")
+    a.reset(3, 0)
+    b.reset(3, 0)
+    act_a = combat_actions(a.obs, a.mask)
+    act_b = act_a.clone()
+    for _ in range(K):
+        a.step(act_a)
+        combat_actions(a.obs, a.mask, out=act_a)
+    b.rollout_bots(act_b, K)
+    for x, y in zip(a.outputs(), b.outputs()):
+        assert torch.equal(x, y)
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"state[{k}]")
+    assert torch.equal(act_a, act_b)
+    assert int(a.counters()[1]) > 0
