@@ -70,12 +70,17 @@ class FlockVec(object):
     def rollout(self, actions):
         """K steps of every env with actions given in advance ([K, E, N, 3] on the device, e.g. a
         random-action rollout), one launch (World.rollout): each env runs its K steps back to back.
-        Same results as K step() calls without autoreset; returns the last step's outputs."""
+        Same results as K step() calls without autoreset; returns the last step's outputs.
+        With ``autoreset`` a step-by-step loop is required (episodes restart between steps)."""
+        if self.autoreset:
+            raise ValueError("rollout steps without autoreset; use step() with autoreset=True")
         return self.world.rollout(actions)
 
     def rollout_bots(self, actions, n_steps):
         """n_steps of the closed loop step -> bots.flock -> step in one launch (World.rollout_bots);
         ``actions`` (uint8 [E, N, 3]) holds the first step's actions on entry, the next on return."""
+        if self.autoreset:
+            raise ValueError("rollout_bots steps without autoreset; use step() with autoreset=True")
         return self.world.rollout_bots(actions, n_steps)
 
     def reset_envs(self, mask=None):
