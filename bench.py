@@ -322,6 +322,8 @@ def main():
                 "launch": (f"one macm_world_rollout{'_bots' if args.policy == 'bots' else ''} launch for the "
                            "K timed steps" if rollout and N <= 64
                            else "one step per launch" if not rollout
+                           else "macm_world_rollout, workgroup path: 2 env slices on streams of their own, 3 "
+                                "launches per step each, no join between steps" if E >= 1024 and N < 512
                            else "macm_world_rollout, workgroup path: 3 launches per step"),
             },
             "roofline": {

@@ -71,6 +71,9 @@ struct macm_world {
   bool mt_valid = false;
   uint32_t* hstat = nullptr;  // host-mapped status word (B.host_status is its device alias)
   unsigned long long* bad = nullptr;  // validate_actions: first failing row (device scratch)
+  // workgroup-path rollouts: env slices on streams of their own (created on first use)
+  std::vector<hipStream_t> slice_streams;
+  std::vector<hipEvent_t> slice_events;  // [0] fork, [1 + s] join of slice s
 };
 
 struct macm_tdm {
@@ -160,6 +163,10 @@ void fill_body_params(StepParams& P, double hz, float radius, float density, flo
 }
 
 void free_world(macm_world* w) {
+  for (hipStream_t st : w->slice_streams) (void)hipStreamDestroy(st);
+  for (hipEvent_t ev : w->slice_events) (void)hipEventDestroy(ev);
+  w->slice_streams.clear();
+  w->slice_events.clear();
   for (void* p : w->allocs) (void)hipFree(p);
   w->allocs.clear();
   if (w->hstat) (void)hipHostFree(w->hstat);
@@ -532,6 +539,84 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
   return MACM_OK;
 }
 
+// Envs [e0, e0 + n) of a world as a world of n envs: every per-env array offset by e0 rows
+// (the sizes macm_world_create allocates), tidx and the status word shared.
+static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, size_t T, size_t C, size_t tcap) {
+  WorldBuffers S = B;
+  const size_t EN = e0 * N, IS = e0 * (N / 2 + 2);
+  auto off = [](auto*& p, size_t n) {
+    if (p) p += n;
+  };
+  off(S.pos, EN), off(S.vel, EN), off(S.angle, EN), off(S.fat, EN), off(S.sleep, EN);
+  off(S.targets, e0 * T);
+  for (int c = 0; c < 2; ++c) off(S.ccount[c], e0), off(S.cab[c], e0 * C), off(S.cimp[c], e0 * C);
+  off(S.step_count, e0), off(S.time_passed, e0), off(S.done, e0), off(S.status, e0);
+  off(S.env_counters, e0 * 4), off(S.stamps, e0 * 32);
+  off(S.scratch, e0 * tcap), off(S.x_cst, e0 * tcap), off(S.x_cimp, e0 * tcap), off(S.x_ord, e0 * tcap);
+  off(S.x_ic, IS), off(S.x_nlvl, e0), off(S.x_ib, IS), off(S.x_ibod, EN), off(S.x_nisl, e0);
+  off(S.x_vmid, EN), off(S.x_cout, EN), off(S.x_vout, EN), off(S.x_deg, EN), off(S.x_isolv, IS);
+  off(S.sp_tab, e0 * C), off(S.sp_adj, e0 * 2 * C), off(S.sp_ord, e0 * C), off(S.sp_cst, e0 * C);
+  off(S.sp_cim, e0 * C), off(S.sp_lam, e0 * C), off(S.spill_count, e0);
+  if (B.sp_rec) S.sp_rec = static_cast<float4*>(B.sp_rec) + EN * 3;  // 48-B records
+  return S;
+}
+
+// Workgroup-path rollout over env slices on streams of their own. The step is three launches whose
+// durations are each set by the slowest env, so the K steps of kSlices env slices run on their own
+// streams with no join between steps: one slice's next kernels fill another's tails. Forked from
+// and joined back into the caller's stream; results are those of the per-step launches (envs are
+// independent). Measured at C3 (4096 x 256, steps 6-25): 568 -> 484 us per step with 2 slices,
+// 481 with 3, but 744 with 4: with the caller's stream that is more streams than the process's 4
+// hardware queues (GPU_MAX_HW_QUEUES), and two slices sharing a queue serialise each other's
+// launches. C5 (N = 1024, 2048 envs) gained nothing (profiles/r02/rollout/).
+static constexpr int kSlices = 2, kSliceMinEnvs = 1024, kSliceMaxAgents = 512;
+static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions, int n_steps,
+                             unsigned long long astride, const macm_outputs* out, hipStream_t user) {
+  const int E = w->P.n_envs, N = w->P.n_agents;
+  if ((int)w->slice_streams.size() < S) {
+    for (int i = (int)w->slice_streams.size(); i < S; ++i) {
+      hipStream_t st;
+      HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      w->slice_streams.push_back(st);
+    }
+  }
+  while ((int)w->slice_events.size() < S + 1) {
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    w->slice_events.push_back(ev);
+  }
+  const size_t od = (size_t)N * obs_dim(w->cfg) * (w->cfg.obs_f64 ? sizeof(double) : sizeof(float));
+  const size_t abytes = astride / (size_t)E;
+  HIP_TRY(hipEventRecord(w->slice_events[0], user));
+  std::vector<StepParams> Ps(S, w->P);
+  std::vector<WorldBuffers> Bs(S);
+  std::vector<size_t> e0s(S);
+  for (int i = 0; i < S; ++i) {
+    const size_t e0 = (size_t)E * i / S, e1 = (size_t)E * (i + 1) / S;
+    e0s[i] = e0;
+    Ps[i].n_envs = (int)(e1 - e0);
+    Bs[i] = slice_buffers(w->B, e0, N, w->P.n_targets, w->P.max_contacts, w->tcap);
+    HIP_TRY(hipStreamWaitEvent(w->slice_streams[i], w->slice_events[0], 0));
+  }
+  for (int k = 0; k < n_steps; ++k) {
+    const int cur = w->cur ^ (k & 1);
+    for (int i = 0; i < S; ++i) {
+      const size_t e0 = e0s[i];
+      auto row = [e0](auto* p, size_t per_env) { return p ? p + e0 * per_env : p; };
+      HIP_TRY(launch_step_wg(Ps[i], Bs[i], cur, w->tcap, actions + k * astride + e0 * abytes,
+                             out->obs ? static_cast<unsigned char*>(out->obs) + e0 * od : nullptr,
+                             w->cfg.obs_f64 != 0, row(out->nbr_id, N), row(out->reward, N), row(out->collided, N),
+                             row(out->done, 1), w->slice_streams[i]));
+    }
+  }
+  for (int i = 0; i < S; ++i) {
+    HIP_TRY(hipEventRecord(w->slice_events[1 + i], w->slice_streams[i]));
+    HIP_TRY(hipStreamWaitEvent(user, w->slice_events[1 + i], 0));
+  }
+  if (n_steps & 1) w->cur ^= 1;
+  return MACM_OK;
+}
+
 int macm_world_rollout(macm_world* w, const void* actions, int n_steps, const macm_outputs* out, void* stream) {
   if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
   if (n_steps == 0) return MACM_OK;  // nothing is read, so actions may be NULL (an empty tensor)
@@ -551,6 +636,9 @@ int macm_world_rollout(macm_world* w, const void* actions, int n_steps, const ma
     HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
                                out->reward, out->collided, out->done, (hipStream_t)stream, n_steps, astride));
     if (n_steps & 1) w->cur ^= 1;
+  } else if (w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents) {
+    return rollout_wg_slices(w, kSlices, static_cast<const unsigned char*>(actions), n_steps, astride, out,
+                             (hipStream_t)stream);
   } else {  // workgroup path: its three launches per step, in order
     for (int k = 0; k < n_steps; ++k) {
       HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, static_cast<const unsigned char*>(actions) + k * astride,

@@ -97,6 +97,26 @@ def test_workgroup_path_rollout_equals_per_step():
     assert_same(a, b, "workgroup rollout")
 
 
+@pytest.mark.parametrize("K", [4, 5])
+def test_workgroup_path_sliced_rollout_equals_per_step(K):
+    """>= 1024 envs on the workgroup path (N < 512): the rollout runs env slices on streams of
+    their own with no join between steps (uneven slices: 1031 envs); twice, so the second rollout
+    starts from the first one's list parity."""
+    E, N = 1031, 100
+    a = FlockVec(E, n_agents=[N], seed=8, device="cuda:0", start_spread=12)
+    b = FlockVec(E, n_agents=[N], seed=8, device="cuda:0", start_spread=12)
+    acts = flock_actions(2 * K, E, N, 6)
+    for k in range(K):
+        a.step(acts[k])
+    b.rollout(acts[:K])
+    assert_same(a, b, "sliced rollout")
+    for k in range(K, 2 * K):
+        a.step(acts[k])
+    b.rollout(acts[K:])
+    assert_same(a, b, "second sliced rollout")
+    assert b.status() == 0
+
+
 def test_rollout_zero_steps_and_validation():
     E, N = 4, 16
     v = FlockVec(E, n_agents=[N], seed=2, device="cuda:0", validate_actions=True)
