@@ -570,6 +570,8 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
 // hardware queues (GPU_MAX_HW_QUEUES), and two slices sharing a queue serialise each other's
 // launches. C5 (N = 1024, 2048 envs) gained nothing (profiles/r02/rollout/).
 static constexpr int kSlices = 2, kSliceMinEnvs = 1024, kSliceMaxAgents = 512;
+// astride == 0: the closed loop (macm_world_rollout_bots): every step of a slice reads the bot's
+// action rows of its envs and the bots kernel writes the next ones from the slice's obs rows.
 static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions, int n_steps,
                              unsigned long long astride, const macm_outputs* out, hipStream_t user) {
   const int E = w->P.n_envs, N = w->P.n_agents;
@@ -586,7 +588,8 @@ static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions,
     w->slice_events.push_back(ev);
   }
   const size_t od = (size_t)N * obs_dim(w->cfg) * (w->cfg.obs_f64 ? sizeof(double) : sizeof(float));
-  const size_t abytes = astride / (size_t)E;
+  const bool bots = astride == 0;
+  const size_t abytes = bots ? 3 * (size_t)N : astride / (size_t)E;
   HIP_TRY(hipEventRecord(w->slice_events[0], user));
   std::vector<StepParams> Ps(S, w->P);
   std::vector<WorldBuffers> Bs(S);
@@ -603,10 +606,13 @@ static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions,
     for (int i = 0; i < S; ++i) {
       const size_t e0 = e0s[i];
       auto row = [e0](auto* p, size_t per_env) { return p ? p + e0 * per_env : p; };
-      HIP_TRY(launch_step_wg(Ps[i], Bs[i], cur, w->tcap, actions + k * astride + e0 * abytes,
-                             out->obs ? static_cast<unsigned char*>(out->obs) + e0 * od : nullptr,
+      unsigned char* obs_i = out->obs ? static_cast<unsigned char*>(out->obs) + e0 * od : nullptr;
+      HIP_TRY(launch_step_wg(Ps[i], Bs[i], cur, w->tcap, actions + k * astride + e0 * abytes, obs_i,
                              w->cfg.obs_f64 != 0, row(out->nbr_id, N), row(out->reward, N), row(out->collided, N),
                              row(out->done, 1), w->slice_streams[i]));
+      if (bots)
+        HIP_TRY(launch_bots_flock(obs_i, w->cfg.obs_f64 != 0, obs_dim(w->cfg), (long long)Ps[i].n_envs * N,
+                                  const_cast<unsigned char*>(actions) + e0 * abytes, w->slice_streams[i]));
     }
   }
   for (int i = 0; i < S; ++i) {
@@ -667,6 +673,8 @@ int macm_world_rollout_bots(macm_world* w, uint8_t* actions, int n_steps, const 
     HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
                                out->reward, out->collided, out->done, s, n_steps, 0));
     if (n_steps & 1) w->cur ^= 1;
+  } else if (w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents) {
+    return rollout_wg_slices(w, kSlices, actions, n_steps, 0, out, s);
   } else {
     const long long rows = (long long)w->P.n_envs * w->P.n_agents;
     for (int k = 0; k < n_steps; ++k) {
