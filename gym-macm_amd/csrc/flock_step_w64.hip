@@ -427,6 +427,195 @@ template <bool B>
 struct BoolC {
   static constexpr bool value = B;
 };
+template <int I>
+struct IntC {
+  static constexpr int value = I;
+};
+
+// Gauss-Seidel levels for 64 < T <= TCAP touching contacts (round 3): contact k of the island
+// order sits in slot k / 64 of lane k % 64 (S = 2 slots up to 128 contacts, 4 up to 256). Levels as
+// in the one-slot path: level(k) = 1 + the level of the last earlier contact sharing a body with k,
+// from one scalar walk in island order, so the contacts of a level share no body and every body
+// takes Box2D's sequence of updates. A level step is branch-free until its stores: every slot
+// reads its two bodies and solves (the S chains interleave), and only the slots of the current
+// level store bodies (exec-masked) and keep their impulses. -DMACM_NO_WIDE_LEVELS: the per-island
+// lanes (one lane walks each island serially through LDS, as in round 2).
+#ifdef MACM_NO_WIDE_LEVELS
+constexpr bool kWideLevels = false;
+#else
+constexpr bool kWideLevels = true;
+#endif
+constexpr int kNoLevel = 0xffff;  // a slot without a contact (or whose island has left the passes)
+
+// S slots per lane; REG: each slot's normal and impulses in registers (S = 2, T <= 128), else read
+// from / written to the touching-contact arrays in LDS at every level step (S = 4: registers for
+// four slots would push the kernel past 96 VGPRs, i.e. below 5 waves per SIMD, for every env)
+struct WideLevels {
+  uint32_t pw[4];      // a | b << 8 | t << 16 (t: touching (list) rank)
+  uint32_t lvis[4];    // level (kNoLevel if none) | island << 16
+  float nx[4], ny[4];  // REG: normal
+  float ln[4], lt[4];  // REG: accumulated normal / tangent impulse
+  int dmax;            // number of levels (wave-uniform)
+
+  __device__ __forceinline__ static int ia(uint32_t w) { return w & 0xffu; }
+  __device__ __forceinline__ static int ib(uint32_t w) { return (w >> 8) & 0xffu; }
+  __device__ __forceinline__ static int it(uint32_t w) { return w >> 16; }
+  __device__ __forceinline__ static int lvl(uint32_t x) { return x & 0xffffu; }
+  __device__ __forceinline__ static int isl(uint32_t x) { return x >> 16; }
+
+  template <int S, bool REG>
+  __device__ __forceinline__ void init(int lane, int Tw, int nisl, const uint8_t* s_ord, const uint32_t* s_tab,
+                                       const float* s_tnx, const float* s_tny, const float* s_tln,
+                                       const float* s_tlt, const uint16_t* s_ic) {
+    uint32_t abq[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const int k = 64 * q + lane;
+      const int t = k < Tw ? (int)s_ord[k] : 0;
+      const uint32_t ab = k < Tw ? s_tab[t] : 0u;
+      abq[q] = (ab & 0xffu) | ((ab >> 8) & 0xff00u);
+      pw[q] = abq[q] | ((uint32_t)t << 16);
+      if constexpr (REG) {
+        nx[q] = s_tnx[t];
+        ny[q] = s_tny[t];
+        ln[q] = s_tln[t];
+        lt[q] = s_tlt[t];
+      }
+    }
+    // levels: scalar walk in island order (lane b of lastv: 1 + the level of the last contact on body b)
+    uint32_t lastv = 0u;
+    int dm = 0;
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      uint32_t lvv = (uint32_t)kNoLevel;
+      const int n = min(64, Tw - 64 * q);
+      for (int kk = 0; kk < n; ++kk) {
+        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane(abq[q], kk);
+        const int a = p & 0xffu, b = p >> 8;
+        const int l = max(__builtin_amdgcn_readlane(lastv, a), __builtin_amdgcn_readlane(lastv, b));
+        lastv = writelane_m0(l + 1, a, lastv);
+        lastv = writelane_m0(l + 1, b, lastv);
+        lvv = writelane_m0(l, kk, lvv);
+        dm = max(dm, l + 1);
+      }
+      lvis[q] = lvv;
+    }
+    dmax = dm;
+    // island of each contact: the islands whose first contact is at or before it
+    const int icv = lane <= nisl ? (int)s_ic[lane] : 0x7fffffff;
+    int is[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) is[q] = 0;
+    for (int I = 1; I < nisl; ++I) {
+      const int c = __builtin_amdgcn_readlane(icv, I);
+#pragma unroll
+      for (int q = 0; q < S; ++q) is[q] += 64 * q + lane >= c ? 1 : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < S; ++q) lvis[q] |= (uint32_t)is[q] << 16;
+  }
+
+  // warm start (pass -1) + vel_iters velocity passes, level by level; then (REG) the impulses to
+  // s_tln / s_tlt
+  template <int S, bool REG>
+  __device__ __forceinline__ void velocity(const StepParams& P, float2* s_v, const float* s_tnx, const float* s_tny,
+                                           float* s_tln, float* s_tlt, float mA, float mB, float kmass,
+                                           float friction) {
+    // One slot at a time, and only the slots with a contact of the current level: a contact update
+    // is ~35 dependent VALU, issued at one per 4 cycles per wave, so a slot's update costs the same
+    // whether or not another slot's runs beside it (measured: two slots interleaved were no faster
+    // than one after the other), and levels grow along the island order, so in most level steps
+    // one slot is busy. The warm-start pass and the velocity passes are separate loops, so that a
+    // level step has no branch before its stores.
+    auto pass = [&](auto warm) {
+      for (int l = 0; l < dmax; ++l) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+          if (S > 1 && __builtin_amdgcn_ballot_w64(lvl(lvis[q]) == l) == 0ull) continue;
+          if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));  // LDS addresses not hoisted (VGPRs)
+          float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
+          float cx, cy, nl, nt;
+          if constexpr (REG) {
+            cx = nx[q];
+            cy = ny[q];
+            nl = ln[q];
+            nt = lt[q];
+          } else {
+            cx = s_tnx[it(pw[q])];
+            cy = s_tny[it(pw[q])];
+            nl = s_tln[it(pw[q])];
+            nt = s_tlt[it(pw[q])];
+          }
+          if constexpr (decltype(warm)::value) warm_start_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB);
+          else solve_velocity_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB, kmass, friction);
+          const bool on = lvl(lvis[q]) == l;
+          if constexpr (REG) {
+            ln[q] = on ? nl : ln[q];
+            lt[q] = on ? nt : lt[q];
+          }
+          if (on) {
+            s_v[ia(pw[q])] = vA;
+            s_v[ib(pw[q])] = vB;
+            if constexpr (!REG) {
+              s_tln[it(pw[q])] = nl;
+              s_tlt[it(pw[q])] = nt;
+            }
+          }
+        }
+        wave_lds_sync();
+      }
+    };
+    if (P.warm_starting) pass(BoolC<true>{});
+    for (int itr = 0; itr < P.vel_iters; ++itr) pass(BoolC<false>{});
+    if constexpr (REG) {
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        if (lvl(lvis[q]) != kNoLevel) {
+          s_tln[it(pw[q])] = ln[q];
+          s_tlt[it(pw[q])] = lt[q];
+        }
+      }
+    }
+  }
+
+  // position passes level by level; an island leaves after the first pass whose minimum separation
+  // (from 0) is >= -3 linearSlop (b2Island::Solve), as in the one-slot level path
+  template <int S>
+  __device__ __forceinline__ void position(const StepParams& P, int lane, int nisl, float2* s_c, int* s_pmin,
+                                           uint8_t* s_isolved, float mA, float mB) {
+    const unsigned long long islm = nisl >= 64 ? ~0ull : ((1ull << nisl) - 1ull);
+    unsigned long long done = 0ull;
+    for (int itr = 0; itr < P.pos_iters && done != islm; ++itr) {
+      if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
+      // an island that has left the passes never returns: its contacts lose their level
+#pragma unroll
+      for (int q = 0; q < S; ++q) lvis[q] |= ((done >> isl(lvis[q])) & 1ull) ? (uint32_t)kNoLevel : 0u;
+      wave_lds_sync();
+      for (int l = 0; l < dmax; ++l) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) {  // one slot at a time, busy slots only, as in the velocity passes
+          if (S > 1 && __builtin_amdgcn_ballot_w64(lvl(lvis[q]) == l) == 0ull) continue;
+          if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));
+          float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
+          const float sep = solve_position_contact(cA.x, cA.y, cB.x, cB.y, P.radius, mA, mB);
+          if (lvl(lvis[q]) == l) {
+            s_c[ia(pw[q])] = cA;
+            s_c[ib(pw[q])] = cB;
+            // order-preserving int of the float for atomicMin
+            const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
+            atomicMin(&s_pmin[isl(lvis[q])], key);
+          }
+        }
+        wave_lds_sync();
+      }
+      int km = lane < nisl ? s_pmin[lane] : 0;
+      km = km >= 0 ? km : (km ^ 0x7fffffff);
+      done |= __builtin_amdgcn_ballot_w64(lane < nisl && !((done >> lane) & 1ull) &&
+                                          __int_as_float(km) >= -3.0f * kLinearSlop);
+    }
+    if (lane < nisl) s_isolved[lane] = (uint8_t)((done >> lane) & 1ull);
+  }
+};
 
 struct SweepState {
   uint32_t ov_lo, ov_hi;  // partner row of this lane's agent (written by lane j = row owner)
@@ -1156,311 +1345,343 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   // of up to KREC contacts run faster one lane each. Only then are the levels computed: a scalar
   // walk of the contacts in island order (lane b of lastv: 1 + the level of the last contact
   // touching body b).
-  lvl_path = lvl_path && __builtin_amdgcn_ballot_w64(lsz > MACM_LEVELS_MIN_ISLAND) != 0ull;
-  if (lvl_path) {
-    const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
-    uint32_t lastv = 0u;
-    for (int k = 0; k < T; ++k) {
-      const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
-      const int a = ab & 0xffffu, bb = ab >> 16;
-      const int l = max(__builtin_amdgcn_readlane(lastv, a), __builtin_amdgcn_readlane(lastv, bb));
-      lastv = writelane_m0(l + 1, a, lastv);
-      lastv = writelane_m0(l + 1, bb, lastv);
-      lvlv = writelane_m0(l, k, lvlv);
+  const bool big_isl = __builtin_amdgcn_ballot_w64(lsz > MACM_LEVELS_MIN_ISLAND) != 0ull;
+  lvl_path = lvl_path && big_isl;
+  // More than 64 touching contacts (converged flocks: islands of 60-100 contacts, tests/gs_depth.py):
+  // the same levels with S = 2 or 4 contacts per lane (WideLevels below); the per-island lanes
+  // would walk such an island serially, ~470 cycles per contact update
+  const bool lvl_wide = kWideLevels && T > 64 && big_isl;
+  const bool skip_isl = lvl_path || lvl_wide;  // no per-island lanes: the level paths solve every island
+  // ---- integrate positions --------------------------------------------------
+  float cx = p.x, cy = p.y;
+  auto integrate_positions = [&]() {
+    if (act) {
+      vx = s_v[lane].x;
+      vy = s_v[lane].y;
+      const float tx = P.dt * vx, ty = P.dt * vy;
+      if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
+        const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
+        vx = vx * ratio;
+        vy = vy * ratio;
+      }
+      cx = cx + P.dt * vx;
+      cy = cy + P.dt * vy;
+      s_c[lane] = make_float2(cx, cy);
     }
-    int isl = 0;  // island of contact `lane`: the islands whose first contact is at or before it
-    for (int I = 1; I < nisl; ++I) isl += (int)s_ic[I] <= lane ? 1 : 0;
-    kislv = (uint32_t)isl;
-  }
-  // level path: lane k holds contact k (island order) for the whole solve
-  const bool lhas = lvl_path && lane < T;
-  const int lvl = (int)lvlv, lisl = (int)kislv;
-  int dmulti = 0;  // levels of the islands with >= 2 contacts (0: only single-contact islands)
-  int lt_ = 0, la = 0, lb = 0;
-  float lnx = 0.0f, lny = 0.0f, lln = 0.0f, llt = 0.0f;
-  if (lvl_path) {
-    const int c0 = lhas ? (int)s_ic[lisl] : 0, c1 = lhas ? (int)s_ic[lisl + 1] : 0;
-    dmulti = wave_max(lhas && c1 - c0 >= 2 ? lvl + 1 : 0);
-    if (lhas) {
-      lt_ = (int)ordv;
-      const uint32_t ab = s_tab[lt_];
-      la = ab & 0xffffu;
-      lb = ab >> 16;
-      lnx = s_tnx[lt_];
-      lny = s_tny[lt_];
-      lln = s_tln[lt_];
-      llt = s_tlt[lt_];
+  };
+  if (lvl_wide) {
+    // the whole solve per slot count, so that the two variants' registers never meet
+    int* s_pmin = reinterpret_cast<int*>(s_imin);  // as in the one-slot level path
+    const int Tw = s_ic[nisl];  // contacts in islands (= T unless TDM's degree cap cut edges)
+    auto wide = [&](auto sc, auto rc) {
+      constexpr int S = decltype(sc)::value;
+      constexpr bool REG = decltype(rc)::value;
+      WideLevels wl;
+      wl.template init<S, REG>(lane, Tw, nisl, s_ord, s_tab, s_tnx, s_tny, s_tln, s_tlt, s_ic);
+      wl.template velocity<S, REG>(P, s_v, s_tnx, s_tny, s_tln, s_tlt, mA, mB, kmass, friction);
+      __syncthreads();
+      STAMP(5);
+      integrate_positions();
+      __syncthreads();
+      STAMP(6);
+      wl.template position<S>(P, lane, nisl, s_c, s_pmin, s_isolved, mA, mB);
+      wave_lds_sync();
+      if (lane < nisl) s_imin[lane] = 0xffffffffu;  // island sleep decision below
+    };
+    if (Tw <= 128) wide(IntC<2>{}, BoolC<true>{});
+    else wide(IntC<4>{}, BoolC<false>{});
+  } else {
+    if (lvl_path) {
+      const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
+      uint32_t lastv = 0u;
+      for (int k = 0; k < T; ++k) {
+        const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
+        const int a = ab & 0xffffu, bb = ab >> 16;
+        const int l = max(__builtin_amdgcn_readlane(lastv, a), __builtin_amdgcn_readlane(lastv, bb));
+        lastv = writelane_m0(l + 1, a, lastv);
+        lastv = writelane_m0(l + 1, bb, lastv);
+        lvlv = writelane_m0(l, k, lvlv);
+      }
+      int isl = 0;  // island of contact `lane`: the islands whose first contact is at or before it
+      for (int I = 1; I < nisl; ++I) isl += (int)s_ic[I] <= lane ? 1 : 0;
+      kislv = (uint32_t)isl;
     }
-  }
-  // between level steps: the next lanes see this step's LDS writes (wave_lds_sync)
-  auto level_sync = [&]() { wave_lds_sync(); };
-  if (lvl_path && dmulti == 0) {  // single-contact islands only: every pass in registers
-    if (lhas) {
-      const float2 vA0 = s_v[la], vB0 = s_v[lb];
-      float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-      if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
-      for (int it = 0; it < P.vel_iters; ++it)
-        solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
-      s_v[la] = make_float2(vAx, vAy);
-      s_v[lb] = make_float2(vBx, vBy);
-    }
-  } else if (lvl_path) {
-    for (int it = P.warm_starting ? -1 : 0; it < P.vel_iters; ++it) {
-      for (int l = 0; l < dmulti; ++l) {
-        if (lhas && lvl == l) {
-          const float2 vA0 = s_v[la], vB0 = s_v[lb];
-          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-          if (it < 0) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
-          else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
-          s_v[la] = make_float2(vAx, vAy);
-          s_v[lb] = make_float2(vBx, vBy);
-        }
-        level_sync();
+    // level path: lane k holds contact k (island order) for the whole solve
+    const bool lhas = lvl_path && lane < T;
+    const int lvl = (int)lvlv, lisl = (int)kislv;
+    int dmulti = 0;  // levels of the islands with >= 2 contacts (0: only single-contact islands)
+    int lt_ = 0, la = 0, lb = 0;
+    float lnx = 0.0f, lny = 0.0f, lln = 0.0f, llt = 0.0f;
+    if (lvl_path) {
+      const int c0 = lhas ? (int)s_ic[lisl] : 0, c1 = lhas ? (int)s_ic[lisl + 1] : 0;
+      dmulti = wave_max(lhas && c1 - c0 >= 2 ? lvl + 1 : 0);
+      if (lhas) {
+        lt_ = (int)ordv;
+        const uint32_t ab = s_tab[lt_];
+        la = ab & 0xffffu;
+        lb = ab >> 16;
+        lnx = s_tnx[lt_];
+        lny = s_tny[lt_];
+        lln = s_tln[lt_];
+        llt = s_tlt[lt_];
       }
     }
-  }
-  if (lhas) {
-    s_tln[lt_] = lln;
-    s_tlt[lt_] = llt;
-  }
-  for (int I = lvl_path ? W : lane; I < nisl; I += W) {
-    const int c0 = s_ic[I], c1 = s_ic[I + 1];
-    if (c1 - c0 == 1 && !krec_wave) {
-      const int t = s_ord[c0];
-      const uint32_t ab = s_tab[t];
-      const int a = ab & 0xffffu, b = ab >> 16;
-      const float nx = s_tnx[t], ny = s_tny[t];
-      float ln = s_tln[t], ltg = s_tlt[t];
-      const float2 vA0 = s_v[a], vB0 = s_v[b];
+    // between level steps: the next lanes see this step's LDS writes (wave_lds_sync)
+    auto level_sync = [&]() { wave_lds_sync(); };
+    if (lvl_path && dmulti == 0) {  // single-contact islands only: every pass in registers
+      if (lhas) {
+        const float2 vA0 = s_v[la], vB0 = s_v[lb];
         float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-      if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB);
-      for (int it = 0; it < P.vel_iters; ++it)
-        solve_velocity_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB, kmass, friction);
-      s_v[a] = make_float2(vAx, vAy);
-      s_v[b] = make_float2(vBx, vBy);
-      s_tln[t] = ln;
-      s_tlt[t] = ltg;
-      continue;
-    }
-    if (c1 - c0 <= KREC) {  // records and impulses in registers, body velocities in LDS (see KREC)
-      const int L = c1 - c0;
-      int rt[KRECA];
-      uint32_t rab_[KRECA];
-      float rnx[KRECA], rny[KRECA], rln[KRECA], rlt[KRECA];
-#pragma unroll
-      for (int q = 0; q < KREC; ++q) rt[q] = q < L ? s_ord[c0 + q] : 0;
-#pragma unroll
-      for (int q = 0; q < KREC; ++q) {
-        rab_[q] = s_tab[rt[q]];
-        rnx[q] = s_tnx[rt[q]];
-        rny[q] = s_tny[rt[q]];
-        rln[q] = s_tln[rt[q]];
-        rlt[q] = s_tlt[rt[q]];
+        if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
+        for (int it = 0; it < P.vel_iters; ++it)
+          solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
+        s_v[la] = make_float2(vAx, vAy);
+        s_v[lb] = make_float2(vBx, vBy);
       }
-      if (P.warm_starting) {
-#pragma unroll
-        for (int q = 0; q < KREC; ++q) {
-          if (q < L) {
-            const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
-            const float2 vA0 = s_v[a], vB0 = s_v[b];
-        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-            warm_start_contact(vAx, vAy, vBx, vBy, rnx[q], rny[q], rln[q], rlt[q], mA, mB);
-            s_v[a] = make_float2(vAx, vAy);
-            s_v[b] = make_float2(vBx, vBy);
+    } else if (lvl_path) {
+      for (int it = P.warm_starting ? -1 : 0; it < P.vel_iters; ++it) {
+        for (int l = 0; l < dmulti; ++l) {
+          if (lhas && lvl == l) {
+            const float2 vA0 = s_v[la], vB0 = s_v[lb];
+            float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+            if (it < 0) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
+            else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
+            s_v[la] = make_float2(vAx, vAy);
+            s_v[lb] = make_float2(vBx, vBy);
           }
+          level_sync();
         }
       }
-      for (int it = 0; it < P.vel_iters; ++it) {
-#pragma unroll
-        for (int q = 0; q < KREC; ++q) {
-          if (q < L) {
-            const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
-            const float2 vA0 = s_v[a], vB0 = s_v[b];
-        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-            solve_velocity_contact(vAx, vAy, vBx, vBy, rnx[q], rny[q], rln[q], rlt[q], mA, mB, kmass, friction);
-            s_v[a] = make_float2(vAx, vAy);
-            s_v[b] = make_float2(vBx, vBy);
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < KREC; ++q) {
-        if (q < L) {
-          s_tln[rt[q]] = rln[q];
-          s_tlt[rt[q]] = rlt[q];
-        }
-      }
-      continue;
     }
-    if (P.warm_starting) {
-      for (int k = c0; k < c1; ++k) {
-        const int t = s_ord[k];
+    if (lhas) {
+      s_tln[lt_] = lln;
+      s_tlt[lt_] = llt;
+    }
+    for (int I = skip_isl ? W : lane; I < nisl; I += W) {
+      const int c0 = s_ic[I], c1 = s_ic[I + 1];
+      if (c1 - c0 == 1 && !krec_wave) {
+        const int t = s_ord[c0];
         const uint32_t ab = s_tab[t];
         const int a = ab & 0xffffu, b = ab >> 16;
-        const float2 vA0 = s_v[a], vB0 = s_v[b];
-        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-        warm_start_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], s_tln[t], s_tlt[t], mA, mB);
-        s_v[a] = make_float2(vAx, vAy);
-        s_v[b] = make_float2(vBx, vBy);
-      }
-    }
-    for (int it = 0; it < P.vel_iters; ++it) {
-      for (int k = c0; k < c1; ++k) {
-        const int t = s_ord[k];
-        const uint32_t ab = s_tab[t];
-        const int a = ab & 0xffffu, b = ab >> 16;
-        const float2 vA0 = s_v[a], vB0 = s_v[b];
-        float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+        const float nx = s_tnx[t], ny = s_tny[t];
         float ln = s_tln[t], ltg = s_tlt[t];
-        solve_velocity_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], ln, ltg, mA, mB, kmass, friction);
+        const float2 vA0 = s_v[a], vB0 = s_v[b];
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+        if (P.warm_starting) warm_start_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB);
+        for (int it = 0; it < P.vel_iters; ++it)
+          solve_velocity_contact(vAx, vAy, vBx, vBy, nx, ny, ln, ltg, mA, mB, kmass, friction);
         s_v[a] = make_float2(vAx, vAy);
         s_v[b] = make_float2(vBx, vBy);
         s_tln[t] = ln;
         s_tlt[t] = ltg;
+        continue;
+      }
+      if (c1 - c0 <= KREC) {  // records and impulses in registers, body velocities in LDS (see KREC)
+        const int L = c1 - c0;
+        int rt[KRECA];
+        uint32_t rab_[KRECA];
+        float rnx[KRECA], rny[KRECA], rln[KRECA], rlt[KRECA];
+  #pragma unroll
+        for (int q = 0; q < KREC; ++q) rt[q] = q < L ? s_ord[c0 + q] : 0;
+  #pragma unroll
+        for (int q = 0; q < KREC; ++q) {
+          rab_[q] = s_tab[rt[q]];
+          rnx[q] = s_tnx[rt[q]];
+          rny[q] = s_tny[rt[q]];
+          rln[q] = s_tln[rt[q]];
+          rlt[q] = s_tlt[rt[q]];
+        }
+        if (P.warm_starting) {
+  #pragma unroll
+          for (int q = 0; q < KREC; ++q) {
+            if (q < L) {
+              const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
+              const float2 vA0 = s_v[a], vB0 = s_v[b];
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+              warm_start_contact(vAx, vAy, vBx, vBy, rnx[q], rny[q], rln[q], rlt[q], mA, mB);
+              s_v[a] = make_float2(vAx, vAy);
+              s_v[b] = make_float2(vBx, vBy);
+            }
+          }
+        }
+        for (int it = 0; it < P.vel_iters; ++it) {
+  #pragma unroll
+          for (int q = 0; q < KREC; ++q) {
+            if (q < L) {
+              const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
+              const float2 vA0 = s_v[a], vB0 = s_v[b];
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+              solve_velocity_contact(vAx, vAy, vBx, vBy, rnx[q], rny[q], rln[q], rlt[q], mA, mB, kmass, friction);
+              s_v[a] = make_float2(vAx, vAy);
+              s_v[b] = make_float2(vBx, vBy);
+            }
+          }
+        }
+  #pragma unroll
+        for (int q = 0; q < KREC; ++q) {
+          if (q < L) {
+            s_tln[rt[q]] = rln[q];
+            s_tlt[rt[q]] = rlt[q];
+          }
+        }
+        continue;
+      }
+      if (P.warm_starting) {
+        for (int k = c0; k < c1; ++k) {
+          const int t = s_ord[k];
+          const uint32_t ab = s_tab[t];
+          const int a = ab & 0xffffu, b = ab >> 16;
+          const float2 vA0 = s_v[a], vB0 = s_v[b];
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+          warm_start_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], s_tln[t], s_tlt[t], mA, mB);
+          s_v[a] = make_float2(vAx, vAy);
+          s_v[b] = make_float2(vBx, vBy);
+        }
+      }
+      for (int it = 0; it < P.vel_iters; ++it) {
+        for (int k = c0; k < c1; ++k) {
+          const int t = s_ord[k];
+          const uint32_t ab = s_tab[t];
+          const int a = ab & 0xffffu, b = ab >> 16;
+          const float2 vA0 = s_v[a], vB0 = s_v[b];
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+          float ln = s_tln[t], ltg = s_tlt[t];
+          solve_velocity_contact(vAx, vAy, vBx, vBy, s_tnx[t], s_tny[t], ln, ltg, mA, mB, kmass, friction);
+          s_v[a] = make_float2(vAx, vAy);
+          s_v[b] = make_float2(vBx, vBy);
+          s_tln[t] = ln;
+          s_tlt[t] = ltg;
+        }
       }
     }
-  }
-  __syncthreads();
-  STAMP(5);
+    __syncthreads();
+    STAMP(5);
+    integrate_positions();
+    __syncthreads();
+    STAMP(6);
 
-  // ---- integrate positions --------------------------------------------------
-  float cx = p.x, cy = p.y;
-  if (act) {
-    vx = s_v[lane].x;
-    vy = s_v[lane].y;
-    const float tx = P.dt * vx, ty = P.dt * vy;
-    if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
-      const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
-      vx = vx * ratio;
-      vy = vy * ratio;
+    // ---- position iterations, one lane per island ------------------------------
+    if (lvl_path) {
+      // per island: the pass's minimum separation (order-preserving int keys); s_imin holds them
+      // until the island sleep decision below re-initialises it (one LDS array fewer keeps 17
+      // waves' LDS per CU: 4096 envs stay a single dispatch round with slack)
+      int* s_pmin = reinterpret_cast<int*>(s_imin);
+      if (dmulti == 0) {  // single-contact islands: lane k runs island k's passes in registers
+        if (lhas) {
+          int solved = 0;
+          const float2 cA0 = s_c[la], cB0 = s_c[lb];
+          float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+          for (int it = 0; it < P.pos_iters; ++it) {
+            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+            if (bmin(0.0f, sep) >= -3.0f * kLinearSlop) {
+              solved = 1;
+              break;
+            }
+          }
+          s_c[la] = make_float2(cAx, cAy);
+          s_c[lb] = make_float2(cBx, cBy);
+          s_isolved[lisl] = (uint8_t)solved;
+        }
+      } else {
+        // passes over the levels; an island leaves after the first pass whose minimum separation
+        // (from 0) is >= -3 linearSlop (b2Island::Solve)
+        const unsigned long long islm = nisl >= 64 ? ~0ull : ((1ull << nisl) - 1ull);
+        unsigned long long done = 0ull;
+        for (int it = 0; it < P.pos_iters && done != islm; ++it) {
+          if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
+          level_sync();
+          for (int l = 0; l < dmulti; ++l) {
+            if (lhas && lvl == l && !((done >> lisl) & 1ull)) {
+              const float2 cA0 = s_c[la], cB0 = s_c[lb];
+              float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+              const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+              s_c[la] = make_float2(cAx, cAy);
+              s_c[lb] = make_float2(cBx, cBy);
+              // order-preserving int of the float for atomicMin
+              const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
+              atomicMin(&s_pmin[lisl], key);
+            }
+            level_sync();
+          }
+          int km = lane < nisl ? s_pmin[lane] : 0;
+          km = km >= 0 ? km : (km ^ 0x7fffffff);
+          done |= __builtin_amdgcn_ballot_w64(lane < nisl && !((done >> lane) & 1ull) &&
+                                              __int_as_float(km) >= -3.0f * kLinearSlop);
+        }
+        if (lane < nisl) s_isolved[lane] = (uint8_t)((done >> lane) & 1ull);
+      }
+      level_sync();
+      if (lane < nisl) s_imin[lane] = 0xffffffffu;  // island sleep decision below
     }
-    cx = cx + P.dt * vx;
-    cy = cy + P.dt * vy;
-    s_c[lane] = make_float2(cx, cy);
-  }
-  __syncthreads();
-  STAMP(6);
-
-  // ---- position iterations, one lane per island ------------------------------
-  if (lvl_path) {
-    // per island: the pass's minimum separation (order-preserving int keys); s_imin holds them
-    // until the island sleep decision below re-initialises it (one LDS array fewer keeps 17
-    // waves' LDS per CU: 4096 envs stay a single dispatch round with slack)
-    int* s_pmin = reinterpret_cast<int*>(s_imin);
-    if (dmulti == 0) {  // single-contact islands: lane k runs island k's passes in registers
-      if (lhas) {
-        int solved = 0;
-        const float2 cA0 = s_c[la], cB0 = s_c[lb];
-        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+    for (int I = skip_isl ? W : lane; I < nisl; I += W) {
+      s_imin[I] = 0xffffffffu;  // island sleep decision below
+      const int c0 = s_ic[I], c1 = s_ic[I + 1];
+      int solved = 0;
+      if (c1 - c0 == 1 && !krec_wave) {  // single contact: registers
+        const uint32_t ab = s_tab[s_ord[c0]];
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const float2 cA0 = s_c[a], cB0 = s_c[b];
+          float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
         for (int it = 0; it < P.pos_iters; ++it) {
           const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-          if (bmin(0.0f, sep) >= -3.0f * kLinearSlop) {
+          const float min_sep = bmin(0.0f, sep);
+          if (min_sep >= -3.0f * kLinearSlop) {
             solved = 1;
             break;
           }
         }
-        s_c[la] = make_float2(cAx, cAy);
-        s_c[lb] = make_float2(cBx, cBy);
-        s_isolved[lisl] = (uint8_t)solved;
-      }
-    } else {
-      // passes over the levels; an island leaves after the first pass whose minimum separation
-      // (from 0) is >= -3 linearSlop (b2Island::Solve)
-      const unsigned long long islm = nisl >= 64 ? ~0ull : ((1ull << nisl) - 1ull);
-      unsigned long long done = 0ull;
-      for (int it = 0; it < P.pos_iters && done != islm; ++it) {
-        if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
-        level_sync();
-        for (int l = 0; l < dmulti; ++l) {
-          if (lhas && lvl == l && !((done >> lisl) & 1ull)) {
-            const float2 cA0 = s_c[la], cB0 = s_c[lb];
-            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-            s_c[la] = make_float2(cAx, cAy);
-            s_c[lb] = make_float2(cBx, cBy);
-            // order-preserving int of the float for atomicMin
-            const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
-            atomicMin(&s_pmin[lisl], key);
-          }
-          level_sync();
-        }
-        int km = lane < nisl ? s_pmin[lane] : 0;
-        km = km >= 0 ? km : (km ^ 0x7fffffff);
-        done |= __builtin_amdgcn_ballot_w64(lane < nisl && !((done >> lane) & 1ull) &&
-                                            __int_as_float(km) >= -3.0f * kLinearSlop);
-      }
-      if (lane < nisl) s_isolved[lane] = (uint8_t)((done >> lane) & 1ull);
-    }
-    level_sync();
-    if (lane < nisl) s_imin[lane] = 0xffffffffu;  // island sleep decision below
-  }
-  for (int I = lvl_path ? W : lane; I < nisl; I += W) {
-    s_imin[I] = 0xffffffffu;  // island sleep decision below
-    const int c0 = s_ic[I], c1 = s_ic[I + 1];
-    int solved = 0;
-    if (c1 - c0 == 1 && !krec_wave) {  // single contact: registers
-      const uint32_t ab = s_tab[s_ord[c0]];
-      const int a = ab & 0xffffu, b = ab >> 16;
-      const float2 cA0 = s_c[a], cB0 = s_c[b];
-        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-      for (int it = 0; it < P.pos_iters; ++it) {
-        const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-        const float min_sep = bmin(0.0f, sep);
-        if (min_sep >= -3.0f * kLinearSlop) {
-          solved = 1;
-          break;
-        }
-      }
-      s_c[a] = make_float2(cAx, cAy);
-      s_c[b] = make_float2(cBx, cBy);
-      s_isolved[I] = (uint8_t)solved;
-      continue;
-    }
-    if (c1 - c0 <= KREC) {  // pairs in registers, body positions in LDS (see KREC)
-      const int L = c1 - c0;
-      uint32_t rab_[KRECA];
-#pragma unroll
-      for (int q = 0; q < KREC; ++q) rab_[q] = s_tab[q < L ? s_ord[c0 + q] : 0];
-      for (int it = 0; it < P.pos_iters; ++it) {
-        float min_sep = 0.0f;
-#pragma unroll
-        for (int q = 0; q < KREC; ++q) {
-          if (q < L) {
-            const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
-            const float2 cA0 = s_c[a], cB0 = s_c[b];
-        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-            min_sep = bmin(min_sep, sep);
-            s_c[a] = make_float2(cAx, cAy);
-            s_c[b] = make_float2(cBx, cBy);
-          }
-        }
-        if (min_sep >= -3.0f * kLinearSlop) {
-          solved = 1;
-          break;
-        }
-      }
-      s_isolved[I] = (uint8_t)solved;
-      continue;
-    }
-    for (int it = 0; it < P.pos_iters; ++it) {
-      float min_sep = 0.0f;
-      for (int k = c0; k < c1; ++k) {
-        const uint32_t ab = s_tab[s_ord[k]];
-        const int a = ab & 0xffffu, b = ab >> 16;
-        const float2 cA0 = s_c[a], cB0 = s_c[b];
-        float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-        const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-        min_sep = bmin(min_sep, sep);
         s_c[a] = make_float2(cAx, cAy);
         s_c[b] = make_float2(cBx, cBy);
+        s_isolved[I] = (uint8_t)solved;
+        continue;
       }
-      if (min_sep >= -3.0f * kLinearSlop) {
-        solved = 1;
-        break;
+      if (c1 - c0 <= KREC) {  // pairs in registers, body positions in LDS (see KREC)
+        const int L = c1 - c0;
+        uint32_t rab_[KRECA];
+  #pragma unroll
+        for (int q = 0; q < KREC; ++q) rab_[q] = s_tab[q < L ? s_ord[c0 + q] : 0];
+        for (int it = 0; it < P.pos_iters; ++it) {
+          float min_sep = 0.0f;
+  #pragma unroll
+          for (int q = 0; q < KREC; ++q) {
+            if (q < L) {
+              const int a = rab_[q] & 0xffffu, b = rab_[q] >> 16;
+              const float2 cA0 = s_c[a], cB0 = s_c[b];
+          float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+              const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+              min_sep = bmin(min_sep, sep);
+              s_c[a] = make_float2(cAx, cAy);
+              s_c[b] = make_float2(cBx, cBy);
+            }
+          }
+          if (min_sep >= -3.0f * kLinearSlop) {
+            solved = 1;
+            break;
+          }
+        }
+        s_isolved[I] = (uint8_t)solved;
+        continue;
       }
+      for (int it = 0; it < P.pos_iters; ++it) {
+        float min_sep = 0.0f;
+        for (int k = c0; k < c1; ++k) {
+          const uint32_t ab = s_tab[s_ord[k]];
+          const int a = ab & 0xffffu, b = ab >> 16;
+          const float2 cA0 = s_c[a], cB0 = s_c[b];
+          float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+          const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+          min_sep = bmin(min_sep, sep);
+          s_c[a] = make_float2(cAx, cAy);
+          s_c[b] = make_float2(cBx, cBy);
+        }
+        if (min_sep >= -3.0f * kLinearSlop) {
+          solved = 1;
+          break;
+        }
+      }
+      s_isolved[I] = (uint8_t)solved;
     }
-    s_isolved[I] = (uint8_t)solved;
+
   }
 
   // After the chain a wave with touching contacts stays above the contact-free ones, and one
