@@ -531,32 +531,29 @@ struct WideLevels {
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {
-          if (S > 1 && __builtin_amdgcn_ballot_w64(lvl(lvis[q]) == l) == 0ull) continue;
-          if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));  // LDS addresses not hoisted (VGPRs)
-          float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
-          float cx, cy, nl, nt;
-          if constexpr (REG) {
-            cx = nx[q];
-            cy = ny[q];
-            nl = ln[q];
-            nt = lt[q];
-          } else {
-            cx = s_tnx[it(pw[q])];
-            cy = s_tny[it(pw[q])];
-            nl = s_tln[it(pw[q])];
-            nt = s_tlt[it(pw[q])];
-          }
-          if constexpr (decltype(warm)::value) warm_start_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB);
-          else solve_velocity_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB, kmass, friction);
-          const bool on = lvl(lvis[q]) == l;
-          if constexpr (REG) {
-            ln[q] = on ? nl : ln[q];
-            lt[q] = on ? nt : lt[q];
-          }
-          if (on) {
+          if (lvl(lvis[q]) == l) {  // exec-masked; a slot with no contact of this level is skipped
+            if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));  // LDS addresses not hoisted (VGPRs)
+            float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
+            float cx, cy, nl, nt;
+            if constexpr (REG) {
+              cx = nx[q];
+              cy = ny[q];
+              nl = ln[q];
+              nt = lt[q];
+            } else {
+              cx = s_tnx[it(pw[q])];
+              cy = s_tny[it(pw[q])];
+              nl = s_tln[it(pw[q])];
+              nt = s_tlt[it(pw[q])];
+            }
+            if constexpr (decltype(warm)::value) warm_start_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB);
+            else solve_velocity_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB, kmass, friction);
             s_v[ia(pw[q])] = vA;
             s_v[ib(pw[q])] = vB;
-            if constexpr (!REG) {
+            if constexpr (REG) {
+              ln[q] = nl;
+              lt[q] = nt;
+            } else {
               s_tln[it(pw[q])] = nl;
               s_tlt[it(pw[q])] = nt;
             }
@@ -594,11 +591,10 @@ struct WideLevels {
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {  // one slot at a time, busy slots only, as in the velocity passes
-          if (S > 1 && __builtin_amdgcn_ballot_w64(lvl(lvis[q]) == l) == 0ull) continue;
-          if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));
-          float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
-          const float sep = solve_position_contact(cA.x, cA.y, cB.x, cB.y, P.radius, mA, mB);
           if (lvl(lvis[q]) == l) {
+            if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));
+            float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
+            const float sep = solve_position_contact(cA.x, cA.y, cB.x, cB.y, P.radius, mA, mB);
             s_c[ia(pw[q])] = cA;
             s_c[ib(pw[q])] = cB;
             // order-preserving int of the float for atomicMin
@@ -1968,8 +1964,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
 #ifdef MACM_ROLLOUT_TU
 // nsteps consecutive steps of env blockIdx.x in one launch (macm_world_rollout): actions of step k
 // at actions + k * astride bytes ([K, E, N, A]), outputs overwritten each step (the last step's
-// remain), counters accumulated. Each env's wave runs its own steps back to back, so no env waits
-// at a launch boundary for the slowest env of the batch. Every step reads only what this wave
+// remain) or, with traj, step k's outputs at row k of [K, ...] buffers (macm_world_rollout_traj),
+// counters accumulated. Each env's wave runs its own steps back to back, so no env waits at a
+// launch boundary for the slowest env of the batch. Every step reads only what this wave
 // wrote in the step before: a workgroup-scope fence completes its stores before the next step's
 // loads; the barrier orders the LDS reuse. This part is compiled in its own translation unit
 // (flock_rollout_w64.hip, -mllvm -disable-machine-licm): with the step inside a loop, machine
@@ -1993,7 +1990,16 @@ struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   // closed loop (macm_world_rollout_bots): every step reads its actions here and the device bot
   // (bots.hpp) writes the next step's from the observation this step wrote; NULL: actions[k]
   uint8_t* policy_act;
+  // trajectory form: every output (and, in the closed loop, the bot's actions: [K + 1, E, N, A],
+  // step k reading row k and writing row k + 1) advances one row per step
+  int traj;
 };
+
+// [K, ...] row k of an output (trajectory form); NULL stays NULL
+template <typename T>
+__device__ __forceinline__ T* traj_row(T* p, size_t k, size_t per_step) {
+  return p ? p + k * per_step : p;
+}
 
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
 __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_rollout_w64(RolloutArgs<OT> A0) {
@@ -2005,25 +2011,37 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
         (const __attribute__((address_space(4))) RolloutArgs<OT>*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(ka));
     const RolloutArgs<OT>& A = *(const RolloutArgs<OT>*)ka;
+    const int N = A.P.n_agents, lane = threadIdx.x;
+    const size_t EN = (size_t)A.P.n_envs * N;
+    const size_t kr = A.traj ? (size_t)k : 0;  // output row of this step
+    const size_t od = MODE == kTdm ? (size_t)(N - 1) * 4 : (A.P.coord == MACM_COORD_CARTESIAN ? 6 : 4);
+    OT* const obs = traj_row(A.obs, kr, EN * od);
+    TdmBuffers TB = A.TB;
+    if constexpr (MODE == kTdm) {
+      TB.mask_out = traj_row(TB.mask_out, kr, EN * (N - 1));
+      TB.health_out = traj_row(TB.health_out, kr, EN);
+      TB.alive_out = traj_row(TB.alive_out, kr, EN);
+      TB.winner_out = traj_row(TB.winner_out, kr, (size_t)A.P.n_envs);
+    }
+    const size_t abytes = MODE == kTdm ? 4 : 3;  // closed loop: uint8 actions per agent
+    uint8_t* const pol_in = A.policy_act ? A.policy_act + kr * EN * abytes : nullptr;
     __builtin_amdgcn_s_setprio(0);  // as at a launch: the chain raises it again
-    step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, A.TB, A.cur ^ (k & 1),
-                                        A.policy_act ? A.policy_act
-                                                     : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
-                                        A.obs, A.nbr_out, A.rew_out, A.coll_out, A.done_out);
+    step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, TB, A.cur ^ (k & 1),
+                                        pol_in ? pol_in : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
+                                        obs, traj_row(A.nbr_out, kr, EN), traj_row(A.rew_out, kr, EN),
+                                        traj_row(A.coll_out, kr, EN), traj_row(A.done_out, kr, (size_t)A.P.n_envs));
     // the next step reads only what this wave wrote: workgroup scope (this CU's L1 and its XCD's L2)
     // suffices; agent scope would write back and invalidate the L2 every step (5x slower, measured)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __syncthreads();
-    if (A.policy_act) {  // every agent row, as the bots kernel over all E x N rows
-      const int N = A.P.n_agents, lane = threadIdx.x;
+    if (pol_in) {  // every agent row, as the bots kernel over all E x N rows
+      uint8_t* const pol_out = A.traj ? pol_in + EN * abytes : pol_in;
       if (lane < N) {
         const size_t row = (size_t)blockIdx.x * N + lane;
         if constexpr (MODE == kTdm)
-          bot_combat_row(A.obs + row * (N - 1) * 4, A.TB.mask_out + row * (N - 1), N, A.policy_act + row * 4);
-        else {
-          const int od = A.P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-          bot_flock_row(A.obs + row * od, od, A.policy_act + row * 3);
-        }
+          bot_combat_row(obs + row * (N - 1) * 4, TB.mask_out + row * (N - 1), N, pol_out + row * 4);
+        else
+          bot_flock_row(obs + row * od, (int)od, pol_out + row * 3);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
@@ -2032,52 +2050,58 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
 }
 
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
-static void launch_roll(int nsteps, unsigned long long astride, hipStream_t s, const StepParams& P,
+static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStream_t s, const StepParams& P,
                         const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
                         void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
   hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s,
-                     RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol});
+                     RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol,
+                                     traj});
 }
 
 // the same instantiation choice as launch_step_w64 / launch_tdm_step_w64
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
-                              int nsteps, unsigned long long astride) {
+                              int nsteps, unsigned long long astride, int traj) {
   const TdmParams TP{};
   const TdmBuffers TB{};
   const bool small = P.n_agents <= 32;
   if (obs_f64) {
     if (small)
-      launch_roll<kFlock, 32, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+      launch_roll<kFlock, 32, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else
-      launch_roll<kFlock, 64, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+      launch_roll<kFlock, 64, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
   } else {
     if (small)
-      launch_roll<kFlock, 32, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+      launch_roll<kFlock, 32, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else if (P.n_envs >= kScalarSweepMinEnvs)
-      launch_roll<kFlock, 64, float, true>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+      launch_roll<kFlock, 64, float, true>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll,
+                                           done);
     else
-      launch_roll<kFlock, 64, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+      launch_roll<kFlock, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
-                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride) {
+                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride, int traj) {
   const bool small = P.n_agents <= 32;
   if (obs_f64) {
     if (small)
-      launch_roll<kTdm, 32, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+      launch_roll<kTdm, 32, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
+                                    nullptr, done);
     else
-      launch_roll<kTdm, 64, double>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+      launch_roll<kTdm, 64, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
+                                    nullptr, done);
   } else {
     if (small)
-      launch_roll<kTdm, 32, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+      launch_roll<kTdm, 32, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
+                                   nullptr, done);
     else
-      launch_roll<kTdm, 64, float>(nsteps, astride, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr, nullptr, done);
+      launch_roll<kTdm, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
+                                   nullptr, done);
   }
   return hipGetLastError();
 }

@@ -19,7 +19,7 @@ hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, 
                            bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
-                              int nsteps, unsigned long long astride);
+                              int nsteps, unsigned long long astride, int traj);
 hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
                            int32_t* nbr, const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
@@ -36,7 +36,7 @@ hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const
                                uint8_t* done, hipStream_t s);
 hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
-                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride);
+                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride, int traj);
 hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                const TdmBuffers& TB, int cur, void* obs, bool obs_f64, const uint8_t* mask,
                                hipStream_t s);
@@ -561,6 +561,21 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
   return S;
 }
 
+// Step k's outputs: row k of [K, ...] buffers in the trajectory form (macm_world_rollout_traj),
+// else the one set every step overwrites.
+static macm_outputs step_outputs(const macm_world* w, const macm_outputs* out, int k, bool traj) {
+  macm_outputs o = *out;
+  if (!traj || k == 0) return o;
+  const size_t E = w->P.n_envs, EN = E * w->P.n_agents;
+  const size_t obytes = EN * obs_dim(w->cfg) * (w->cfg.obs_f64 ? sizeof(double) : sizeof(float));
+  if (o.obs) o.obs = static_cast<unsigned char*>(o.obs) + k * obytes;
+  if (o.nbr_id) o.nbr_id += k * EN;
+  if (o.reward) o.reward += k * EN;
+  if (o.collided) o.collided += k * EN;
+  if (o.done) o.done += k * E;
+  return o;
+}
+
 // Workgroup-path rollout over env slices on streams of their own. The step is three launches whose
 // durations are each set by the slowest env, so the K steps of kSlices env slices run on their own
 // streams with no join between steps: one slice's next kernels fill another's tails. Forked from
@@ -571,9 +586,10 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
 // launches. C5 (N = 1024, 2048 envs) gained nothing (profiles/r02/rollout/).
 static constexpr int kSlices = 2, kSliceMinEnvs = 1024, kSliceMaxAgents = 512;
 // astride == 0: the closed loop (macm_world_rollout_bots): every step of a slice reads the bot's
-// action rows of its envs and the bots kernel writes the next ones from the slice's obs rows.
+// action rows of its envs and the bots kernel writes the next ones from the slice's obs rows
+// (trajectory form: step k reads action row k and writes row k + 1 of [K + 1, E, N, 3]).
 static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions, int n_steps,
-                             unsigned long long astride, const macm_outputs* out, hipStream_t user) {
+                             unsigned long long astride, const macm_outputs* out, bool traj, hipStream_t user) {
   const int E = w->P.n_envs, N = w->P.n_agents;
   if ((int)w->slice_streams.size() < S) {
     for (int i = (int)w->slice_streams.size(); i < S; ++i) {
@@ -590,6 +606,7 @@ static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions,
   const size_t od = (size_t)N * obs_dim(w->cfg) * (w->cfg.obs_f64 ? sizeof(double) : sizeof(float));
   const bool bots = astride == 0;
   const size_t abytes = bots ? 3 * (size_t)N : astride / (size_t)E;
+  const unsigned long long kstride = bots ? (traj ? (unsigned long long)E * abytes : 0ull) : astride;
   HIP_TRY(hipEventRecord(w->slice_events[0], user));
   std::vector<StepParams> Ps(S, w->P);
   std::vector<WorldBuffers> Bs(S);
@@ -601,90 +618,98 @@ static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions,
     Bs[i] = slice_buffers(w->B, e0, N, w->P.n_targets, w->P.max_contacts, w->tcap);
     HIP_TRY(hipStreamWaitEvent(w->slice_streams[i], w->slice_events[0], 0));
   }
-  for (int k = 0; k < n_steps; ++k) {
+  // every launch is enqueued before the join below; a failed launch still joins the slice streams
+  // into the caller's (no unjoined work left behind) and leaves the list parity of
+  // the steps that were launched
+  int rc = MACM_OK, launched = 0;
+  for (int k = 0; k < n_steps && rc == MACM_OK; ++k) {
     const int cur = w->cur ^ (k & 1);
-    for (int i = 0; i < S; ++i) {
+    const macm_outputs ok = step_outputs(w, out, k, traj);
+    for (int i = 0; i < S && rc == MACM_OK; ++i) {
       const size_t e0 = e0s[i];
       auto row = [e0](auto* p, size_t per_env) { return p ? p + e0 * per_env : p; };
-      unsigned char* obs_i = out->obs ? static_cast<unsigned char*>(out->obs) + e0 * od : nullptr;
-      HIP_TRY(launch_step_wg(Ps[i], Bs[i], cur, w->tcap, actions + k * astride + e0 * abytes, obs_i,
-                             w->cfg.obs_f64 != 0, row(out->nbr_id, N), row(out->reward, N), row(out->collided, N),
-                             row(out->done, 1), w->slice_streams[i]));
-      if (bots)
-        HIP_TRY(launch_bots_flock(obs_i, w->cfg.obs_f64 != 0, obs_dim(w->cfg), (long long)Ps[i].n_envs * N,
-                                  const_cast<unsigned char*>(actions) + e0 * abytes, w->slice_streams[i]));
+      unsigned char* obs_i = ok.obs ? static_cast<unsigned char*>(ok.obs) + e0 * od : nullptr;
+      const unsigned char* act_k = actions + k * kstride + e0 * abytes;
+      hipError_t he = launch_step_wg(Ps[i], Bs[i], cur, w->tcap, act_k, obs_i, w->cfg.obs_f64 != 0,
+                                     row(ok.nbr_id, N), row(ok.reward, N), row(ok.collided, N), row(ok.done, 1),
+                                     w->slice_streams[i]);
+      if (he == hipSuccess && bots)
+        he = launch_bots_flock(obs_i, w->cfg.obs_f64 != 0, obs_dim(w->cfg), (long long)Ps[i].n_envs * N,
+                               const_cast<unsigned char*>(act_k) + (traj ? (size_t)E * abytes : 0), w->slice_streams[i]);
+      if (he != hipSuccess) rc = fail(MACM_E_HIP, std::string("rollout launch: ") + hipGetErrorString(he));
     }
+    if (rc == MACM_OK) ++launched;
   }
   for (int i = 0; i < S; ++i) {
     HIP_TRY(hipEventRecord(w->slice_events[1 + i], w->slice_streams[i]));
     HIP_TRY(hipStreamWaitEvent(user, w->slice_events[1 + i], 0));
   }
-  if (n_steps & 1) w->cur ^= 1;
+  if (launched & 1) w->cur ^= 1;
+  return rc;
+}
+
+// macm_world_rollout / _traj (bots = false) and macm_world_rollout_bots / _traj (bots = true)
+static int world_rollout(macm_world* w, const void* actions, int n_steps, const macm_outputs* out, void* stream,
+                         bool bots, bool traj) {
+  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
+  if (n_steps == 0) return MACM_OK;  // nothing is read, so actions may be NULL (an empty tensor)
+  if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
+  if (bots && !out->obs) return fail(MACM_E_INVALID, "out->obs is NULL (the bots act on it)");
+  if (bots && w->cfg.action_mode != MACM_ACTION_DISCRETE) return fail(MACM_E_INVALID, "bots.flock acts in discrete mode");
+  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  const int mode = w->cfg.action_mode == MACM_ACTION_DISCRETE ? 0 : 1;
+  if (w->cfg.validate_actions) {  // every step's actions before any env is stepped (bots: the caller's first)
+    const long long rows = (long long)(bots ? 1 : n_steps) * w->P.n_envs;
+    if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
+    const int rc = check_actions(w->bad, actions, mode, nullptr, (int)rows, w->P.n_agents, s);
+    if (rc) return rc;
+  }
+  const unsigned long long astride =
+      bots ? 0ull
+           : (unsigned long long)w->P.n_envs * w->P.n_agents * (mode == 0 ? 3 * sizeof(uint8_t) : 2 * sizeof(float));
+  if (w->wave) {  // one launch; astride 0: the closed-loop form of the rollout kernel
+    HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
+                               out->collided, out->done, s, n_steps, astride, traj ? 1 : 0));
+    if (n_steps & 1) w->cur ^= 1;
+    return MACM_OK;
+  }
+  const unsigned char* act = static_cast<const unsigned char*>(actions);
+  if (w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents)
+    return rollout_wg_slices(w, kSlices, act, n_steps, astride, out, traj, s);
+  // workgroup path: its three launches per step (and the bot's), in order
+  const long long rows = (long long)w->P.n_envs * w->P.n_agents;
+  const unsigned long long kstride = bots ? (traj ? (unsigned long long)rows * 3 : 0ull) : astride;
+  for (int k = 0; k < n_steps; ++k) {
+    const macm_outputs ok = step_outputs(w, out, k, traj);
+    const unsigned char* act_k = act + k * kstride;
+    HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, act_k, ok.obs, w->cfg.obs_f64 != 0, ok.nbr_id, ok.reward,
+                           ok.collided, ok.done, s));
+    w->cur ^= 1;
+    if (bots)
+      HIP_TRY(launch_bots_flock(ok.obs, w->cfg.obs_f64 != 0, obs_dim(w->cfg), rows,
+                                const_cast<unsigned char*>(act_k) + (traj ? rows * 3 : 0), s));
+  }
   return MACM_OK;
 }
 
 int macm_world_rollout(macm_world* w, const void* actions, int n_steps, const macm_outputs* out, void* stream) {
-  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
-  if (n_steps == 0) return MACM_OK;  // nothing is read, so actions may be NULL (an empty tensor)
-  if (!w || !actions || !out || !out->reward) return fail(MACM_E_INVALID, "world/actions/out/reward is NULL");
-  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
-  DeviceGuard g(w->device);
-  const int mode = w->cfg.action_mode == MACM_ACTION_DISCRETE ? 0 : 1;
-  if (w->cfg.validate_actions) {  // every step's actions before any env is stepped
-    const long long rows = (long long)n_steps * w->P.n_envs;
-    if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
-    const int rc = check_actions(w->bad, actions, mode, nullptr, (int)rows, w->P.n_agents, (hipStream_t)stream);
-    if (rc) return rc;
-  }
-  const unsigned long long astride =
-      (unsigned long long)w->P.n_envs * w->P.n_agents * (mode == 0 ? 3 * sizeof(uint8_t) : 2 * sizeof(float));
-  if (w->wave) {
-    HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
-                               out->reward, out->collided, out->done, (hipStream_t)stream, n_steps, astride));
-    if (n_steps & 1) w->cur ^= 1;
-  } else if (w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents) {
-    return rollout_wg_slices(w, kSlices, static_cast<const unsigned char*>(actions), n_steps, astride, out,
-                             (hipStream_t)stream);
-  } else {  // workgroup path: its three launches per step, in order
-    for (int k = 0; k < n_steps; ++k) {
-      HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, static_cast<const unsigned char*>(actions) + k * astride,
-                             out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward, out->collided, out->done,
-                             (hipStream_t)stream));
-      w->cur ^= 1;
-    }
-  }
-  return MACM_OK;
+  return world_rollout(w, actions, n_steps, out, stream, false, false);
+}
+
+int macm_world_rollout_traj(macm_world* w, const void* actions, int n_steps, const macm_outputs* traj,
+                            void* stream) {
+  return world_rollout(w, actions, n_steps, traj, stream, false, true);
 }
 
 int macm_world_rollout_bots(macm_world* w, uint8_t* actions, int n_steps, const macm_outputs* out, void* stream) {
-  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
-  if (n_steps == 0) return MACM_OK;
-  if (!w || !actions || !out || !out->obs || !out->reward)
-    return fail(MACM_E_INVALID, "world/actions/out/obs/reward is NULL");
-  if (w->cfg.action_mode != MACM_ACTION_DISCRETE) return fail(MACM_E_INVALID, "bots.flock acts in discrete mode");
-  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
-  DeviceGuard g(w->device);
-  hipStream_t s = (hipStream_t)stream;
-  if (w->cfg.validate_actions) {  // the first step's (the caller's); the bot's are in range
-    const int rc = check_actions(w->bad, actions, 0, nullptr, w->P.n_envs, w->P.n_agents, s);
-    if (rc) return rc;
-  }
-  if (w->wave) {  // astride 0: the closed-loop form of the rollout kernel
-    HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
-                               out->reward, out->collided, out->done, s, n_steps, 0));
-    if (n_steps & 1) w->cur ^= 1;
-  } else if (w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents) {
-    return rollout_wg_slices(w, kSlices, actions, n_steps, 0, out, s);
-  } else {
-    const long long rows = (long long)w->P.n_envs * w->P.n_agents;
-    for (int k = 0; k < n_steps; ++k) {
-      HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
-                             out->reward, out->collided, out->done, s));
-      w->cur ^= 1;
-      HIP_TRY(launch_bots_flock(out->obs, w->cfg.obs_f64 != 0, obs_dim(w->cfg), rows, actions, s));
-    }
-  }
-  return MACM_OK;
+  return world_rollout(w, actions, n_steps, out, stream, true, false);
+}
+
+int macm_world_rollout_bots_traj(macm_world* w, uint8_t* actions, int n_steps, const macm_outputs* traj,
+                                 void* stream) {
+  return world_rollout(w, actions, n_steps, traj, stream, true, true);
 }
 
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
@@ -1085,42 +1110,49 @@ int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out,
   return MACM_OK;
 }
 
-int macm_tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
+// macm_tdm_rollout / _traj (bots = false) and macm_tdm_rollout_bots / _traj (bots = true)
+static int tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm_tdm_outputs* out, void* stream,
+                       bool bots, bool traj) {
   if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
   if (n_steps == 0) return MACM_OK;
   if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
-  if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
-  DeviceGuard g(w->device);
-  if (w->cfg.validate_actions) {  // every agent's actions of every step, alive or not (deaths are not known yet)
-    const long long rows = (long long)n_steps * w->P.n_envs;
-    if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
-    const int rc = check_actions(w->bad, actions, 2, nullptr, (int)rows, w->P.n_agents, (hipStream_t)stream);
-    if (rc) return rc;
-  }
-  const TdmBuffers TB = tdm_with_outputs(w, out);
-  const unsigned long long astride = (unsigned long long)w->P.n_envs * w->P.n_agents * 4;
-  HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
-                                 w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream, n_steps, astride));
-  if (n_steps & 1) w->cur ^= 1;
-  return MACM_OK;
-}
-
-int macm_tdm_rollout_bots(macm_tdm* w, uint8_t* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
-  if (n_steps < 0) return fail(MACM_E_INVALID, "n_steps must be >= 0");
-  if (n_steps == 0) return MACM_OK;
-  if (!w || !actions || !out || !out->obs || !out->mask) return fail(MACM_E_INVALID, "tdm/actions/obs/mask is NULL");
+  if ((bots || traj) && !out) return fail(MACM_E_INVALID, "out is NULL");
+  if (bots && (!out->obs || !out->mask)) return fail(MACM_E_INVALID, "out->obs/mask is NULL (the bots act on them)");
   if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
   DeviceGuard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   if (w->cfg.validate_actions) {
-    const int rc = check_actions(w->bad, actions, 2, w->TB.alive, w->P.n_envs, w->P.n_agents, s);
+    // bots: the caller's first step, alive agents; else every agent's actions of every step, alive
+    // or not (deaths are not known yet)
+    const long long rows = (long long)(bots ? 1 : n_steps) * w->P.n_envs;
+    if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
+    const int rc = check_actions(w->bad, actions, 2, bots ? w->TB.alive : nullptr, (int)rows, w->P.n_agents, s);
     if (rc) return rc;
   }
   const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->done,
-                                 s, n_steps, 0));
+  const unsigned long long astride = bots ? 0ull : (unsigned long long)w->P.n_envs * w->P.n_agents * 4;
+  HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
+                                 w->cfg.obs_f64 != 0, out ? out->done : nullptr, s, n_steps, astride, traj ? 1 : 0));
   if (n_steps & 1) w->cur ^= 1;
   return MACM_OK;
+}
+
+int macm_tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
+  return tdm_rollout(w, actions, n_steps, out, stream, false, false);
+}
+
+int macm_tdm_rollout_traj(macm_tdm* w, const void* actions, int n_steps, const macm_tdm_outputs* traj,
+                          void* stream) {
+  return tdm_rollout(w, actions, n_steps, traj, stream, false, true);
+}
+
+int macm_tdm_rollout_bots(macm_tdm* w, uint8_t* actions, int n_steps, const macm_tdm_outputs* out, void* stream) {
+  return tdm_rollout(w, actions, n_steps, out, stream, true, false);
+}
+
+int macm_tdm_rollout_bots_traj(macm_tdm* w, uint8_t* actions, int n_steps, const macm_tdm_outputs* traj,
+                               void* stream) {
+  return tdm_rollout(w, actions, n_steps, traj, stream, true, true);
 }
 
 int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream) {

@@ -190,6 +190,8 @@ SIGNATURES = {
     "macm_world_step": (c_int, [c_void_p, c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_rollout": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmOutputs), c_void_p]),
     "macm_world_rollout_bots": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmOutputs), c_void_p]),
+    "macm_world_rollout_traj": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmOutputs), c_void_p]),
+    "macm_world_rollout_bots_traj": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmOutputs), c_void_p]),
     "macm_world_observe": (c_int, [c_void_p, POINTER(MacmOutputs), c_void_p]),
     "macm_world_get_state": (c_int, [c_void_p, POINTER(MacmState), c_void_p]),
     "macm_world_set_state": (c_int, [c_void_p, POINTER(MacmState), c_void_p]),
@@ -207,6 +209,8 @@ SIGNATURES = {
     "macm_tdm_step": (c_int, [c_void_p, c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_rollout": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_rollout_bots": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_rollout_traj": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmTdmOutputs), c_void_p]),
+    "macm_tdm_rollout_bots_traj": (c_int, [c_void_p, c_void_p, c_int, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_observe": (c_int, [c_void_p, POINTER(MacmTdmOutputs), c_void_p]),
     "macm_tdm_get_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),
     "macm_tdm_set_state": (c_int, [c_void_p, POINTER(MacmTdmState), c_void_p]),
@@ -250,6 +254,6 @@ def check(code: int, fn: str) -> None:
         msg = msg.decode() if msg else ""
         if code == E_OVERFLOW:
             raise MacmOverflowError(code, fn, msg)
-        if code == E_INVALID and fn.endswith(("_step", "_rollout")) and "action space" in msg:
+        if code == E_INVALID and fn.endswith(("_step", "_rollout", "_rollout_traj")) and "action space" in msg:
             raise MacmInvalidActionError(code, fn, msg)
         raise MacmError(code, fn, msg)

@@ -151,6 +151,52 @@ class TdmWorld:
                                            self._stream()), "macm_tdm_rollout")
         return self.outputs()
 
+    _TRAJ_KEYS = ("obs", "mask", "health", "alive", "done", "winner")
+
+    def trajectory_buffers(self, n_steps: int) -> dict:
+        """[n_steps, ...] output buffers for rollout_traj / rollout_bots_traj (reusable across calls)."""
+        K, E, N, d = int(n_steps), self.E, self.N, self.device
+        odt = torch.float64 if self.cfg.obs_f64 else torch.float32
+        return dict(obs=torch.empty((K, E, N, N - 1, 4), dtype=odt, device=d),
+                    mask=torch.empty((K, E, N, N - 1), dtype=torch.uint8, device=d),
+                    health=torch.empty((K, E, N), dtype=torch.float64, device=d),
+                    alive=torch.empty((K, E, N), dtype=torch.uint8, device=d),
+                    done=torch.empty((K, E), dtype=torch.uint8, device=d),
+                    winner=torch.empty((K, E), dtype=torch.int32, device=d))
+
+    def _traj_call(self, fn, name, actions, K, traj):
+        traj = self.trajectory_buffers(K) if traj is None else traj
+        for k, t in traj.items():
+            if t is not None and (t.device != self.device or not t.is_contiguous() or t.shape[0] < K):
+                raise ValueError(f"trajectory buffer {k!r} must be a contiguous [>= {K}, ...] tensor on {self.device}")
+        out = _abi.MacmTdmOutputs(*[_ptr(traj.get(k)) for k in self._TRAJ_KEYS])
+        _abi.check(fn(self.h, _ptr(actions), K, ctypes.byref(out), self._stream()), name)
+        if K > 0:  # the world's own buffers keep the current step's outputs
+            for k in self._TRAJ_KEYS:
+                if traj.get(k) is not None:
+                    getattr(self, k).copy_(traj[k][K - 1])
+        return traj
+
+    def rollout_traj(self, actions: torch.Tensor, traj: dict = None) -> dict:
+        """As rollout(), keeping every step's outputs (macm_tdm_rollout_traj): {obs [K,E,N,N-1,4],
+        mask [K,E,N,N-1], health, alive [K,E,N], done, winner [K,E]}."""
+        if actions.device != self.device or not actions.is_contiguous() or actions.dim() != 4:
+            raise ValueError("actions must be a contiguous [K, E, N, 4] tensor on the world's device")
+        if actions.dtype not in (torch.uint8, torch.int8) or tuple(actions.shape[1:]) != (self.E, self.N, 4):
+            raise ValueError(f"TDM rollout actions must be uint8 [K,{self.E},{self.N},4]")
+        return self._traj_call(self.L.macm_tdm_rollout_traj, "macm_tdm_rollout_traj", actions,
+                               int(actions.shape[0]), traj)
+
+    def rollout_bots_traj(self, actions: torch.Tensor, n_steps: int, traj: dict = None) -> dict:
+        """As rollout_bots(), keeping every step's outputs and actions (macm_tdm_rollout_bots_traj):
+        actions uint8 [n_steps + 1, E, N, 4], row 0 the first step's; step k's bot actions in row k + 1."""
+        K = int(n_steps)
+        if (actions.device != self.device or not actions.is_contiguous() or actions.dtype != torch.uint8
+                or tuple(actions.shape) != (K + 1, self.E, self.N, 4)):
+            raise ValueError(f"actions must be a contiguous uint8 [{K + 1},{self.E},{self.N},4] tensor on the "
+                             "world's device")
+        return self._traj_call(self.L.macm_tdm_rollout_bots_traj, "macm_tdm_rollout_bots_traj", actions, K, traj)
+
     def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
         """Minimal-overhead rollout for timed loops (no validation)."""
         self.L.macm_tdm_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),

@@ -67,20 +67,27 @@ class FlockVec(object):
             self.world.reset_envs(self.world.done)
         return out
 
-    def rollout(self, actions):
+    def rollout(self, actions, trajectory=False, traj=None):
         """K steps of every env with actions given in advance ([K, E, N, 3] on the device, e.g. a
         random-action rollout), one launch (World.rollout): each env runs its K steps back to back.
-        Same results as K step() calls without autoreset; returns the last step's outputs.
-        With ``autoreset`` a step-by-step loop is required (episodes restart between steps)."""
+        Same results as K step() calls without autoreset; returns the last step's outputs, or with
+        ``trajectory=True`` every step's (World.rollout_traj: a dict of [K, ...] tensors, written
+        into ``traj`` if given). With ``autoreset`` a step-by-step loop is required."""
         if self.autoreset:
             raise ValueError("rollout steps without autoreset; use step() with autoreset=True")
+        if trajectory:
+            return self.world.rollout_traj(actions, traj)
         return self.world.rollout(actions)
 
-    def rollout_bots(self, actions, n_steps):
+    def rollout_bots(self, actions, n_steps, trajectory=False, traj=None):
         """n_steps of the closed loop step -> bots.flock -> step in one launch (World.rollout_bots);
-        ``actions`` (uint8 [E, N, 3]) holds the first step's actions on entry, the next on return."""
+        ``actions`` (uint8 [E, N, 3]) holds the first step's actions on entry, the next on return.
+        ``trajectory=True``: actions is [n_steps + 1, E, N, 3] and every step's outputs and actions
+        are kept (World.rollout_bots_traj)."""
         if self.autoreset:
             raise ValueError("rollout_bots steps without autoreset; use step() with autoreset=True")
+        if trajectory:
+            return self.world.rollout_bots_traj(actions, n_steps, traj)
         return self.world.rollout_bots(actions, n_steps)
 
     def reset_envs(self, mask=None):

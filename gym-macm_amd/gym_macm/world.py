@@ -150,6 +150,65 @@ class World:
                                              self._stream()), "macm_world_rollout")
         return self.obs, self.nbr_id, self.reward, self.done
 
+    def trajectory_buffers(self, n_steps: int) -> dict:
+        """[n_steps, ...] output buffers for rollout_traj / rollout_bots_traj (reusable across calls)."""
+        K, E, N = int(n_steps), self.E, self.N
+        odt = torch.float64 if self.cfg.obs_f64 else torch.float32
+        d = self.device
+        return dict(obs=torch.empty((K, E, N, self.OD), dtype=odt, device=d),
+                    nbr_id=torch.empty((K, E, N), dtype=torch.int32, device=d),
+                    reward=torch.empty((K, E, N), dtype=torch.float32, device=d),
+                    collided=torch.empty((K, E, N), dtype=torch.uint8, device=d),
+                    done=torch.empty((K, E), dtype=torch.uint8, device=d))
+
+    def _traj_out(self, traj: dict, K: int):
+        for k, t in traj.items():
+            if t is not None and (t.device != self.device or not t.is_contiguous() or t.shape[0] < K):
+                raise ValueError(f"trajectory buffer {k!r} must be a contiguous [>= {K}, ...] tensor on {self.device}")
+        return _abi.MacmOutputs(*[_ptr(traj.get(k)) for k in ("obs", "nbr_id", "reward", "collided", "done")])
+
+    def _keep_last(self, traj: dict, K: int) -> None:
+        # the world's own buffers keep "the current step's outputs", as after step() / rollout()
+        for k in ("obs", "nbr_id", "reward", "collided", "done"):
+            if traj.get(k) is not None:
+                getattr(self, k).copy_(traj[k][K - 1])
+
+    def rollout_traj(self, actions: torch.Tensor, traj: dict = None) -> dict:
+        """As rollout(), keeping every step's outputs (macm_world_rollout_traj): returns
+        {obs [K,E,N,OD], nbr_id, reward, collided [K,E,N], done [K,E]} — the reference's (obs,
+        rewards) of every env.step (mvmnt.py:140). ``traj``: buffers from trajectory_buffers(K)."""
+        if actions.device != self.device or not actions.is_contiguous() or actions.dim() != 4:
+            raise ValueError("actions must be a contiguous [K, E, N, A] tensor on the world's device")
+        A = 3 if self.cfg.action_mode == _abi.ACTION_DISCRETE else 2
+        ok = actions.dtype in (torch.uint8, torch.int8) if A == 3 else actions.dtype == torch.float32
+        if not ok or tuple(actions.shape[1:]) != (self.E, self.N, A):
+            raise ValueError(f"rollout actions must be [K,{self.E},{self.N},{A}] of the step's action dtype")
+        K = int(actions.shape[0])
+        traj = self.trajectory_buffers(K) if traj is None else traj
+        out = self._traj_out(traj, K)
+        _abi.check(self.L.macm_world_rollout_traj(self.h, _ptr(actions), K, ctypes.byref(out), self._stream()),
+                   "macm_world_rollout_traj")
+        if K > 0:
+            self._keep_last(traj, K)
+        return traj
+
+    def rollout_bots_traj(self, actions: torch.Tensor, n_steps: int, traj: dict = None) -> dict:
+        """As rollout_bots(), keeping every step's outputs and actions (macm_world_rollout_bots_traj):
+        actions uint8 [n_steps + 1, E, N, 3], row 0 the first step's on entry; step k's bot actions
+        land in row k + 1. Returns the trajectory dict of rollout_traj()."""
+        K = int(n_steps)
+        if (actions.device != self.device or not actions.is_contiguous() or actions.dtype != torch.uint8
+                or tuple(actions.shape) != (K + 1, self.E, self.N, 3)):
+            raise ValueError(f"actions must be a contiguous uint8 [{K + 1},{self.E},{self.N},3] tensor on the "
+                             "world's device")
+        traj = self.trajectory_buffers(K) if traj is None else traj
+        out = self._traj_out(traj, K)
+        _abi.check(self.L.macm_world_rollout_bots_traj(self.h, _ptr(actions), K, ctypes.byref(out), self._stream()),
+                   "macm_world_rollout_bots_traj")
+        if K > 0:
+            self._keep_last(traj, K)
+        return traj
+
     def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
         """Minimal-overhead rollout for timed loops (no validation)."""
         self.L.macm_world_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 4
+#define MACM_ABI_VERSION 5
 
 enum {
   MACM_OK = 0,
@@ -338,6 +338,20 @@ int macm_world_rollout(macm_world* w, const void* actions, int32_t n_steps, cons
  */
 int macm_world_rollout_bots(macm_world* w, uint8_t* actions, int32_t n_steps, const macm_outputs* out, void* stream);
 
+/*
+ * Trajectory forms: as macm_world_rollout / macm_world_rollout_bots, but every step's outputs are
+ * kept, as the reference returns (obs, rewards) from every env.step (mvmnt.py:140): each non-NULL
+ * field of `traj` is a [n_steps, ...] buffer whose row k receives step k's outputs
+ * (obs [n_steps, E, N, OD], nbr_id / reward / collided [n_steps, E, N], done [n_steps, E]).
+ * Bots form: actions is [n_steps + 1, E, N, 3]; row 0 holds the first step's actions on entry and
+ * step k writes the bot's actions for step k + 1 into row k + 1, so (obs, action, reward) of every
+ * step stay in HBM. Same results as the per-step calls; one launch on the wave path (ABI 5).
+ */
+int macm_world_rollout_traj(macm_world* w, const void* actions, int32_t n_steps, const macm_outputs* traj,
+                            void* stream);
+int macm_world_rollout_bots_traj(macm_world* w, uint8_t* actions, int32_t n_steps, const macm_outputs* traj,
+                                 void* stream);
+
 /* Observation of the current state without stepping (Flock.get_obs, mvmnt.py:181-222). */
 int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream);
 
@@ -418,6 +432,14 @@ int macm_tdm_rollout(macm_tdm* w, const void* actions, int32_t n_steps, const ma
 /* The closed loop `step -> bots.combat -> step` in one launch (as macm_world_rollout_bots);
  * actions uint8 [E, N, 4] in/out, out->obs and out->mask must be set. */
 int macm_tdm_rollout_bots(macm_tdm* w, uint8_t* actions, int32_t n_steps, const macm_tdm_outputs* out, void* stream);
+
+/* Trajectory forms of the two above (as macm_world_rollout_traj): obs [n_steps, E, N, N-1, 4],
+ * mask [n_steps, E, N, N-1], health / alive [n_steps, E, N], done / winner [n_steps, E]; bots:
+ * actions [n_steps + 1, E, N, 4]. */
+int macm_tdm_rollout_traj(macm_tdm* w, const void* actions, int32_t n_steps, const macm_tdm_outputs* traj,
+                          void* stream);
+int macm_tdm_rollout_bots_traj(macm_tdm* w, uint8_t* actions, int32_t n_steps, const macm_tdm_outputs* traj,
+                               void* stream);
 
 /* TDM.get_obs of the current state without stepping. */
 int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream);

@@ -105,7 +105,7 @@ def test_c3_full_size_4096x256_four_flocks():
 
 
 def test_c5_shard_full_size_2048x1024():
-    flock_full(2048, 1024, 3, max_contacts=16384, n_sample=1)
+    flock_full(2048, 1024, 10, max_contacts=16384, n_sample=1)
 
 
 def test_c4_tdm_full_size_4096x2x16():

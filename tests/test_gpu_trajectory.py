@@ -1,0 +1,161 @@
+"""Trajectory rollouts (macm_world_rollout_traj / _bots_traj, macm_tdm_rollout_traj / _bots_traj):
+K steps in one launch that keep every step's outputs, as the reference returns (obs, rewards) from
+every env.step (gym_macm/envs/mvmnt.py:140; TDM: obs every step, combat.py:184).
+
+The bar: row k of every [K, ...] output equals what step k of K per-step calls returned, bit for
+bit; the state and counters after the rollout equal the per-step path's; the closed-loop form keeps
+every step's bot actions (row k + 1 = bots.flock / bots.combat of step k's observation)."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_rollout import assert_same, flock_actions
+
+pytestmark = pytest.mark.gpu
+
+from gym_macm.bots import combat_actions  # noqa: E402
+from gym_macm.bots import flock_actions as bot_flock  # noqa: E402
+from gym_macm.tdm_world import TdmWorld, tdm_config  # noqa: E402
+from gym_macm.vec import FlockVec  # noqa: E402
+
+KEYS = ("obs", "nbr_id", "reward", "collided", "done")
+
+
+def per_step(vec, acts):
+    rows = {k: [] for k in KEYS}
+    for k in range(acts.shape[0]):
+        vec.step(acts[k])
+        for key in KEYS:
+            rows[key].append(getattr(vec.world, key).clone())
+    return {k: torch.stack(v) for k, v in rows.items()}
+
+
+def assert_traj(ref, traj, ctx):
+    for k in ref:
+        assert traj[k].shape == ref[k].shape, f"{ctx}: {k} shape"
+        assert torch.equal(traj[k], ref[k]), f"{ctx}: {k} (first differing step " \
+            f"{int((traj[k] != ref[k]).reshape(ref[k].shape[0], -1).any(1).nonzero()[0])})"
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (64, 64, 9, {}),
+    (48, 20, 8, {"obs_dtype": torch.float64, "coord": "cartesian"}),
+    (40, 30, 6, {"action_mode": "continuous"}),
+    (8, 64, 10, {"start_spread": 4}),  # dense: the spill step inside the loop
+    (2100, 64, 4, {}),                 # >= 2048 envs: the headline's scalar-sweep instantiation
+    (6, 100, 5, {"start_spread": 12}),  # workgroup path: three launches per step
+    (1031, 100, 4, {"start_spread": 12}),  # workgroup path in env slices on their own streams
+])
+def test_flock_trajectory_equals_per_step(E, N, K, kw):
+    cont = kw.get("action_mode") == "continuous"
+    a = FlockVec(E, n_agents=[N], seed=5, device="cuda:0", **kw)
+    b = FlockVec(E, n_agents=[N], seed=5, device="cuda:0", **kw)
+    acts = flock_actions(K, E, N, 13, cont)
+    ref = per_step(a, acts)
+    traj = b.rollout(acts, trajectory=True)
+    assert_traj(ref, traj, "trajectory")
+    assert_same(a, b, "after the trajectory rollout")  # state, counters, the world's current outputs
+    # into caller buffers, twice (the second starts from the first's list parity)
+    buf = b.world.trajectory_buffers(K)
+    acts2 = flock_actions(K, E, N, 14, cont)
+    ref2 = per_step(a, acts2)
+    b.rollout(acts2, trajectory=True, traj=buf)
+    assert_traj(ref2, buf, "second trajectory")
+    assert_same(a, b, "after the second trajectory rollout")
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (64, 64, 12, {}),
+    (32, 20, 8, {"obs_dtype": torch.float64}),
+    (4, 100, 4, {"start_spread": 12}),
+    (1031, 100, 3, {"start_spread": 12}),
+])
+def test_flock_closed_loop_trajectory(E, N, K, kw):
+    a = FlockVec(E, n_agents=[N], seed=12, device="cuda:0", start_spread=kw.pop("start_spread", 6), **kw)
+    b = FlockVec(E, n_agents=[N], seed=12, device="cuda:0", start_spread=a.settings.start_spread, **kw)
+    act = bot_flock(a.obs)
+    acts_b = torch.empty((K + 1, E, N, 3), dtype=torch.uint8, device="cuda:0")
+    acts_b[0] = act
+    rows_a = [act.clone()]
+    ref = {k: [] for k in KEYS}
+    for _ in range(K):
+        a.step(act)
+        for key in KEYS:
+            ref[key].append(getattr(a.world, key).clone())
+        bot_flock(a.obs, out=act)
+        rows_a.append(act.clone())
+    ref = {k: torch.stack(v) for k, v in ref.items()}
+    traj = b.rollout_bots(acts_b, K, trajectory=True)
+    assert_traj(ref, traj, "closed-loop trajectory")
+    assert torch.equal(acts_b, torch.stack(rows_a)), "every step's bot actions"
+    assert_same(a, b, "after the closed-loop trajectory")
+
+
+def tdm_pair(teams, E, obs_f64=False):
+    a = TdmWorld(tdm_config(teams, obs_f64=obs_f64), E, device="cuda:0")
+    b = TdmWorld(tdm_config(teams, obs_f64=obs_f64), E, device="cuda:0")
+    a.reset(7, 0)
+    b.reset(7, 0)
+    return a, b
+
+
+TKEYS = TdmWorld._TRAJ_KEYS
+
+
+def assert_tdm_state(a, b):
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"state[{k}]")
+    np.testing.assert_array_equal(a.counters(), b.counters())
+
+
+@pytest.mark.parametrize("teams,K,obs_f64", [([16, 16], 9, False), ([8, 8, 8], 10, True)])
+def test_tdm_trajectory_equals_per_step(teams, K, obs_f64):
+    E, N = 48, sum(teams)
+    a, b = tdm_pair(teams, E, obs_f64)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(2)
+    acts = torch.randint(0, 3, (K, E, N, 4), dtype=torch.uint8, device="cuda:0", generator=g)
+    acts[..., 3] = torch.randint(0, 2, (K, E, N), dtype=torch.uint8, device="cuda:0", generator=g)
+    ref = {k: [] for k in TKEYS}
+    for k in range(K):
+        a.step(acts[k])
+        for key, t in zip(TKEYS, a.outputs()):
+            ref[key].append(t.clone())
+    ref = {k: torch.stack(v) for k, v in ref.items()}
+    traj = b.rollout_traj(acts)
+    assert_traj(ref, traj, "TDM trajectory")
+    assert_tdm_state(a, b)
+    assert int(a.counters()[1]) > 0
+
+
+def test_tdm_closed_loop_trajectory():
+    E, teams, K = 32, [8, 8], 30
+    a, b = tdm_pair(teams, E)
+    act = combat_actions(a.obs, a.mask)
+    acts_b = torch.empty((K + 1, E, 16, 4), dtype=torch.uint8, device="cuda:0")
+    acts_b[0] = act
+    rows_a = [act.clone()]
+    ref = {k: [] for k in TKEYS}
+    for _ in range(K):
+        a.step(act)
+        for key, t in zip(TKEYS, a.outputs()):
+            ref[key].append(t.clone())
+        combat_actions(a.obs, a.mask, out=act)
+        rows_a.append(act.clone())
+    ref = {k: torch.stack(v) for k, v in ref.items()}
+    traj = b.rollout_bots_traj(acts_b, K)
+    assert_traj(ref, traj, "TDM closed-loop trajectory")
+    assert torch.equal(acts_b, torch.stack(rows_a))
+    assert_tdm_state(a, b)
+
+
+def test_trajectory_argument_checks():
+    v = FlockVec(4, n_agents=[16], seed=2, device="cuda:0")
+    acts = flock_actions(3, 4, 16, 9)
+    with pytest.raises(ValueError):
+        v.rollout(acts, trajectory=True, traj=v.world.trajectory_buffers(2))  # too few rows
+    with pytest.raises(ValueError):
+        v.rollout_bots(torch.zeros((3, 4, 16, 3), dtype=torch.uint8, device="cuda:0"), 3, trajectory=True)
+    out = v.rollout(acts[:0], trajectory=True)  # K = 0: nothing is stepped
+    assert out["reward"].shape == (0, 4, 16)
