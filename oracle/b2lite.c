@@ -495,7 +495,9 @@ static void find_new_contacts(b2l_world* w) {
     }
   }
   w->move_count = 0;
-  qsort(w->pair_buf, (size_t)w->pair_count, 2 * sizeof(int), pair_less);
+  /* qsort's base must be non-NULL even for 0 elements (the pair buffer is allocated lazily);
+   * found by the sanitizer leg (tools/asan_oracle.sh) */
+  if (w->pair_count > 1) qsort(w->pair_buf, (size_t)w->pair_count, 2 * sizeof(int), pair_less);
   int i = 0;
   while (i < w->pair_count) {
     int a = w->pair_buf[2 * i], b = w->pair_buf[2 * i + 1];

@@ -22,7 +22,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB = os.path.join(HERE, "liboracle_flock.so")
+# MACM_ORACLE_LIB: an alternative build of the same sources, e.g. the sanitizer leg
+# (make -C oracle asan -> oracle/_asan/liboracle_flock.so, tools/asan_oracle.sh)
+LIB = os.environ.get("MACM_ORACLE_LIB") or os.path.join(HERE, "liboracle_flock.so")
 
 def _load_abi():
     # ctypes mirror of include/macm.h, loaded by path so that this module never
