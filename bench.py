@@ -149,6 +149,16 @@ def main():
                          "launches per step either way); step: one launch per step (plus the bot's). A rollout run "
                          "also times the per-step launches on the same window (per_step_launch)")
     ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--total-envs", type=int, default=0,
+                    help="strong scaling: split this many envs over the ranks (contiguous global env ids, "
+                         "BASELINE config 4: 4096 over 8, config 5: 16384 over 8) instead of --envs per GPU; "
+                         "actions are drawn for the whole job, so every env's results are those of a "
+                         "single-process run")
+    ap.add_argument("--trajectory", action="store_true",
+                    help="random policy, rollout launch: keep every step's outputs ([K, E, N, ...] buffers, "
+                         "macm_world_rollout_traj), as the reference returns (obs, rewards) from every env.step")
+    ap.add_argument("--dump-final", default=None,
+                    help="test hook: every rank writes its final state and counters to PATH.rank<r>.npz")
     args = ap.parse_args()
     if args.traffic_json is None:
         args.traffic_json = os.path.join(REPO, "profiles", "pmc_flock_step.json" if args.env == "flock"
@@ -171,26 +181,41 @@ def main():
 
     from gym_macm import dist as gdist
 
-    E, K, W = args.envs, args.steps, args.warmup
+    K, W = args.steps, args.warmup
+    strong = args.total_envs > 0
+    if strong:  # this rank's contiguous share of the job's envs
+        e_off, E = gdist.strong_split(args.total_envs, world, rank)
+    else:  # weak: --envs per GPU
+        E = args.envs
+        e_off = gdist.env_offset(rank, E)
+    if args.trajectory and (args.policy != "random" or args.launch != "rollout" or args.env != "flock"):
+        raise SystemExit("--trajectory times the Flock random-action rollout launch")
     gen = torch.Generator(device=dev)
-    gen.manual_seed(args.seed + 1 + rank)
+    gen.manual_seed(args.seed + 1 + (0 if strong else rank))
+
+    def draw(shape, high=3):  # uniform uint8 in [0, high); strong: the whole job's draw, this rank's rows
+        if not strong:
+            return torch.randint(0, high, shape, dtype=torch.uint8, device=dev, generator=gen)
+        full = torch.randint(0, high, (shape[0], args.total_envs) + tuple(shape[2:]), dtype=torch.uint8, device=dev,
+                             generator=gen)
+        return full[:, e_off:e_off + E].contiguous()
     if args.env == "flock":
         from gym_macm.vec import FlockVec
         N = args.agents
         targets = None if args.flocks <= 1 else [i * args.flocks // N for i in range(N)]
-        vec = FlockVec(E, n_agents=[N], targets=targets, seed=args.seed, env_offset=gdist.env_offset(rank, E),
+        vec = FlockVec(E, n_agents=[N], targets=targets, seed=args.seed, env_offset=e_off,
                        device=dev, obs_dtype=torch.float64 if args.obs_f64 else torch.float32)
         world_h = vec.world
-        acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device=dev, generator=gen)
+        acts = draw((W + K, E, N, 3))
         stride = E * N * 3
     else:
         from gym_macm.tdm_world import TdmWorld, tdm_config
         teams = [int(x) for x in args.teams.split(",")]
         N = sum(teams)
         world_h = TdmWorld(tdm_config(teams, obs_f64=args.obs_f64), E, device=dev)
-        world_h.reset(args.seed, gdist.env_offset(rank, E))
-        acts = torch.randint(0, 3, (W + K, E, N, 4), dtype=torch.uint8, device=dev, generator=gen)
-        acts[..., 3] = torch.randint(0, 2, (W + K, E, N), dtype=torch.uint8, device=dev, generator=gen)
+        world_h.reset(args.seed, e_off)
+        acts = draw((W + K, E, N, 4))
+        acts[..., 3] = draw((W + K, E, N), 2)
         stride = E * N * 4
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -213,6 +238,8 @@ def main():
             world_h.step_raw(loop_ptr, sh_)
             policy()
     rollout = args.launch == "rollout"
+    traj = world_h.trajectory_buffers(K) if args.trajectory else None
+    rname = "macm_world_rollout_traj" if traj is not None else "macm_world_rollout"
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}, "
         f"{'one rollout launch' if rollout else 'one launch per step'}")
 
@@ -239,6 +266,8 @@ def main():
         ev0.record(stream)
         if roll and args.policy == "bots":
             world_h.rollout_bots_raw(loop_ptr, K, sh)
+        elif roll and traj is not None:
+            world_h.rollout_traj_raw(base + W * stride, K, traj, sh)
         elif roll:
             world_h.rollout_raw(base + W * stride, K, sh)
         else:
@@ -257,12 +286,16 @@ def main():
     status = int(gdist.reduce_counters([world_h.status()], device=red_dev, op="max")[0])
     cnt = gdist.reduce_counters(world_h.counters(), device=red_dev)
     elapsed = gdist.reduce_max(elapsed, device=red_dev)
-    total_agent_steps = world * E * N * K
+    total_agent_steps = (args.total_envs if strong else world * E) * N * K
     if args.env == "flock":
         assert int(cnt[0]) == total_agent_steps, (cnt, total_agent_steps)
     if status != 0:
         raise RuntimeError(f"device status bits {status}: a capacity overflowed, results invalid")
     value = total_agent_steps / elapsed
+    if args.dump_final:
+        st = world_h.get_state()
+        np.savez(f"{args.dump_final}.rank{rank}.npz", env_offset=e_off, counters=world_h.counters(),
+                 **{k: v for k, v in st.items() if isinstance(v, np.ndarray)})
 
     if rank == 0:
         # float64 obs: the 4 obs values take 8 B each (Flock +16 B; TDM +16 B per observed agent)
@@ -271,6 +304,7 @@ def main():
         ncap = 32 if N <= 32 else 64
         if args.env == "tdm":
             kname = f"env_{'rollout' if rollout else 'step'}_w64<1, {ncap}, float, false>"
+            scal = "false"
         else:
             # N > 64: the workgroup path's three launches per step (split step; kernel_ms covers all)
             # N > 32 with >= 2048 envs: the scalar-sweep instantiation (flock_step_w64.hip,
@@ -280,12 +314,13 @@ def main():
                      else "flock_step_wg_a + flock_solve_wg + flock_step_wg_c<float>")
         traffic = None
         tj = load_traffic(args.traffic_json)
-        if args.obs_f64:
-            kname = kname.replace("float", "double")
+        if args.obs_f64:  # the scalar sweep exists only in the float32-obs instantiation
+            kname = kname.replace("float", "double").replace("double, true>", "double, false>")
         if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
                 and tj.get("policy", "random") == args.policy):
             # per step (a rollout launch's bytes over its steps), like achieved
             traffic = tj.get("hbm_bytes_per_launch") / tj.get("steps_per_launch", 1)
+        hbm_frac = None if traffic is None else traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
         if args.env == "tdm":
@@ -309,26 +344,37 @@ def main():
             "warmup": W,
             "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",  # the physics; observations per config.obs
             "data": "synthetic",
             "config": {
                 "workload": workload,
-                "envs_per_gpu": E, "n_agents": N, "total_envs": E * world,
+                "envs_per_gpu": E, "n_agents": N,
+                "total_envs": args.total_envs if strong else E * world,
+                "split": (f"strong: {args.total_envs} envs over {world} ranks (this rank: global envs "
+                          f"{e_off}..{e_off + E - 1})") if strong else f"weak: {E} envs per GPU",
                 "parallelism": f"env-sharded x{world} (no data-path collective)"
                                + ("" if world == 1 or args.dist_backend == "nccl" else ", gloo counters (test mode)"),
                 "obs": "float64" if args.obs_f64 else "float32",
-                "launch": (f"one macm_world_rollout{'_bots' if args.policy == 'bots' else ''} launch for the "
-                           "K timed steps" if rollout and N <= 64
+                "launch": (f"one {rname}{'_bots' if args.policy == 'bots' else ''} launch for the K timed steps"
+                           if rollout and N <= 64
                            else "one step per launch" if not rollout
-                           else "macm_world_rollout, workgroup path: 2 env slices on streams of their own, 3 "
-                                "launches per step each, no join between steps" if E >= 1024 and N < 512
-                           else "macm_world_rollout, workgroup path: 3 launches per step"),
+                           else f"{rname}, workgroup path: 2 env slices on streams of their own, 3 launches per "
+                                "step each, no join between steps" if E >= 1024 and N < 512
+                           else f"{rname}, workgroup path: 3 launches per step"),
+                # what the caller gets back: the reference returns (obs, rewards) from every env.step
+                # (mvmnt.py:140); the plain rollout launch overwrites its outputs every step
+                "outputs": ("every step's ([K, E, N, ...] trajectory buffers)" if traj is not None
+                            else "every step's (one launch per step)" if not rollout
+                            else "the last step's (each step overwrites them; counters cover all K steps); "
+                                 "--trajectory keeps every step's"),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                # the PMC-measured HBM bytes over the same time: how far from HBM-bound the kernel is
+                "hbm_frac_measured": hbm_frac,
                 "kernel": kname, "kernel_ms": kernel_ms,  # per step
                 "steps_per_launch": K if (rollout and N <= 64) else 1,
                 "bytes_alg_per_launch": b_alg * E * N,
@@ -345,7 +391,7 @@ def main():
             if args.env == "flock":
                 vec.reset()
             else:
-                world_h.reset(args.seed, gdist.env_offset(rank, E))
+                world_h.reset(args.seed, e_off)
             if args.policy == "bots":
                 policy()  # the first actions from the initial obs again
             el2, ev2 = timed_window(False)

@@ -33,6 +33,15 @@ def shard_slice(rank: int, envs_per_rank: int) -> slice:
     return slice(o, o + envs_per_rank)
 
 
+def strong_split(total_envs: int, world: int, rank: int):
+    """(first global env id, env count) of `rank` when `total_envs` are split over `world` ranks
+    (strong scaling, e.g. BASELINE config 4: 4096 envs over 8 GPUs; config 5: 16384 over 8):
+    contiguous shards, the first total_envs % world ranks one env larger."""
+    base, extra = divmod(int(total_envs), int(world))
+    count = base + (1 if rank < extra else 0)
+    return rank * base + min(rank, extra), count
+
+
 def reduce_counters(counters, device=None, op="sum"):
     """All-reduce an int64 counter vector across ranks (no-op without a process group)."""
     t = torch.as_tensor(np.asarray(counters, np.int64), dtype=torch.int64)

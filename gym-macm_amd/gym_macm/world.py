@@ -209,6 +209,13 @@ class World:
             self._keep_last(traj, K)
         return traj
 
+    def rollout_traj_raw(self, actions_ptr: int, n_steps: int, traj: dict, stream_handle: int) -> None:
+        """Minimal-overhead trajectory rollout for timed loops (no validation); ``traj`` from
+        trajectory_buffers(n_steps)."""
+        out = _abi.MacmOutputs(*[_ptr(traj.get(k)) for k in ("obs", "nbr_id", "reward", "collided", "done")])
+        self.L.macm_world_rollout_traj(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(out),
+                                       ctypes.c_void_p(stream_handle))
+
     def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
         """Minimal-overhead rollout for timed loops (no validation)."""
         self.L.macm_world_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),

@@ -88,3 +88,14 @@ def test_offsets_partition_global_env_ids():
     ids = np.concatenate([np.arange(4 * 8)[gdist.shard_slice(r, 8)] for r in range(4)])
     np.testing.assert_array_equal(ids, np.arange(32))
     assert gdist.env_offset(3, 4096) == 12288
+
+
+@pytest.mark.parametrize("total,world", [(4096, 8), (16384, 8), (301, 2), (7, 3), (5, 8)])
+def test_strong_split_partitions_the_job(total, world):
+    """bench.py --total-envs: contiguous shares covering every global env id once, sizes within 1."""
+    from gym_macm import dist as gdist
+    parts = [gdist.strong_split(total, world, r) for r in range(world)]
+    ids = np.concatenate([np.arange(o, o + n) for o, n in parts])
+    np.testing.assert_array_equal(ids, np.arange(total))
+    sizes = [n for _, n in parts]
+    assert max(sizes) - min(sizes) <= 1

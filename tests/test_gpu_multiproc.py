@@ -42,3 +42,43 @@ def test_two_ranks_sharded_bench(env, extra):
     if env != "tdm":
         assert d["counters"]["agent_steps"] == 2 * E * N * K
     assert d["value"] > 0 and d["ms_per_step"] > 0
+
+
+def _run(cmd):
+    env_vars = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env_vars, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("extra", [[], ["--agents", "100"]])
+def test_strong_split_two_ranks_equal_single_process(tmp_path, extra):
+    """bench.py --total-envs T (BASELINE configs 4 and 5 name totals: 4096 / 16384 envs over 8 GPUs):
+    2 ranks take contiguous shares of T = 301 envs (151 + 150), the actions are the whole job's draw,
+    so every env's final state equals the single-process run of all 301 envs, bit for bit, and the
+    reduced counters equal its counters."""
+    import numpy as np
+    T, K, W = 301, 6, 2
+    base = [os.path.join(REPO, "bench.py"), "--steps", str(K), "--warmup", str(W), "--total-envs", str(T),
+            "--no-cpu-baseline"] + extra
+    one = _run([sys.executable] + base + ["--dump-final", str(tmp_path / "one")])
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + base +
+               ["--gpus", "2", "--dist-backend", "gloo", "--dump-final", str(tmp_path / "two")])
+    for d in (one, two):
+        assert d["scaling"] == "strong" and d["config"]["total_envs"] == T
+    assert two["counters"] == one["counters"]
+    ref = np.load(tmp_path / "one.rank0.npz")
+    seen = 0
+    for r in range(2):
+        part = np.load(tmp_path / f"two.rank{r}.npz")
+        o = int(part["env_offset"])
+        n = part["pos"].shape[0]
+        assert (o, n) == ((0, 151) if r == 0 else (151, 150))
+        for k in ("pos", "vel", "angle", "fat", "sleep", "contact_count", "contact_ab", "contact_imp", "step_count",
+                  "time_passed"):
+            np.testing.assert_array_equal(part[k], ref[k][o:o + n], err_msg=f"rank {r} {k}")
+        seen += n
+    assert seen == T
