@@ -1435,19 +1435,22 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         s_v[lb] = make_float2(vBx, vBy);
       }
     } else if (lvl_path) {
-      for (int it = P.warm_starting ? -1 : 0; it < P.vel_iters; ++it) {
+      // the warm-start pass and the velocity passes as separate loops: no branch inside a level step
+      auto lpass = [&](auto warm) {
         for (int l = 0; l < dmulti; ++l) {
           if (lhas && lvl == l) {
             const float2 vA0 = s_v[la], vB0 = s_v[lb];
             float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-            if (it < 0) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
+            if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
             else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
             s_v[la] = make_float2(vAx, vAy);
             s_v[lb] = make_float2(vBx, vBy);
           }
           level_sync();
         }
-      }
+      };
+      if (P.warm_starting) lpass(BoolC<true>{});
+      for (int it = 0; it < P.vel_iters; ++it) lpass(BoolC<false>{});
     }
     if (lhas) {
       s_tln[lt_] = lln;

@@ -1077,7 +1077,9 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   };
 
   // Warm start and velocity passes. last: the final impulses go straight to list order (g_lam).
-  auto vel_pass = [&](bool warm, bool last) {
+  // warm is a compile-time flag (BoolC-like): no branch inside a level step
+  auto vel_pass = [&](auto warm_c, bool last) {
+    constexpr bool warm = decltype(warm_c)::value;
     if (nch == 0) return;
     Slot cur, nxt;
     load(0, cur);
@@ -1092,7 +1094,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       for (int lv = lv0; lv <= lv1; ++lv) {
         if (mylv == lv) {
           float2 va = s_v[a], vb = s_v[b];
-          if (warm) gs_warm(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB);
+          if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB);
           else gs_velocity(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB, kmass, friction);
           s_v[a] = va;
           s_v[b] = vb;
@@ -1108,8 +1110,8 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       cur = nxt;
     }
   };
-  if (P.warm_starting) vel_pass(true, false);
-  for (int it = 0; it < P.vel_iters; ++it) vel_pass(false, it + 1 == P.vel_iters);
+  if (P.warm_starting) vel_pass(std::true_type{}, false);
+  for (int it = 0; it < P.vel_iters; ++it) vel_pass(std::false_type{}, it + 1 == P.vel_iters);
   if (P.vel_iters == 0)  // StoreImpulses of the (warm-started) impulses as they are
     for (int k = lane; k < nc; k += W) g_lam[xord[k]] = cimp[k];
 
