@@ -357,6 +357,10 @@ def main():
                 "parallelism": f"env-sharded x{world} (no data-path collective)"
                                + ("" if world == 1 or args.dist_backend == "nccl" else ", gloo counters (test mode)"),
                 "obs": "float64" if args.obs_f64 else "float32",
+                # per-env contact-list capacity and spill working-set slots (macm_world_create's
+                # defaults from 1/8 of the device's free memory)
+                "max_contacts": int(world_h.C) if args.env == "flock" else None,
+                "spill_slots": int(world_h.spill_slots) if args.env == "flock" else None,
                 "launch": (f"one {rname}{'_bots' if args.policy == 'bots' else ''} launch for the K timed steps"
                            if rollout and N <= 64
                            else "one step per launch" if not rollout

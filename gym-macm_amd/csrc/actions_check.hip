@@ -44,4 +44,30 @@ hipError_t launch_check_actions(const void* actions, int mode, const uint8_t* al
   return hipGetLastError();
 }
 
+// set_state's contact lists (macm_world_set_state), checked on the device (a host loop
+// over E x C entries): the kernels index a list by its count and its packed pairs, so every env
+// needs 0 <= count <= C and a < b < N in each of its first `count` entries. One block per env; the
+// lowest failing (env << 32 | entry) is kept, entry 0xffffffff for a count out of range.
+// C: row pitch of ab; cap: entries of a row that hold the caller's list (min(C, the caller's stride))
+__global__ void check_lists_kernel(const int32_t* __restrict__ count, const uint32_t* __restrict__ ab, int C, int cap,
+                                   int N, unsigned long long* __restrict__ first_bad) {
+  const int e = blockIdx.x;
+  const int n = count[e];
+  if (n < 0 || n > cap) {
+    if (threadIdx.x == 0) atomicMin(first_bad, ((unsigned long long)e << 32) | 0xffffffffull);
+    return;
+  }
+  const uint32_t* row = ab + (size_t)e * C;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const uint32_t v = row[k], a = v & 0xffffu, b = v >> 16;
+    if (!(a < b && b < (uint32_t)N)) atomicMin(first_bad, ((unsigned long long)e << 32) | (unsigned)k);
+  }
+}
+
+hipError_t launch_check_lists(const int32_t* count, const uint32_t* ab, int E, int C, int cap, int N,
+                              unsigned long long* first_bad, hipStream_t s) {
+  hipLaunchKernelGGL(check_lists_kernel, dim3((unsigned)E), dim3(256), 0, s, count, ab, C, cap, N, first_bad);
+  return hipGetLastError();
+}
+
 }  // namespace macm

@@ -81,15 +81,19 @@ struct WorldBuffers {
   float2* x_vout;                // [E, N]    velocities after the solve (max-translation clamped)
   uint8_t* x_deg;                // [E, N]    body has touching edges
   uint8_t* x_isolv;              // [E, IS]   island position-solved
-  // Spill step (flock_spill.hpp): per-env HBM working set for envs whose touching contacts exceed
-  // the fast kernels' LDS capacities; capacity C = max_contacts (touching contacts are in the list).
-  uint32_t* sp_tab;              // [E, C]    touching contacts in list order (bit 31: DFS visited)
-  uint32_t* sp_adj;              // [E, 2C]   CSR edges (touching-contact indices)
-  uint32_t* sp_ord;              // [E, C]    island order -> touching index
-  float4* sp_cst;                // [E, C]    island-ordered records (ab bits, nx, ny, 0)
-  float2* sp_cim;                // [E, C]    their impulses
-  float2* sp_lam;                // [E, C]    list-order impulses of the touching contacts
-  void* sp_rec;                  // [E, N]    pair-sweep records (48 B) when not in LDS (N > 64)
+  // Spill step (flock_spill.hpp): HBM working set for envs whose touching contacts exceed the fast
+  // kernels' LDS capacities, capacity C = max_contacts per slot (touching contacts are in the list).
+  // S slots: S = E (slot = env) when the memory budget allows, else a pool that a spilling env
+  // takes a slot of for the duration of its spill step (sp_lock, see spill::acquire_slot).
+  uint32_t* sp_tab;              // [S, C]    touching contacts in list order (bit 31: DFS visited)
+  uint32_t* sp_adj;              // [S, 2C]   CSR edges (touching-contact indices)
+  uint32_t* sp_ord;              // [S, C]    island order -> touching index
+  float4* sp_cst;                // [S, C]    island-ordered records (ab bits, nx, ny, 0)
+  float2* sp_cim;                // [S, C]    their impulses
+  float2* sp_lam;                // [S, C]    list-order impulses of the touching contacts
+  void* sp_rec;                  // [S, N]    pair-sweep records (48 B) when not in LDS (N > 64)
+  uint32_t* sp_lock;             // [S]       pool: 0 free, 1 taken; NULL: one slot per env
+  int32_t sp_pool;               // pool size S (0: one slot per env, slot = env)
   uint32_t* spill_count;         // [E]       steps taken by the spill step (macm_world_spilled)
   uint32_t* host_status;         // mapped pinned host word: nonzero once any env set a status bit
 };

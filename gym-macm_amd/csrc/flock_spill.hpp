@@ -111,6 +111,46 @@ __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
   return total;
 }
 
+// The working-set slot of env e. One slot per env (sp_pool == 0): slot e. A pool (the memory budget
+// holds fewer slots than envs, macm_world_create): thread 0 takes a free slot by compare-and-swap,
+// starting at e % S. A holder never waits for anything while it holds a slot (it runs its spill
+// step to the end and releases), so waiting envs always progress; the wait is still bounded
+// (about 1 s), after which the env is not stepped and MACM_ST_SPILL_WAIT is reported. Every access
+// of a slot's arrays writes before it reads, and the release writes the holder's L2 back
+// (agent-scope release), so no stale line of an earlier holder can land over a later one's data.
+constexpr unsigned kSlotSpins = 1u << 17;  // x s_sleep 127 (~8k cycles): ~0.5-1 s
+__device__ __forceinline__ int acquire_slot(const WorldBuffers& B, int e, int* s_slot) {
+  if (B.sp_pool == 0) return e;
+  if (threadIdx.x == 0) {
+    const int S = B.sp_pool;
+    int got = -1;
+    for (unsigned it = 0; got < 0 && it < kSlotSpins; ++it) {
+      for (int k = 0; k < S; ++k) {
+        const int q = (e + k) % S;
+        if (__hip_atomic_load(&B.sp_lock[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+            atomicCAS(&B.sp_lock[q], 0u, 1u) == 0u) {
+          got = q;
+          break;
+        }
+      }
+      if (got < 0) __builtin_amdgcn_s_sleep(127);
+    }
+    *s_slot = got;
+  }
+  __syncthreads();
+  return *s_slot;
+}
+
+__device__ __forceinline__ void release_slot(const WorldBuffers& B, int slot) {
+  if (B.sp_pool == 0) return;
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's stores are done (vmcnt / lgkmcnt 0)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the XCD's L2 written back before the slot is free
+    __hip_atomic_store(&B.sp_lock[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <typename OT>
 __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float best, float rx, float ry, float tdx,
                                           float tdy, float td2) {
@@ -158,17 +198,25 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   uint8_t* s_isolv = (uint8_t*)(lds + L.isolv);
   int* s_scan = (int*)(lds + L.scan);
   int* s_misc = (int*)(lds + L.misc);
+  __syncthreads();  // the caller's last LDS accesses are done before the arrays are reused
+  // the HBM working set of this env's slot, capacity C (touching contacts are a subset of the list)
+  const int slot = acquire_slot(B, e, s_misc + 7);
+  if (slot < 0) {  // the pool stayed full for ~1 s: not stepped, reported
+    if (tid == 0) {
+      B.status[e] |= MACM_ST_SPILL_WAIT;
+      report_status(B, MACM_ST_SPILL_WAIT);
+    }
+    return;
+  }
   Rec* recs;
   if constexpr (RECS_LDS) recs = (Rec*)(lds + L.recs);
-  else recs = (Rec*)B.sp_rec + (size_t)e * N;
-  // per-env HBM working set, capacity C (touching contacts are a subset of the list)
-  uint32_t* g_tab = B.sp_tab + (size_t)e * C;
-  uint32_t* g_adj = B.sp_adj + (size_t)e * 2 * C;
-  uint32_t* g_ord = B.sp_ord + (size_t)e * C;
-  float4* g_cst = B.sp_cst + (size_t)e * C;
-  float2* g_cim = B.sp_cim + (size_t)e * C;
-  float2* g_lam = B.sp_lam + (size_t)e * C;
-  __syncthreads();  // the caller's last LDS accesses are done before the arrays are reused
+  else recs = (Rec*)B.sp_rec + (size_t)slot * N;
+  uint32_t* g_tab = B.sp_tab + (size_t)slot * C;
+  uint32_t* g_adj = B.sp_adj + (size_t)slot * 2 * C;
+  uint32_t* g_ord = B.sp_ord + (size_t)slot * C;
+  float4* g_cst = B.sp_cst + (size_t)slot * C;
+  float2* g_cim = B.sp_cim + (size_t)slot * C;
+  float2* g_lam = B.sp_lam + (size_t)slot * C;
 
   // ---- loads ------------------------------------------------------------------------------
   const uint32_t* cab = B.cab[cur] + (size_t)e * C;
@@ -198,7 +246,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
   for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
   for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0u;
-  if (tid < 8) s_misc[tid] = 0;
+  if (tid < 7) s_misc[tid] = 0;  // [7]: the slot (acquire_slot)
 
   // ---- actions -> angle, force (mvmnt.py:97-129) -------------------------------------------
   float Fx = 0.0f, Fy = 0.0f;
@@ -647,6 +695,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     ec[3] += (unsigned long long)dn;
     if (B.spill_count) B.spill_count[e] += 1u;
   }
+  release_slot(B, slot);
 }
 
 }  // namespace spill

@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,8 @@ int wg_block(int N);
 int wg_lds_bytes(int N, int tcap);
 hipError_t launch_check_actions(const void* actions, int mode, const uint8_t* alive, long long rows,
                                 unsigned long long* first_bad, hipStream_t s);
+hipError_t launch_check_lists(const int32_t* count, const uint32_t* ab, int E, int C, int cap, int N,
+                              unsigned long long* first_bad, hipStream_t s);
 }  // namespace macm
 
 using namespace macm;
@@ -187,21 +190,52 @@ void clear_host_status(uint32_t* h) {
   if (h) __atomic_store_n(h, 0u, __ATOMIC_RELEASE);
 }
 
-// Per-env contact capacity C (see macm_world_create in include/macm.h): every pair when that
-// fits the memory budget (and always for N <= 64, the wave kernel), else the budget's C.
-int64_t default_capacity(int N, int E) {
+// After reset_envs: the init kernel rewrote the reset envs' status, so a set host word becomes the OR
+// of what the envs still carry (0 once every overflowed env was reset; ADVICE r02: it kept the stale
+// bits, and every later step failed). Only then does it synchronise the stream: with the word clear
+// (the normal case, e.g. autoreset every step) reset_envs stays asynchronous.
+int resync_host_status(uint32_t* h, const int32_t* dev_status, int E, hipStream_t s) {
+  if (read_host_status(h) == 0u) return MACM_OK;
+  std::vector<int32_t> st(E);
+  HIP_TRY(hipMemcpyAsync(st.data(), dev_status, E * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  uint32_t acc = 0u;
+  for (int32_t v : st) acc |= (uint32_t)v;
+  if (h) __atomic_store_n(h, acc, __ATOMIC_RELEASE);
+  return MACM_OK;
+}
+
+// Default capacities (macm_world_create in include/macm.h), from a per-world memory budget of
+// 1/8 of the device's free memory at creation (a fixed 8 GiB per world multiplied with
+// the worlds or ranks sharing a device; every world now shrinks what the next one sees), half for
+// the contact lists, half for the spill step's working set:
+//   C = every pair when E * C * 24 B (two lists of pair + impulses) fits the lists' half (always
+//       for N <= 64, the wave kernel), else the largest such C (at least 32 N);
+//   S = spill working-set slots of 48 B per entry (C entries) + 48 B per body: one per env when
+//       they fit the other half, else as many as fit (at least 16), taken by spilling envs in turn.
+struct Capacity {
+  int64_t C;
+  int64_t slots;  // == E: one slot per env
+};
+Capacity default_capacity(int N, int E, int64_t max_contacts, size_t free_bytes) {
   const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
-  if (N <= 64) return all_pairs;
-  const int64_t budget = 8LL << 30, per_entry = 80;  // lists 2 x (4 + 8) B + spill working set 56 B
-  if (all_pairs * per_entry * E <= budget) return all_pairs;
-  int64_t c = budget / (per_entry * E);
-  if (c < 32LL * N) c = 32LL * N;
-  return c < all_pairs ? c : all_pairs;
+  const int64_t budget = std::max<int64_t>((int64_t)(free_bytes / 8), 256LL << 20);
+  const int64_t half = budget / 2;
+  Capacity cap;
+  if (max_contacts > 0) cap.C = max_contacts;
+  else if (N <= 64 || all_pairs * 24 * E <= half) cap.C = all_pairs;
+  else cap.C = std::max<int64_t>(32LL * N, half / (24LL * E));
+  cap.C = std::max<int64_t>(1, std::min(cap.C, all_pairs));
+  const int64_t per_slot = cap.C * 48 + (int64_t)N * 48;
+  cap.slots = std::min<int64_t>(E, std::max<int64_t>(16, half / per_slot));
+  return cap;
 }
 
 // validate_actions (macm_config / macm_tdm_config): run the check kernel and wait for it.
+// rows = n_steps * n_envs for a rollout's [K, E, N, A] actions; n_envs decodes the offending row
+// into (step, env) (the env was reported as step * E + env)
 int check_actions(unsigned long long* bad, const void* actions, int mode, const uint8_t* alive, int E, int N,
-                  hipStream_t s) {
+                  hipStream_t s, int n_envs = 0) {
   HIP_TRY(hipMemsetAsync(bad, 0xff, sizeof(unsigned long long), s));
   HIP_TRY(launch_check_actions(actions, mode, alive, (long long)E * N, bad, s));
   unsigned long long h = ~0ull;
@@ -210,7 +244,11 @@ int check_actions(unsigned long long* bad, const void* actions, int mode, const 
   if (h != ~0ull) {
     const char* space = mode == 0 ? "MultiDiscrete([3, 3, 3])" : mode == 1 ? "Box([-1, -1], [1, 1])"
                                                                            : "MultiDiscrete([3, 3, 3, 2])";
-    return fail(MACM_E_INVALID, "action of env " + std::to_string(h / N) + " agent " + std::to_string(h % N) +
+    const unsigned long long row = h / N;
+    const std::string where = n_envs > 0 && (unsigned long long)E > (unsigned long long)n_envs
+                                  ? "step " + std::to_string(row / n_envs) + " env " + std::to_string(row % n_envs)
+                                  : "env " + std::to_string(row);
+    return fail(MACM_E_INVALID, "action of " + where + " agent " + std::to_string(h % N) +
                                     " is not in the action space " + space + " (no env was stepped)");
   }
   return MACM_OK;
@@ -295,17 +333,17 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       if (targets_idx[i] < 0 || targets_idx[i] >= T) return fail(MACM_E_INVALID, "targets_idx out of range");
       tidx[i] = targets_idx[i];
     }
-  const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
   if (max_contacts < 0) return fail(MACM_E_INVALID, "max_contacts must be >= 0");
-  int64_t C64 = max_contacts > 0 ? (int64_t)max_contacts : default_capacity(N, n_envs);
-  if (C64 > all_pairs) C64 = all_pairs;
-  if (C64 < 1) C64 = 1;
-  const int C = (int)C64;
 
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(MACM_E_INVALID, "device index out of range");
   DeviceGuard g(device);
+  size_t free_bytes = 0, total_bytes = 0;
+  HIP_TRY(hipMemGetInfo(&free_bytes, &total_bytes));
+  const Capacity cap = default_capacity(N, n_envs, max_contacts, free_bytes);
+  const int C = (int)cap.C;
+  const int64_t SL = cap.slots;  // spill working-set slots
 
   macm_world* w = new macm_world();
   w->cfg = c;
@@ -363,11 +401,12 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
                     (rc = dalloc(w, &B.x_vmid, EN)) || (rc = dalloc(w, &B.x_cout, EN)) ||
                     (rc = dalloc(w, &B.x_vout, EN)) || (rc = dalloc(w, &B.x_deg, EN)) ||
                     (rc = dalloc(w, &B.x_isolv, (size_t)n_envs * (N / 2 + 2))))) ||
-      // spill step working set (flock_spill.hpp), capacity C per env
-      (rc = dalloc(w, &B.sp_tab, (size_t)n_envs * C)) || (rc = dalloc(w, &B.sp_adj, (size_t)n_envs * 2 * C)) ||
-      (rc = dalloc(w, &B.sp_ord, (size_t)n_envs * C)) || (rc = dalloc(w, &B.sp_cst, (size_t)n_envs * C)) ||
-      (rc = dalloc(w, &B.sp_cim, (size_t)n_envs * C)) || (rc = dalloc(w, &B.sp_lam, (size_t)n_envs * C)) ||
-      (!w->wave && (rc = dalloc(w, (float4**)&B.sp_rec, EN * 3))) ||  // 48-B records
+      // spill step working set (flock_spill.hpp), capacity C per slot, SL slots
+      (rc = dalloc(w, &B.sp_tab, (size_t)SL * C)) || (rc = dalloc(w, &B.sp_adj, (size_t)SL * 2 * C)) ||
+      (rc = dalloc(w, &B.sp_ord, (size_t)SL * C)) || (rc = dalloc(w, &B.sp_cst, (size_t)SL * C)) ||
+      (rc = dalloc(w, &B.sp_cim, (size_t)SL * C)) || (rc = dalloc(w, &B.sp_lam, (size_t)SL * C)) ||
+      (!w->wave && (rc = dalloc(w, (float4**)&B.sp_rec, (size_t)SL * N * 3))) ||  // 48-B records
+      (SL < n_envs && (rc = dalloc(w, &B.sp_lock, (size_t)SL))) ||
       (rc = dalloc(w, &B.spill_count, (size_t)n_envs)) || (rc = dalloc(w, &w->bad, 1)) ||
       (rc = dalloc(w, &w->mt, (size_t)n_envs * kMtStride)) || (rc = dalloc(w, &w->rmask, (size_t)n_envs))
   ) {
@@ -385,6 +424,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.spill_count, 0, sizeof(uint32_t) * n_envs);
+  B.sp_pool = SL < n_envs ? (int32_t)SL : 0;
+  if (e == hipSuccess && B.sp_lock) e = hipMemset(B.sp_lock, 0, sizeof(uint32_t) * SL);
   if (e == hipSuccess && !w->wave) {
     hipDeviceProp_t prop;
     e = hipGetDeviceProperties(&prop, device);
@@ -422,7 +463,7 @@ int macm_world_info_get(const macm_world* w, macm_world_info* info) {
   info->max_contacts = w->P.max_contacts;
   info->max_touching = w->tcap;
   info->device = w->device;
-  info->_pad = 0;
+  info->spill_slots = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;
   return MACM_OK;
 }
 
@@ -507,7 +548,7 @@ int macm_world_reset_envs(macm_world* w, const uint8_t* env_mask, const macm_out
   D.start_y = w->cfg.start_point[1];
   HIP_TRY(launch_draw_poses(w->rmask, w->mt, D, w->P.n_envs, w->B.pos, w->B.angle, s));
   HIP_TRY(launch_init(w, out, w->rmask, s));
-  return MACM_OK;
+  return resync_host_status(w->hstat, w->B.status, w->P.n_envs, s);
 }
 
 static int overflow_error(uint32_t st) {
@@ -515,6 +556,7 @@ static int overflow_error(uint32_t st) {
   if (st & MACM_ST_CONTACT_OVERFLOW) what += " contact-list capacity (max_contacts);";
   if (st & MACM_ST_TOUCH_OVERFLOW) what += " touching-contact capacity;";
   if (st & MACM_ST_DEGREE_OVERFLOW) what += " per-body contact capacity;";
+  if (st & MACM_ST_SPILL_WAIT) what += " spill working-set pool (a dense env waited ~1 s for a slot);";
   return fail(MACM_E_OVERFLOW, "an env outgrew its" + what +
                                    " the results since that step are not the reference's (status bits " +
                                    std::to_string(st) + "; reset, place or set_state clears them)");
@@ -555,9 +597,12 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
   off(S.scratch, e0 * tcap), off(S.x_cst, e0 * tcap), off(S.x_cimp, e0 * tcap), off(S.x_ord, e0 * tcap);
   off(S.x_ic, IS), off(S.x_nlvl, e0), off(S.x_ib, IS), off(S.x_ibod, EN), off(S.x_nisl, e0);
   off(S.x_vmid, EN), off(S.x_cout, EN), off(S.x_vout, EN), off(S.x_deg, EN), off(S.x_isolv, IS);
-  off(S.sp_tab, e0 * C), off(S.sp_adj, e0 * 2 * C), off(S.sp_ord, e0 * C), off(S.sp_cst, e0 * C);
-  off(S.sp_cim, e0 * C), off(S.sp_lam, e0 * C), off(S.spill_count, e0);
-  if (B.sp_rec) S.sp_rec = static_cast<float4*>(B.sp_rec) + EN * 3;  // 48-B records
+  off(S.spill_count, e0);
+  if (B.sp_pool == 0) {  // one working-set slot per env: the slice's rows; a pool is shared as it is
+    off(S.sp_tab, e0 * C), off(S.sp_adj, e0 * 2 * C), off(S.sp_ord, e0 * C), off(S.sp_cst, e0 * C);
+    off(S.sp_cim, e0 * C), off(S.sp_lam, e0 * C);
+    if (B.sp_rec) S.sp_rec = static_cast<float4*>(B.sp_rec) + EN * 3;  // 48-B records
+  }
   return S;
 }
 
@@ -663,7 +708,7 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
   if (w->cfg.validate_actions) {  // every step's actions before any env is stepped (bots: the caller's first)
     const long long rows = (long long)(bots ? 1 : n_steps) * w->P.n_envs;
     if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
-    const int rc = check_actions(w->bad, actions, mode, nullptr, (int)rows, w->P.n_agents, s);
+    const int rc = check_actions(w->bad, actions, mode, nullptr, (int)rows, w->P.n_agents, s, w->P.n_envs);
     if (rc) return rc;
   }
   const unsigned long long astride =
@@ -722,40 +767,73 @@ int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
   return MACM_OK;
 }
 
-// set_state: the kernels index a list by its count and its packed pairs (cab + e*C, LDS arrays
-// by body index), so only lists with 0 <= count <= C and a < b < N in every entry are accepted.
-static int validate_lists(const void* count, const void* ab, size_t E, size_t C, int N, hipStream_t s) {
-  if (!count && !ab) return MACM_OK;
-  if (!count || !ab) return fail(MACM_E_INVALID, "contact_count and contact_ab must be given together");
-  std::vector<int32_t> cnt(E);
-  std::vector<uint32_t> lst(E * C);
-  HIP_TRY(hipMemcpyAsync(cnt.data(), count, E * sizeof(int32_t), hipMemcpyDefault, s));
-  HIP_TRY(hipMemcpyAsync(lst.data(), ab, E * C * sizeof(uint32_t), hipMemcpyDefault, s));
+// Rows of E contact lists between the caller's [E, stride] layout and the world's [E, C] buffers:
+// the first min(stride, C) entries of each row (the rest of a device row is never read, the rest
+// of a caller's row is left as it is).
+static hipError_t copy_rows(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t E,
+                            hipStream_t s) {
+  if (E == 0 || width == 0) return hipSuccess;
+  return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, E, hipMemcpyDefault, s);
+}
+
+// set_state's contact lists: staged in the spare list buffer (cur ^ 1: the next step's output, unused
+// between steps) and validated there on the device (a host loop over E x C entries).
+// On success the caller flips its `cur` to take them; on failure nothing of the world changed.
+static int stage_lists(WorldBuffers& B, int cur, unsigned long long* bad, size_t E, size_t C, size_t Cs, int N,
+                       const void* count, const void* ab, const void* imp, hipStream_t s) {
+  const int nb = cur ^ 1;
+  const size_t Cw = Cs < C ? Cs : C;
+  HIP_TRY(hipMemcpyAsync(B.ccount[nb], count, E * sizeof(int32_t), hipMemcpyDefault, s));
+  HIP_TRY(copy_rows(B.cab[nb], C * sizeof(uint32_t), ab, Cs * sizeof(uint32_t), Cw * sizeof(uint32_t), E, s));
+  HIP_TRY(hipMemsetAsync(bad, 0xff, sizeof(unsigned long long), s));
+  HIP_TRY(launch_check_lists(B.ccount[nb], B.cab[nb], (int)E, (int)C, (int)Cw, N, bad, s));
+  unsigned long long h = ~0ull;
+  HIP_TRY(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  for (size_t e = 0; e < E; ++e) {
-    if (cnt[e] < 0 || (size_t)cnt[e] > C)
-      return fail(MACM_E_INVALID, "env " + std::to_string(e) + ": contact_count " + std::to_string(cnt[e]) +
-                                      " outside [0, max_contacts = " + std::to_string(C) + "]");
-    for (int k = 0; k < cnt[e]; ++k) {
-      const uint32_t v = lst[e * C + k], a = v & 0xffffu, b = v >> 16;
-      if (!(a < b && b < (uint32_t)N))
-        return fail(MACM_E_INVALID, "env " + std::to_string(e) + ": contact_ab[" + std::to_string(k) +
-                                        "] is not a pair a < b < n_agents");
-    }
+  if (h != ~0ull) {
+    const unsigned long long e = h >> 32, k = h & 0xffffffffull;
+    if (k == 0xffffffffull)
+      return fail(MACM_E_INVALID, "env " + std::to_string(e) + ": contact_count outside [0, min(max_contacts = " +
+                                      std::to_string(C) + ", contact_stride = " + std::to_string(Cs) + ")]");
+    return fail(MACM_E_INVALID, "env " + std::to_string(e) + ": contact_ab[" + std::to_string(k) +
+                                    "] is not a pair a < b < n_agents");
   }
+  if (imp)
+    HIP_TRY(copy_rows(B.cimp[nb], C * sizeof(float2), imp, Cs * sizeof(float2), Cw * sizeof(float2), E, s));
+  else
+    HIP_TRY(hipMemsetAsync(B.cimp[nb], 0, E * C * sizeof(float2), s));
   return MACM_OK;
 }
 
 static int copy_state(macm_world* w, const macm_state* st, void* stream, bool to_device) {
   if (!w || !st) return fail(MACM_E_INVALID, "world/state is NULL");
+  if (st->contact_stride < 0) return fail(MACM_E_INVALID, "contact_stride must be >= 0");
   DeviceGuard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   const size_t E = w->P.n_envs, N = w->P.n_agents, T = w->P.n_targets, C = w->P.max_contacts;
+  const size_t Cs = st->contact_stride > 0 ? (size_t)st->contact_stride : C;  // the caller's row length
+  const size_t Cw = Cs < C ? Cs : C;                                           // entries moved per row
   if (to_device) {
-    if (const int rc = validate_lists(st->contact_count, st->contact_ab, E, C, (int)N, s)) return rc;
+    if (!st->contact_count != !st->contact_ab)
+      return fail(MACM_E_INVALID, "contact_count and contact_ab must be given together");
+    if (st->contact_count) {
+      const int rc = stage_lists(w->B, w->cur, w->bad, E, C, Cs, (int)N, st->contact_count, st->contact_ab,
+                                 st->contact_imp, s);
+      if (rc) return rc;
+      w->cur ^= 1;
+    }
     HIP_TRY(hipStreamSynchronize(s));
     clear_host_status(w->hstat);  // an injected state starts clean
     HIP_TRY(hipMemsetAsync(w->B.status, 0, E * sizeof(int32_t), s));
+  } else {
+    if (st->contact_count)
+      HIP_TRY(hipMemcpyAsync(st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t), hipMemcpyDefault, s));
+    if (st->contact_ab)
+      HIP_TRY(copy_rows(st->contact_ab, Cs * sizeof(uint32_t), w->B.cab[w->cur], C * sizeof(uint32_t),
+                        Cw * sizeof(uint32_t), E, s));
+    if (st->contact_imp)
+      HIP_TRY(copy_rows(st->contact_imp, Cs * sizeof(float2), w->B.cimp[w->cur], C * sizeof(float2),
+                        Cw * sizeof(float2), E, s));
   }
   struct Item {
     void* user;
@@ -768,9 +846,6 @@ static int copy_state(macm_world* w, const macm_state* st, void* stream, bool to
       {st->fat, w->B.fat, E * N * sizeof(float4)},
       {st->sleep, w->B.sleep, E * N * sizeof(float)},
       {st->targets, w->B.targets, E * T * sizeof(float2)},
-      {st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t)},
-      {st->contact_ab, w->B.cab[w->cur], E * C * sizeof(uint32_t)},
-      {st->contact_imp, w->B.cimp[w->cur], E * C * sizeof(float2)},
       {st->step_count, w->B.step_count, E * sizeof(int32_t)},
       {st->time_passed, w->B.time_passed, E * sizeof(double)},
   };
@@ -850,8 +925,18 @@ int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream) {
 
 int macm_world_set_debug(macm_world* w, int32_t flags) {
   if (!w) return fail(MACM_E_INVALID, "world is NULL");
-  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SWEEP_CELLS | MACM_DEBUG_SWEEP_ALL_PAIRS))
+  const int pool = (flags & MACM_DEBUG_SPILL_POOL) ? (flags >> 8) : 0;
+  flags &= 0xff;
+  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SWEEP_CELLS | MACM_DEBUG_SWEEP_ALL_PAIRS | MACM_DEBUG_SPILL_POOL))
     return fail(MACM_E_INVALID, "unknown debug flag");
+  if (flags & MACM_DEBUG_SPILL_POOL) {
+    const int have = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;  // slots allocated
+    if (pool < 1 || pool > have) return fail(MACM_E_INVALID, "SPILL_POOL: 1 <= slots <= the slots allocated");
+    DeviceGuard g(w->device);
+    if (!w->B.sp_lock && dalloc(w, &w->B.sp_lock, (size_t)have)) return MACM_E_OOM;
+    HIP_TRY(hipMemset(w->B.sp_lock, 0, sizeof(uint32_t) * have));
+    w->B.sp_pool = pool;
+  }
   if ((flags & MACM_DEBUG_SWEEP_CELLS) && (flags & MACM_DEBUG_SWEEP_ALL_PAIRS))
     return fail(MACM_E_INVALID, "SWEEP_CELLS and SWEEP_ALL_PAIRS exclude each other");
   w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
@@ -1092,7 +1177,7 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
   const TdmBuffers TB = tdm_with_outputs(w, out);
   HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
                               w->rmask, s));
-  return MACM_OK;
+  return resync_host_status(w->hstat, w->B.status, w->P.n_envs, s);
 }
 
 int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream) {
@@ -1126,7 +1211,8 @@ static int tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm
     // or not (deaths are not known yet)
     const long long rows = (long long)(bots ? 1 : n_steps) * w->P.n_envs;
     if (rows > INT32_MAX) return fail(MACM_E_INVALID, "n_steps * n_envs too large to validate");
-    const int rc = check_actions(w->bad, actions, 2, bots ? w->TB.alive : nullptr, (int)rows, w->P.n_agents, s);
+    const int rc =
+        check_actions(w->bad, actions, 2, bots ? w->TB.alive : nullptr, (int)rows, w->P.n_agents, s, w->P.n_envs);
     if (rc) return rc;
   }
   const TdmBuffers TB = tdm_with_outputs(w, out);
@@ -1189,16 +1275,28 @@ static int tdm_copy_state(macm_tdm* w, const macm_tdm_state* st, void* stream, b
       {st->cd_mov, w->TB.cd_mov, E * N * sizeof(double)},
       {st->alive, w->TB.alive, E * N},
       {st->listener, w->TB.listener, E * sizeof(int2)},
-      {st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t)},
-      {st->contact_ab, w->B.cab[w->cur], E * C * sizeof(uint32_t)},
-      {st->contact_imp, w->B.cimp[w->cur], E * C * sizeof(float2)},
       {st->step_count, w->B.step_count, E * sizeof(int32_t)},
       {st->time_passed, w->B.time_passed, E * sizeof(double)},
       {st->done, w->B.done, E},
       {st->winner, w->TB.winner, E * sizeof(int32_t)},
   };
+  if (!to_device) {
+    if (st->contact_count)
+      HIP_TRY(hipMemcpyAsync(st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t), hipMemcpyDefault, s));
+    if (st->contact_ab)
+      HIP_TRY(hipMemcpyAsync(st->contact_ab, w->B.cab[w->cur], E * C * sizeof(uint32_t), hipMemcpyDefault, s));
+    if (st->contact_imp)
+      HIP_TRY(hipMemcpyAsync(st->contact_imp, w->B.cimp[w->cur], E * C * sizeof(float2), hipMemcpyDefault, s));
+  }
   if (to_device) {
-    if (const int rc = validate_lists(st->contact_count, st->contact_ab, E, C, (int)N, s)) return rc;
+    if (!st->contact_count != !st->contact_ab)
+      return fail(MACM_E_INVALID, "contact_count and contact_ab must be given together");
+    if (st->contact_count) {
+      const int rc = stage_lists(w->B, w->cur, w->bad, E, C, C, (int)N, st->contact_count, st->contact_ab,
+                                 st->contact_imp, s);
+      if (rc) return rc;
+      w->cur ^= 1;
+    }
     HIP_TRY(hipStreamSynchronize(s));
     clear_host_status(w->hstat);
     HIP_TRY(hipMemsetAsync(w->B.status, 0, E * sizeof(int32_t), s));

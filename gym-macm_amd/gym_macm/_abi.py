@@ -14,10 +14,11 @@ ACTION_DISCRETE, ACTION_CONTINUOUS = 0, 1
 REWARD_BINARY, REWARD_LINEAR = 0, 1
 COORD_POLAR, COORD_CARTESIAN = 0, 1
 
-ST_CONTACT_OVERFLOW, ST_TOUCH_OVERFLOW, ST_DEGREE_OVERFLOW, ST_INVALID_ACTION = 1, 2, 4, 8
+ST_CONTACT_OVERFLOW, ST_TOUCH_OVERFLOW, ST_DEGREE_OVERFLOW, ST_INVALID_ACTION, ST_SPILL_WAIT = 1, 2, 4, 8, 16
 DEBUG_FORCE_SPILL = 1
 DEBUG_SWEEP_CELLS = 2
 DEBUG_SWEEP_ALL_PAIRS = 4
+DEBUG_SPILL_POOL = 8  # | slots << 8
 E_INVALID, E_OVERFLOW = -1, -5
 
 _ERRORS = {
@@ -70,7 +71,7 @@ class MacmOutputs(Structure):
 class MacmState(Structure):
     _fields_ = [(n, c_void_p) for n in (
         "pos", "vel", "angle", "fat", "sleep", "targets", "contact_count", "contact_ab",
-        "contact_imp", "step_count", "time_passed")]
+        "contact_imp", "step_count", "time_passed")] + [("contact_stride", c_int64)]
 
 
 class MacmWorldInfo(Structure):
@@ -82,7 +83,7 @@ class MacmWorldInfo(Structure):
         ("max_contacts", c_int32),
         ("max_touching", c_int32),
         ("device", c_int32),
-        ("_pad", c_int32),
+        ("spill_slots", c_int32),
     ]
 
 
@@ -163,7 +164,9 @@ class MacmError(MacmLibraryError):
 
 class MacmOverflowError(MacmError):
     """MACM_E_OVERFLOW: an env outgrew a capacity in an earlier step, so the results since then
-    are not the reference's (the step refuses to continue until reset / place / set_state)."""
+    are not the reference's (the step refuses to continue until reset / place / set_state).
+    Detection is eventual: steps queued behind the overflowing one still run, and the first call
+    that sees the device's host-mapped status word raises; check_status() synchronises and is exact."""
 
 
 class MacmInvalidActionError(MacmError):

@@ -60,7 +60,9 @@ class FlockVec(object):
 
         Raises MacmOverflowError (a MacmLibraryError) once an earlier step has overflowed a
         capacity (the contact list's max_contacts; dense touching contacts never overflow: the
-        spill step takes them), MacmInvalidActionError with ``validate_actions=True`` and an
+        spill step takes them) — on the first call after the device reported it, which without a
+        synchronisation may be a few queued steps later (check_status() is exact) —
+        MacmInvalidActionError with ``validate_actions=True`` and an
         action outside the action space (no env is stepped, as the reference asserts first)."""
         out = self.world.step(actions)
         if self.autoreset:

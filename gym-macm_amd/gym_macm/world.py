@@ -55,6 +55,7 @@ class World:
         self.info = info
         self.OD = info.obs_dim
         self.C = info.max_contacts
+        self.spill_slots = info.spill_slots
         odt = torch.float64 if cfg.obs_f64 else torch.float32
         # host_outputs: outputs live in pinned host memory that the kernels write over
         # the bus (zero-copy views for the small-E dict API; actions may be pinned too)
@@ -242,8 +243,14 @@ class World:
         return self.obs, self.nbr_id
 
     # -- state ---------------------------------------------------------------
-    def state_buffers(self):
-        E, N, T, C = self.E, self.N, self.T, self.C
+    _STATE_KEYS = ("pos", "vel", "angle", "fat", "sleep", "targets", "contact_count", "contact_ab", "contact_imp",
+                   "step_count", "time_passed")
+
+    def state_buffers(self, stride=None):
+        """Host arrays of get_state's layout; contact_ab / contact_imp rows of `stride` entries
+        (default: max_contacts)."""
+        E, N, T = self.E, self.N, self.T
+        C = self.C if stride is None else int(stride)
         return dict(pos=np.zeros((E, N, 2), np.float32), vel=np.zeros((E, N, 2), np.float32),
                     angle=np.zeros((E, N), np.float32), fat=np.zeros((E, N, 4), np.float32),
                     sleep=np.zeros((E, N), np.float32), targets=np.zeros((E, T, 2), np.float32),
@@ -251,38 +258,47 @@ class World:
                     contact_imp=np.zeros((E, C, 2), np.float32), step_count=np.zeros((E,), np.int32),
                     time_passed=np.zeros((E,), np.float64))
 
+    def _state_struct(self, arrs, stride):
+        return _abi.MacmState(*[ctypes.c_void_p(arrs[k].ctypes.data) if arrs.get(k) is not None else None
+                                for k in self._STATE_KEYS], int(stride))
+
     def get_state(self) -> dict:
-        s = self.state_buffers()
-        st = _abi.MacmState(*[ctypes.c_void_p(s[k].ctypes.data) for k, _ in _abi.MacmState._fields_])
-        _abi.check(self.L.macm_world_get_state(self.h, ctypes.byref(st), self._stream()), "macm_world_get_state")
+        """The world's state as host arrays. The contact lists' rows hold max(contact_count)
+        entries (at least 1), not max_contacts: only their used part crosses the bus (C can be
+        large for N > 64); entries past an env's count are zero."""
+        cnt = np.zeros((self.E,), np.int32)
+        _abi.check(self.L.macm_world_get_state(self.h, ctypes.byref(self._state_struct({"contact_count": cnt}, 0)),
+                                               self._stream()), "macm_world_get_state")
+        stride = max(1, int(cnt.max(initial=0)))
+        s = self.state_buffers(stride)
+        _abi.check(self.L.macm_world_get_state(self.h, ctypes.byref(self._state_struct(s, stride)), self._stream()),
+                   "macm_world_get_state")
         # entries past each env's contact_count are scratch: zero them so states compare/serialise cleanly
-        idx = np.arange(self.C)[None, :] >= s["contact_count"][:, None]
+        idx = np.arange(stride)[None, :] >= s["contact_count"][:, None]
         s["contact_ab"][idx] = 0
         s["contact_imp"][idx] = 0
         return s
 
     def set_state(self, s: dict) -> None:
-        """Inject a state (get_state's layout). Contact lists saved from a world with a different
-        max_contacts are re-padded; a list longer than this world's capacity raises ValueError
-        (truncating it would change the physics). The library validates the pairs too."""
-        ref = self.state_buffers()
+        """Inject a state (get_state's layout; the contact rows may have any length >= the counts,
+        e.g. another world's max_contacts). A list longer than this world's capacity raises
+        ValueError (truncating it would change the physics); the library validates the pairs on
+        the device and takes nothing if any is invalid."""
         counts = np.asarray(s["contact_count"], dtype=np.int32)
         if counts.shape == (self.E,) and (counts.max(initial=0) > self.C or counts.min(initial=0) < 0):
             raise ValueError(f"contact_count must lie in [0, {self.C}] (this world's max_contacts); "
                              f"got [{int(counts.min())}, {int(counts.max())}]")
+        ab = np.asarray(s["contact_ab"])
+        stride = ab.shape[1] if ab.ndim == 2 else self.C
+        ref = self.state_buffers(stride)
         arrs = {}
         for k, v in ref.items():
             a = np.ascontiguousarray(np.asarray(s[k], dtype=v.dtype))
-            if k in ("contact_ab", "contact_imp") and a.ndim >= 2 and a.shape[1] != self.C:
-                pad = np.zeros_like(v)
-                n = min(a.shape[1], self.C)
-                pad[:, :n] = a[:, :n]
-                a = pad
             if a.shape != v.shape:
                 raise ValueError(f"state[{k!r}] has shape {a.shape}, expected {v.shape}")
             arrs[k] = a
-        st = _abi.MacmState(*[ctypes.c_void_p(arrs[k].ctypes.data) for k, _ in _abi.MacmState._fields_])
-        _abi.check(self.L.macm_world_set_state(self.h, ctypes.byref(st), self._stream()), "macm_world_set_state")
+        _abi.check(self.L.macm_world_set_state(self.h, ctypes.byref(self._state_struct(arrs, stride)), self._stream()),
+                   "macm_world_set_state")
         self.done.copy_(torch.from_numpy((arrs["time_passed"] > self.cfg.time_limit).astype(np.uint8)))
 
     def status(self) -> int:

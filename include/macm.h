@@ -56,21 +56,30 @@ enum { MACM_COORD_POLAR = 0, MACM_COORD_CARTESIAN = 1 };
  * Status bits accumulated per env on the device (macm_world_status). Flock never sets
  * TOUCH/DEGREE: an env whose touching contacts exceed a fast kernel's LDS capacity is stepped
  * by the spill step (HBM working set sized by max_contacts) instead. CONTACT_OVERFLOW (the
- * fat-AABB pair list itself outgrew max_contacts) and TDM's TOUCH/DEGREE caps remain; once any
- * bit is set, the next step call returns MACM_E_OVERFLOW.
+ * fat-AABB pair list itself outgrew max_contacts) and TDM's TOUCH/DEGREE caps remain. Detection
+ * is eventual, not synchronous: the kernels store the bits into a host-mapped word, and each step /
+ * rollout call reads it before launching, without synchronising, so steps already queued behind an
+ * overflowing one still run (and a rollout keeps stepping the overflowed env for its K steps); the
+ * first call that sees the word returns MACM_E_OVERFLOW. macm_world_status() (which synchronises)
+ * is exact. reset / place / set_state clear the bits; reset_envs re-derives the word from the envs
+ * it did not reset.
  */
 enum {
   MACM_ST_CONTACT_OVERFLOW = 1, /* Ov(F_t) list exceeded max_contacts                   */
   MACM_ST_TOUCH_OVERFLOW = 2,   /* TDM: touching contacts exceeded the solver capacity   */
   MACM_ST_DEGREE_OVERFLOW = 4,  /* TDM: a body touched more bodies than the adjacency cap */
-  MACM_ST_INVALID_ACTION = 8    /* validate_actions: an action outside the action space  */
+  MACM_ST_INVALID_ACTION = 8,   /* validate_actions: an action outside the action space  */
+  MACM_ST_SPILL_WAIT = 16       /* a dense env found no free spill working-set slot for ~1 s
+                                   (a pooled world: fewer slots than envs) and was not stepped */
 };
 
 /* macm_world_set_debug flags (test hooks; 0 = product behaviour). */
 enum {
   MACM_DEBUG_FORCE_SPILL = 1,     /* every env takes the spill step (parity tests of that path)  */
   MACM_DEBUG_SWEEP_CELLS = 2,     /* N > 64: pair sweep over strip cells at any N (else N >= 512) */
-  MACM_DEBUG_SWEEP_ALL_PAIRS = 4  /* N > 64: all-pairs pair sweep at any N                        */
+  MACM_DEBUG_SWEEP_ALL_PAIRS = 4, /* N > 64: all-pairs pair sweep at any N                        */
+  MACM_DEBUG_SPILL_POOL = 8       /* the spill working set as a pool of (flags >> 8) slots, at most
+                                     the slots allocated (pooled-slot tests at small E)            */
 };
 
 /*
@@ -220,7 +229,10 @@ typedef struct macm_outputs {
  *   contact_imp   [E, C, 2] float32   (normalImpulse, tangentImpulse) warm start
  *   step_count    [E]       int32     steps taken (0 => dtRatio 0 on next step)
  *   time_passed   [E]       float64
- * C = macm_world_info().max_contacts.
+ *   contact_stride            entries per env row of the caller's contact_ab / contact_imp
+ *                             (0 = C = macm_world_info().max_contacts). get_state fills the first
+ *                             min(stride, C) entries of each row: a stride of max(contact_count)
+ *                             moves only the lists' used part (ABI 5; C can be large for N > 64).
  */
 typedef struct macm_state {
   void* pos;
@@ -234,6 +246,7 @@ typedef struct macm_state {
   void* contact_imp;
   void* step_count;
   void* time_passed;
+  int64_t contact_stride;
 } macm_state;
 
 typedef struct macm_world_info {
@@ -241,7 +254,7 @@ typedef struct macm_world_info {
   int32_t max_contacts;   /* per-env ordered contact list capacity */
   int32_t max_touching;   /* per-env solver capacity               */
   int32_t device;
-  int32_t _pad;
+  int32_t spill_slots;    /* spill working-set slots (= n_envs: one per env; fewer: a pool) */
 } macm_world_info;
 
 typedef struct macm_world macm_world;
@@ -257,12 +270,15 @@ int macm_config_default(macm_config* cfg);
 /*
  * Create E envs of one Flock configuration on `device`.
  *   targets_idx: host int32[N], agent -> target index (mvmnt.py:43), or NULL = all 0.
- *   max_contacts: per-env capacity C of the ordered fat-AABB pair list (and of the spill
- *   step's HBM working set, 80 B per entry and env with the list). 0 = the default:
- *   N(N-1)/2 (every pair: the list can never overflow) when N <= 64 or when E * N(N-1)/2 * 80 B
- *   fits in 8 GiB; otherwise the largest C with E * C * 80 B <= 8 GiB (at least 32 N).
- *   macm_world_info reports the value chosen. Overflow of the list sets
- *   MACM_ST_CONTACT_OVERFLOW and the next macm_world_step returns MACM_E_OVERFLOW.
+ *   max_contacts: per-env capacity C of the ordered fat-AABB pair list (and of each slot of
+ *   the spill step's HBM working set). 0 = the default, from a budget of 1/8 of the device's
+ *   free memory at creation (so every world shrinks what the next one sees), half for the lists
+ *   (24 B per entry and env): N(N-1)/2 (every pair: the list can never overflow) when N <= 64 or
+ *   when that fits, otherwise the largest C that fits (at least 32 N). The other half holds the
+ *   spill working set, 48 B per entry and 48 B per body per slot: one slot per env when they fit,
+ *   otherwise a pool (>= 16 slots) that dense envs take turns on (macm_world_info: spill_slots).
+ *   On an idle 288 GB MI355X: C5's shard (2048 envs x 1024 agents) gets C ~ 366k and ~1k slots.
+ *   Overflow of the list sets MACM_ST_CONTACT_OVERFLOW and a later step returns MACM_E_OVERFLOW.
  * Replaces: Flock.__init__ world + body creation (mvmnt.py:35-79,
  * cm_framework.py:155-167). State is undefined until macm_world_reset.
  */
@@ -357,10 +373,10 @@ int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream);
 
 /*
  * Copy state out / in (synchronous w.r.t. `stream`). set_state validates the contact lists
- * it is given (when contact_count is non-NULL): 0 <= count <= C and, for every entry below the
- * count, a < b < N (host copies of contact_ab are checked on the host, device copies after a
- * staging copy); otherwise MACM_E_INVALID and nothing is copied. contact_ab and contact_count
- * must be given together. Clears the status bits.
+ * it is given (when contact_count is non-NULL): 0 <= count <= min(C, contact_stride) and, for
+ * every entry below the count, a < b < N, checked on the device after staging the lists into the
+ * world's spare list buffer; otherwise MACM_E_INVALID and nothing is copied. contact_count and
+ * contact_ab must be given together (contact_imp NULL: zero impulses). Clears the status bits.
  */
 int macm_world_get_state(macm_world* w, const macm_state* dst, void* stream);
 int macm_world_set_state(macm_world* w, const macm_state* src, void* stream);

@@ -44,6 +44,37 @@ def test_dense_256_agents_spread_8_spill_bit_exact():
     assert vec.spilled() > 0
 
 
+@pytest.mark.parametrize("E,N,spread,slots,steps", [(12, 64, 3, 2, 30), (3, 256, 8, 1, 12)])
+def test_spill_pool_takes_turns(E, N, spread, slots, steps):
+    """A world whose memory budget holds fewer spill working-set slots than envs (the
+    working set was allocated for every env) shares a pool: dense envs take a slot for their spill
+    step in turn (spill::acquire_slot). Forced here to 2 / 1 slots for 12 / 3 dense envs: results
+    stay bit-exact and every env is stepped (no MACM_ST_SPILL_WAIT)."""
+    vec, orc = make_pair(E, [N], seed=E + N, start_spread=spread)
+    vec.world.set_debug(_abi.DEBUG_SPILL_POOL | (slots << 8))
+    check_rollout(vec, orc, steps, np.random.default_rng(N), state_every=5)
+    assert vec.status() == 0
+    assert vec.spilled() >= E, "the envs never took the spill step"
+
+
+def test_default_capacities_from_the_device_budget():
+    """max_contacts = 0: every pair for N <= 64; one spill slot per env where the budget allows."""
+    v = FlockVec(64, n_agents=[64], seed=1, device="cuda:0")
+    assert v.world.C == 64 * 63 // 2 and v.world.spill_slots == 64
+    w = FlockVec(8, n_agents=[1024], seed=1, device="cuda:0")
+    assert w.world.C == 1024 * 1023 // 2 and w.world.spill_slots == 8  # 8 envs fit every pair
+
+
+def test_c5_shaped_world_at_start_spread_5():
+    """a C5-shaped env (1024 agents) at start_spread 5 (41 bodies per m^2: ~10^5
+    fat-AABB pairs and tens of thousands of touching contacts per env) steps through the spill step
+    with status 0 and the default capacity, bit-exact against the oracle."""
+    vec, orc = make_pair(2, [1024], seed=5, start_spread=5)
+    assert vec.world.C == 1024 * 1023 // 2
+    check_rollout(vec, orc, 2, np.random.default_rng(5), state_every=1)
+    assert vec.status() == 0 and vec.spilled() == 4
+
+
 def test_dense_1024_agents_spread_14_spill():
     """N = 1024 at start_spread 14 (5.2 bodies per m^2): beyond kernel A's 4608 touching contacts."""
     vec, orc = make_pair(1, [1024], seed=14, start_spread=14)
@@ -130,6 +161,28 @@ def test_list_overflow_during_stepping_raises_on_next_step():
         v.step(a)
     v.reset()
     v.step(a)  # a reset clears the condition
+
+
+def test_reset_envs_clears_the_overflow_of_the_envs_it_resets():
+    """reset_envs re-derives the host status word from the envs it did not reset. Env 1
+    outgrows max_contacts; resetting env 0 only leaves the error, resetting env 1 clears it."""
+    E, N = 2, 100
+    v = FlockVec(E, n_agents=[N], seed=9, device="cuda:0", start_spread=30, max_contacts=150)
+    st = v.get_state()
+    st["pos"][1] = st["pos"][1] * np.float32(0.2)  # env 1 only: far more overlapping pairs
+    st["contact_count"][:] = 0
+    v.set_state(st)
+    a = torch.ones((E, N, 3), dtype=torch.uint8, device="cuda:0")
+    v.step(a)
+    torch.cuda.synchronize()
+    with pytest.raises(_abi.MacmOverflowError):
+        v.step(a)
+    v.reset_envs(torch.tensor([1, 0], dtype=torch.uint8, device="cuda:0"))
+    with pytest.raises(_abi.MacmOverflowError):
+        v.step(a)
+    v.reset_envs(torch.tensor([0, 1], dtype=torch.uint8, device="cuda:0"))
+    assert v.status() == 0
+    v.step(a)  # the overflowed env was reset: stepping resumes
 
 
 def test_tdm_capacity_overflow_raises():
