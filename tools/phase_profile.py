@@ -32,6 +32,7 @@ PHASES_C = ["oldc+sleep_clock", "island_sleep", "sync_fixtures", "grid_build", "
             "new_pairs", "old_list", "reward+obs", "writeback"]
 PHASES_B = ["solve_velocity", "solve_position"]
 PHASES_A = ["A:actions", "A:collide", "A:csr+sort", "A:dfs+levels", "A:level_sort", "A:records"]
+PHASES_D = ["A2:dfs+levels", "A2:level_sort+records"]  # flock_dfs_wg (dense envs)
 PHASES_WG = ["loads+actions", "collide", "csr+sort", "dfs", "integrate+records", "velocity_solve",
              "impulses+integrate+position", "sleep", "sync_fixtures", "pairs+nearest", "list_build",
              "reward+obs+writeback"]
@@ -79,7 +80,9 @@ def main():
                 t = np.concatenate([buf[:, :10], buf[:, 13:16]], 1).astype(np.int64)
                 dd = np.diff(t, axis=1)
                 da = np.diff(buf[:, 16:23].astype(np.int64), axis=1)
-                deltas.append(np.concatenate([da, dd[:, :9], dd[:, 10:]], 1))
+                # flock_dfs_wg (dense envs' DFS kernel, stamps 26..28; zero for the envs kernel A walked)
+                d2 = np.where(buf[:, 26:27] > 0, np.diff(buf[:, 26:29].astype(np.int64), axis=1), 0)
+                deltas.append(np.concatenate([da, dd[:, :9], dd[:, 10:], d2], 1))
             else:
                 b16 = buf.reshape(-1)[:E * 16].reshape(E, 16)
                 t = b16[:, :14].astype(np.int64)
@@ -87,7 +90,7 @@ def main():
             stats.append(buf.reshape(-1)[:E * 16].reshape(E, 16)[:, 14:].copy())
             stats_wg.append(np.concatenate([buf[:, 10:13], buf[:, 24:26]], 1).copy())
     d = np.concatenate(deltas)  # [steps*E, 13]
-    phases = PHASES if N <= 64 else PHASES_A + PHASES_C + PHASES_B
+    phases = PHASES if N <= 64 else PHASES_A + PHASES_C + PHASES_B + PHASES_D
     st = np.concatenate(stats)
     total = d.sum(axis=1)
     out = {"envs": E, "agents": N, "spread": args.spread, "policy": args.policy, "kernel_ms_stamped": float(np.mean(walls)),
