@@ -81,6 +81,11 @@ struct WorldBuffers {
   float2* x_vout;                // [E, N]    velocities after the solve (max-translation clamped)
   uint8_t* x_deg;                // [E, N]    body has touching edges
   uint8_t* x_isolv;              // [E, IS]   island position-solved
+  // Dense envs' island DFS in its own kernel (flock_dfs_wg): kernel A hands over
+  uint32_t* x_tab;               // [E, tcap] touching contacts in list order (a | b << 16)
+  uint32_t* x_adj;               // [E, 2 tcap] CSR edges: touching index | other body << 16
+  uint16_t* x_off;               // [E, N + 1] CSR offsets ([N] = 2 T)
+  uint32_t* x_dfs;               // [E, tcap] island order: touching index | level << 16
   // Spill step (flock_spill.hpp): HBM working set for envs whose touching contacts exceed the fast
   // kernels' LDS capacities, capacity C = max_contacts per slot (touching contacts are in the list).
   // S slots: S = E (slot = env) when the memory budget allows, else a pool that a spilling env

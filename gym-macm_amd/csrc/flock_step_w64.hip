@@ -1217,11 +1217,13 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           while (m) {
             const int t = __builtin_ctzll(m);
             m &= m - 1ull;
-            if (!W2 || nord < 64) ordv = writelane_m0(base + t, nord, ordv);  // s_ord[nord]
-            else ordv1 = writelane_m0(base + t, nord - 64, ordv1);
+            // s_ord[nord]: lane nord % 64 of ordv; the first 64 entries are set aside in ordv1 once
+            // complete (a select, instead of a branch between two registers on every edge)
+            ordv = writelane_m0(base + t, W2 ? (nord & 63) : nord, ordv);
             const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tab, t);
             const int a = ab & 0xffffu, bb = ab >> 16;
             ++nord;
+            if constexpr (W2) ordv1 = nord == 64 ? ordv : ordv1;
             const int o = (a == b) ? bb : a;
             if ((vis >> o) & 1ull) continue;
             vis |= 1ull << o;
@@ -1247,8 +1249,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     else dfs(BoolC<false>{});
     icv = writelane_m0(nord, nisl, icv);
     ibv = writelane_m0(nb, nisl, ibv);
-    if (lane < nord) s_ord[lane] = (uint8_t)ordv;
-    if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv1;
+    const bool wrapped = TMW == 2 && nord > 64;  // entries 0..63 in ordv1, 64.. in ordv
+    if (lane < nord) s_ord[lane] = (uint8_t)(wrapped ? ordv1 : ordv);
+    if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv;
     if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
     if ((hasdeg >> lane) & 1ull) s_bisl[lane] = (uint8_t)islv;
     if (lane <= nisl) {

@@ -46,6 +46,16 @@ constexpr bool kDfsPriority = false;
 #else
 constexpr bool kDfsPriority = true;
 #endif
+// Dense envs (the wave-parallel walk: average touching degree >= 4, e.g. C5) take the island DFS,
+// the Gauss-Seidel levels and the level-ordered records in their own kernel (flock_dfs_wg: one wave
+// per env, ~45 KB of LDS, so 3 envs share a CU), instead of in kernel A, whose 78 KB block would
+// hold a CU while one of its 16 waves walks. -DMACM_NO_DFS_KERNEL: kernel A walks them.
+#ifdef MACM_NO_DFS_KERNEL
+constexpr bool kDfsKernel = false;
+#else
+constexpr bool kDfsKernel = true;
+#endif
+constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
 // block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
@@ -530,6 +540,38 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 #else
   const bool par_dfs = 2 * T >= 4 * N;
 #endif
+  if (kDfsKernel && par_dfs) {
+    // the touching contacts, the CSR offsets and every edge with its other body to HBM; the
+    // integrated velocities as after the walk; flock_dfs_wg does the rest of this kernel
+    const int IS = wg_isl_stride(N);
+    (void)IS;
+    uint32_t* xt = B.x_tab + (size_t)e * tcap;
+    for (int t = tid; t < T; t += BS) xt[t] = s_tab[t];
+    if (act) {
+      uint32_t* xa = B.x_adj + (size_t)e * 2 * tcap;
+      const int o0 = s_off[tid], o1 = o0 + deg;
+      for (int q = o0; q < o1; ++q) {
+        const int t = s_adj[q];
+        const uint32_t ab = s_tab[t];
+        const int a = ab & 0xffffu, b = ab >> 16;
+        xa[q] = (uint32_t)t | ((uint32_t)(a == tid ? b : a) << 16);
+      }
+      B.x_off[(size_t)e * (N + 1) + tid] = s_off[tid];
+      const float vx = v.x + P.dt * (0.0f + P.inv_mass * Fx);
+      const float vy = v.y + P.dt * (0.0f + P.inv_mass * Fy);
+      B.x_vmid[ag] = make_float2(vx * P.damp, vy * P.damp);
+      B.x_deg[ag] = deg > 0 ? 1 : 0;
+    }
+    if (tid == 0) {
+      B.x_off[(size_t)e * (N + 1) + N] = (uint16_t)(2 * T);
+      B.x_nisl[e] = kDfsPending;
+    }
+#ifdef MACM_STAMPS
+    if (tid == 0)
+      for (int k = 20; k <= 22; ++k) B.stamps[(size_t)e * 32 + k] = B.stamps[(size_t)e * 32 + 19];
+#endif
+    return;
+  }
   // One island walked by a whole wave from seed sd (its todo bit already cleared): a popped
   // body's edges one per lane, levels by a prefix maximum (below). Appends to s_ord / s_lvl at
   // nord and s_ibod at nb; the stack lives at s_stk[sbase...]. Every lane of the wave calls it.
@@ -943,6 +985,237 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     B.x_ib[(size_t)e * IS + q] = s_ib[q];
   }
   if (tid == 0) B.x_nisl[e] = nisl;
+}
+
+namespace wg {
+// flock_dfs_wg's LDS (one wave per env): CSR edges (touching index | other body << 16), offsets,
+// per-body level bookkeeping, the stack, the unvisited-body and visited-contact bitmasks, the
+// island contact starts. The level counts of the records' counting sort reuse the edges.
+struct WgLayoutD {
+  int adj, off, last, stk, todo, cvis, ic, total;
+};
+__host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
+  WgLayoutD L;
+  int o = 0;
+  auto take = [&](int bytes) {
+    int r = o;
+    o = align16(o + bytes);
+    return r;
+  };
+  L.adj = take(8 * tcap);
+  L.off = take(2 * (N + 1));
+  L.last = take(2 * N);
+  L.stk = take(2 * N);
+  L.todo = take(8 * ((N + 63) / 64));
+  L.cvis = take(4 * ((tcap + 31) / 32));
+  L.ic = take(2 * (N / 2 + 2));
+  L.total = o;
+  return L;
+}
+}  // namespace wg
+
+// Kernel A2 (dense envs): the island DFS in Box2D order by one wave (the wave-parallel walk of
+// kernel A: a popped body's edges one per lane, levels by a prefix maximum), then the Gauss-Seidel
+// levels' counting sort and the level-ordered records for kernel B. Same order, levels and records
+// as kernel A's walk; the edge carries its other body, so a popped body's contacts take one LDS
+// round trip fewer (edge -> {visited bit, todo bit, level, CSR range} instead of edge -> pair -> ...).
+__global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B, int tcap) {
+  using namespace wg;
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int e = blockIdx.x, lane = threadIdx.x, N = P.n_agents;
+  const int tid = lane;  // WSTAMP
+  (void)tid;
+  if (B.x_nisl[e] != kDfsPending) return;  // kernel A walked it, or the spill step stepped it
+  WSTAMP(26);
+  const WgLayoutD L = wg_layout_d(N, tcap);
+  uint32_t* s_adj = (uint32_t*)(lds + L.adj);
+  uint16_t* s_off = (uint16_t*)(lds + L.off);
+  uint16_t* s_last = (uint16_t*)(lds + L.last);
+  uint16_t* s_stk = (uint16_t*)(lds + L.stk);
+  unsigned long long* s_todo = (unsigned long long*)(lds + L.todo);
+  uint32_t* s_cvis = (uint32_t*)(lds + L.cvis);
+  uint16_t* s_ic = (uint16_t*)(lds + L.ic);
+  const int IS = wg_isl_stride(N);
+  const uint16_t* xoff = B.x_off + (size_t)e * (N + 1);
+  const uint32_t* xadj = B.x_adj + (size_t)e * 2 * tcap;
+  uint32_t* xdfs = B.x_dfs + (size_t)e * tcap;
+  uint16_t* xibod = B.x_ibod + (size_t)e * N;
+  uint16_t* xib = B.x_ib + (size_t)e * IS;
+  const int T2 = xoff[N];
+  for (int b = lane; b <= N; b += W) s_off[b] = xoff[b];
+  for (int q = lane; q < T2; q += W) s_adj[q] = xadj[q];
+  for (int b = lane; b < N; b += W) s_last[b] = 0;
+  for (int q = lane; q < (tcap + 31) / 32; q += W) s_cvis[q] = 0u;
+  __syncthreads();
+  for (int w = 0; w < (N + 63) / 64; ++w) {  // bodies with touching edges: DFS seeds / unvisited
+    const int b = w * 64 + lane;
+    const unsigned long long m = __ballot(b < N && s_off[b + 1] > s_off[b]);
+    if (lane == 0) s_todo[w] = m;
+  }
+  __syncthreads();
+  if (kDfsPriority) __builtin_amdgcn_s_setprio(3);
+  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int nord = 0, nisl = 0, nb = 0, dmax = 0;
+  for (int w = (N + 63) / 64 - 1; w >= 0;) {
+    const unsigned long long m = s_todo[w];
+    if (m == 0ull) {
+      --w;
+      continue;
+    }
+    const int sd = w * 64 + 63 - __clzll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      s_todo[w] = m & ~(1ull << (sd & 63));
+      s_ic[nisl] = (uint16_t)nord;
+      xib[nisl] = (uint16_t)nb;
+      s_stk[0] = (uint16_t)sd;
+    }
+    int sp = 1;
+    int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;  // the last push of the previous pop
+    __builtin_amdgcn_wave_barrier();
+    while (sp > 0) {
+      int bdy, e0, e1, xcur;
+      --sp;
+      if (top_b >= 0) {
+        bdy = top_b;
+        e0 = top_e0;
+        e1 = top_e1;
+        xcur = top_last;
+      } else {
+        bdy = s_stk[sp];
+        e0 = s_off[bdy];
+        e1 = s_off[bdy + 1];
+        xcur = s_last[bdy];
+      }
+      top_b = -1;
+      if (lane == 0) xibod[nb] = (uint16_t)bdy;
+      ++nb;
+      // levels of the new contacts c_1..c_m of bdy in order: X_i = i + max(X_0, max_{j<=i}(y_j - j + 1))
+      // (see par_walk in kernel A)
+      for (int q0 = e0; q0 < e1; q0 += W) {
+        const int q = q0 + lane;
+        int t = 0, o = 0, lo = 0, oe0 = 0, oe1 = 0;
+        uint32_t cv = 0xffffffffu;
+        unsigned long long tw = 0ull;
+        if (q < e1) {  // one round of LDS reads after the edge's
+          const uint32_t ed = s_adj[q];
+          t = ed & 0xffffu;
+          o = ed >> 16;
+          cv = s_cvis[t >> 5];
+          tw = s_todo[o >> 6];
+          lo = s_last[o];
+          oe0 = s_off[o];
+          oe1 = s_off[o + 1];
+        }
+        const bool newc = !((cv >> (t & 31)) & 1u);
+        const unsigned long long mc = __ballot(newc);
+        int rank = 0, z = -0x3fffffff, xi = 0;
+        bool push = false;
+        if (newc) {
+          atomicOr(&s_cvis[t >> 5], 1u << (t & 31));
+          rank = __popcll(mc & lt) + 1;
+          push = (tw >> (o & 63)) & 1ull;
+          z = lo - rank + 1;
+        }
+        z = wave_prefix_max(z);
+        if (newc) {
+          xi = rank + max(xcur, z);
+          s_last[o] = (uint16_t)xi;
+          xdfs[nord + rank - 1] = (uint32_t)t | ((uint32_t)(xi - 1) << 16);
+        }
+        const int mnew = __popcll(mc);
+        if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
+        nord += mnew;
+        const unsigned long long mp = __ballot(push);
+        if (push) {
+          atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
+          s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
+        }
+        sp += __popcll(mp);
+        if (mp) {  // the new top: the highest pushing lane
+          const int hl = 63 - __clzll(mp);
+          top_b = __builtin_amdgcn_readlane(o, hl);
+          top_e0 = __builtin_amdgcn_readlane(oe0, hl);
+          top_e1 = __builtin_amdgcn_readlane(oe1, hl);
+          top_last = __builtin_amdgcn_readlane(xi, hl);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) s_last[bdy] = (uint16_t)xcur;
+      dmax = max(dmax, xcur);
+      __builtin_amdgcn_wave_barrier();
+    }
+    ++nisl;
+  }
+  if (lane == 0) {
+    s_ic[nisl] = (uint16_t)nord;
+    xib[nisl] = (uint16_t)nb;
+  }
+  if (kDfsPriority) __builtin_amdgcn_s_setprio(0);
+  // this wave's x_dfs stores are read back below (workgroup scope: this CU, this XCD's L2)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __syncthreads();
+  WSTAMP(27);
+
+  // ---- Gauss-Seidel levels: counting sort into level order; the records for kernel B ------------
+  uint32_t* s_cnt = s_adj;  // [dmax + 1] (the edges are dead; dmax <= T <= tcap)
+  for (int l = lane; l <= dmax; l += W) s_cnt[l] = 0u;
+  __syncthreads();
+  for (int k = lane; k < nord; k += W) atomicAdd(&s_cnt[xdfs[k] >> 16], 1u);
+  __syncthreads();
+  {  // exclusive scan over the levels: lane L owns levels [L per, (L + 1) per)
+    const int per = (dmax + W - 1) / W;
+    const int l0 = lane * per, l1 = min(dmax, l0 + per);
+    int sum = 0;
+    for (int l = l0; l < l1; ++l) sum += (int)s_cnt[l];
+    int incl = sum;
+    for (int d = 1; d < W; d <<= 1) {
+      const int y = __shfl_up(incl, d, W);
+      if (lane >= d) incl += y;
+    }
+    int run = incl - sum;
+    for (int l = l0; l < l1; ++l) {
+      const int c = (int)s_cnt[l];
+      s_cnt[l] = (uint32_t)run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  const uint32_t* xt = B.x_tab + (size_t)e * tcap;
+  const float2* g_lam = B.scratch + (size_t)e * tcap;
+  float4* xc = B.x_cst + (size_t)e * tcap;
+  float2* xi = B.x_cimp + (size_t)e * tcap;
+  uint16_t* xo = B.x_ord + (size_t)e * tcap;
+  const float2* pos = B.pos + (size_t)e * N;
+  for (int k = lane; k < nord; k += W) {
+    const uint32_t d = xdfs[k];
+    const int t = d & 0xffffu, lv = d >> 16;
+    const uint32_t ab = xt[t];
+    const int a = ab & 0xffffu, b = ab >> 16;
+    const float2 pa = pos[a], pb = pos[b];  // the start-of-step positions (kernel C writes them back)
+    float nx = 1.0f, ny = 0.0f;             // InitializeVelocityConstraints: (1, 0) when the centres coincide
+    const float ddx = pa.x - pb.x, ddy = pa.y - pb.y;
+    if (ddx * ddx + ddy * ddy > kEps * kEps) {
+      nx = pb.x - pa.x;
+      ny = pb.y - pa.y;
+      normalize(nx, ny);
+    }
+    int lo = 0, hi = nisl - 1;  // the island of contact k
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int)s_ic[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    const int p = (int)atomicAdd(&s_cnt[lv], 1u);  // any slot of its level: a level's contacts share no body
+    xc[p] = make_float4(__uint_as_float(ab), nx, ny, __int_as_float((lv << 16) | lo));
+    xi[p] = g_lam[t];
+    xo[p] = (uint16_t)t;
+  }
+  for (int q = lane; q <= nisl; q += W) B.x_ic[(size_t)e * IS + q] = s_ic[q];
+  if (lane == 0) {
+    B.x_nlvl[e] = dmax;
+    B.x_nisl[e] = nisl;
+  }
+  WSTAMP(28);
 }
 
 namespace wg {
@@ -1596,6 +1869,7 @@ static int wg_a_lds_bytes(int N, int tcap) {
 int wg_lds_bytes(int N, int tcap) {
   int m = wg_a_lds_bytes(N, tcap);
   if (wg_solve_lds(N) > m) m = wg_solve_lds(N);
+  if (wg::wg_layout_d(N, tcap).total > m) m = wg::wg_layout_d(N, tcap).total;
   if (wg_layout_c(N).total > m) m = wg_layout_c(N).total;
   if (wg_init_lds_bytes(N) > m) m = wg_init_lds_bytes(N);
   return m;
@@ -1614,6 +1888,9 @@ hipError_t wg_configure(int N, int tcap) {
   const int lsplit[] = {la, la, wg_solve_lds(N), lc, lc};
   for (int i = 0; i < 5; ++i)
     if (e == hipSuccess) e = hipFuncSetAttribute(fsplit[i], hipFuncAttributeMaxDynamicSharedMemorySize, lsplit[i]);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)flock_dfs_wg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            wg::wg_layout_d(N, tcap).total);
   return e;
 }
 
@@ -1622,15 +1899,18 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
                           hipStream_t s) {
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
   const int N = P.n_agents, la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
+  const int ld = wg::wg_layout_d(N, tcap).total;
   if (obs_f64) {
     hipLaunchKernelGGL(flock_step_wg_a<double>, grid, block, la, s, P, B, cur, tcap, actions, (double*)obs, nbr, rew,
                        coll, done);
+    if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
     hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
     hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, s, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
                        done);
   } else {
     hipLaunchKernelGGL(flock_step_wg_a<float>, grid, block, la, s, P, B, cur, tcap, actions, (float*)obs, nbr, rew,
                        coll, done);
+    if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
     hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
     hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, s, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
                        done);

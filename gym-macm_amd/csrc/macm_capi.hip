@@ -400,7 +400,11 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
                     (rc = dalloc(w, &B.x_ibod, EN)) || (rc = dalloc(w, &B.x_nisl, (size_t)n_envs)) ||
                     (rc = dalloc(w, &B.x_vmid, EN)) || (rc = dalloc(w, &B.x_cout, EN)) ||
                     (rc = dalloc(w, &B.x_vout, EN)) || (rc = dalloc(w, &B.x_deg, EN)) ||
-                    (rc = dalloc(w, &B.x_isolv, (size_t)n_envs * (N / 2 + 2))))) ||
+                    (rc = dalloc(w, &B.x_isolv, (size_t)n_envs * (N / 2 + 2))) ||
+                    (rc = dalloc(w, &B.x_tab, (size_t)n_envs * w->tcap)) ||
+                    (rc = dalloc(w, &B.x_adj, (size_t)n_envs * 2 * w->tcap)) ||
+                    (rc = dalloc(w, &B.x_off, (size_t)n_envs * (N + 1))) ||
+                    (rc = dalloc(w, &B.x_dfs, (size_t)n_envs * w->tcap)))) ||
       // spill step working set (flock_spill.hpp), capacity C per slot, SL slots
       (rc = dalloc(w, &B.sp_tab, (size_t)SL * C)) || (rc = dalloc(w, &B.sp_adj, (size_t)SL * 2 * C)) ||
       (rc = dalloc(w, &B.sp_ord, (size_t)SL * C)) || (rc = dalloc(w, &B.sp_cst, (size_t)SL * C)) ||
@@ -597,6 +601,7 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
   off(S.scratch, e0 * tcap), off(S.x_cst, e0 * tcap), off(S.x_cimp, e0 * tcap), off(S.x_ord, e0 * tcap);
   off(S.x_ic, IS), off(S.x_nlvl, e0), off(S.x_ib, IS), off(S.x_ibod, EN), off(S.x_nisl, e0);
   off(S.x_vmid, EN), off(S.x_cout, EN), off(S.x_vout, EN), off(S.x_deg, EN), off(S.x_isolv, IS);
+  off(S.x_tab, e0 * tcap), off(S.x_adj, e0 * 2 * tcap), off(S.x_off, e0 * (N + 1)), off(S.x_dfs, e0 * tcap);
   off(S.spill_count, e0);
   if (B.sp_pool == 0) {  // one working-set slot per env: the slice's rows; a pool is shared as it is
     off(S.sp_tab, e0 * C), off(S.sp_adj, e0 * 2 * C), off(S.sp_ord, e0 * C), off(S.sp_cst, e0 * C);
