@@ -23,9 +23,11 @@
 #pragma once
 
 #include "flock_common.hpp"
+#include "tdm_obs.hpp"
 
 namespace macm {
 namespace spill {
+
 
 constexpr int W = 64;
 
@@ -87,8 +89,6 @@ __device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Norm
   x *= inv;
   y *= inv;
 }
-__device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
-__device__ __forceinline__ double wrap_pi(double t) { return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t; }
 
 // Exclusive scan over the block in thread order; returns the block total.
 __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
@@ -169,17 +169,25 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 // thread of the block must call it). `lds` holds layout(N, RECS_LDS).total bytes; the caller's
 // LDS contents are dead (a barrier on entry orders its last accesses). RECS_LDS = false keeps the
 // pair records in HBM (B.sp_rec) for callers whose LDS is smaller than 88 B per body.
-template <typename OT, bool RECS_LDS>
+// MODE kTdm (TDM.step, combat.py:104-184): called by the TDM wave kernel (64 threads) after it has
+// taken this step's actions, melee casts and deaths and committed them (angles, cooldowns, health,
+// alive flags, listener, counters 0-2); each lane passes its force `F`. The physics skips the bodies
+// that are not alive (their contacts were destroyed with their proxies) and the env layer is TDM's:
+// the body state, the [N, N-1, 4] observation, done / winner, counter 3.
+template <typename OT, bool RECS_LDS, int MODE = kFlock>
 __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers& B, int e, int cur,
                                          const void* __restrict__ actions, OT* __restrict__ obs,
                                          int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
                                          uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out,
-                                         unsigned char* lds) {
+                                         unsigned char* lds, const TdmParams* TP = nullptr,
+                                         const TdmBuffers* TB = nullptr, float2 F = make_float2(0.0f, 0.0f)) {
+  constexpr bool kT = MODE == kTdm;
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
   const int N = P.n_agents;
   const int C = P.max_contacts;
-  const bool act = tid < N;
+  const bool act = tid < N && (!kT || TB->alive[(size_t)e * N + tid] != 0);  // in the physics step
+  const unsigned long long livem = kT ? __ballot(act) : ~0ull;
   const size_t ag = (size_t)e * N + tid;
   const int nxt = cur ^ 1;
   const Layout L = layout(N, RECS_LDS);
@@ -228,21 +236,23 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   int a0 = 1, a1 = 1, a2 = 1;
   float ax = 0.0f, ay = 0.0f;
-  if (act) {
+  if (tid < N) {
     p = B.pos[ag];
     v = B.vel[ag];
     ang = B.angle[ag];
     fo = B.fat[ag];
     slp = B.sleep[ag];
-    if (P.action_mode == MACM_ACTION_DISCRETE) {
-      const uint8_t* a = (const uint8_t*)actions + ag * 3;
-      a0 = a[0]; a1 = a[1]; a2 = a[2];
-    } else {
-      const float2 c = ((const float2*)actions)[ag];
-      ax = c.x; ay = c.y;
+    if constexpr (!kT) {
+      if (P.action_mode == MACM_ACTION_DISCRETE) {
+        const uint8_t* a = (const uint8_t*)actions + ag * 3;
+        a0 = a[0]; a1 = a[1]; a2 = a[2];
+      } else {
+        const float2 c = ((const float2*)actions)[ag];
+        ax = c.x; ay = c.y;
+      }
+      tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
     }
-    tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
-    s_c[tid] = p;
+    s_c[tid] = p;  // TDM: dead bodies' positions too (the observation)
   }
   for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
   for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0u;
@@ -250,7 +260,12 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
 
   // ---- actions -> angle, force (mvmnt.py:97-129) -------------------------------------------
   float Fx = 0.0f, Fy = 0.0f;
-  if (act) {
+  if constexpr (kT) {
+    if (act) {
+      Fx = F.x;  // already m_force = 0 + F (the wave kernel's action loop)
+      Fy = F.y;
+    }
+  } else if (act) {
     if (P.action_mode == MACM_ACTION_DISCRETE) {
       float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
       const double ad = (double)af;
@@ -289,11 +304,14 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       ab = cab[k];
       lam = cimp[k];
       const int a = ab & 0xffffu, b = ab >> 16;
-      const float2 pa = s_c[a], pb = s_c[b];
-      const float dx = pb.x - pa.x, dy = pb.y - pa.y;
-      touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
-      atomicOr(&s_oldc[a >> 5], 1u << (a & 31));
-      atomicOr(&s_oldc[b >> 5], 1u << (b & 31));
+      // TDM: the contacts of a dead body were destroyed with its proxy (combat.py:162)
+      if (!kT || ((livem >> a) & (livem >> b) & 1ull)) {
+        const float2 pa = s_c[a], pb = s_c[b];
+        const float dx = pb.x - pa.x, dy = pb.y - pa.y;
+        touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
+        atomicOr(&s_oldc[a >> 5], 1u << (a & 31));
+        atomicOr(&s_oldc[b >> 5], 1u << (b & 31));
+      }
     }
     int pos;
     const int n = block_scan_excl(touch ? 1 : 0, pos, s_scan);
@@ -316,7 +334,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   {
     int off;
     block_scan_excl(deg, off, s_scan);
-    if (act) s_off[tid] = (uint32_t)off;
+    if (tid < N) s_off[tid] = (uint32_t)off;  // TDM: dead bodies too (s_off[b + 1] ends body b's edges)
     if (tid == 0) s_off[N] = (uint32_t)(2 * T);
     const unsigned long long m = __ballot(act && deg > 0);  // DFS seeds / unvisited bodies
     if ((tid & (W - 1)) == 0 && tid / W < (N + 63) / 64) s_todo[tid / W] = m;
@@ -572,6 +590,11 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     r0.fo = fo;
     r0.c = make_float2(cx, cy);
     recs[tid] = r0;
+  } else if (kT && tid < N) {  // a dead body: overlaps nothing, infinitely far
+    Rec r0;
+    r0.fn = r0.fo = make_float4(__builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff());
+    r0.c = make_float2(__builtin_inff(), __builtin_inff());
+    recs[tid] = r0;
   }
   __syncthreads();
 
@@ -626,7 +649,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       // touching at Collide, from the start-of-step positions (the state is not yet written back)
       const float2 pa = B.pos[(size_t)e * N + a], pb = B.pos[(size_t)e * N + b];
       const float dx = pb.x - pa.x, dy = pb.y - pa.y;
-      touch = !(dx * dx + dy * dy > rr);
+      touch = !(dx * dx + dy * dy > rr) && (!kT || ((livem >> a) & (livem >> b) & 1ull));
     }
     int tpos, kpos;
     const int tn = block_scan_excl(touch ? 1 : 0, tpos, s_scan);
@@ -648,52 +671,100 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     total = C;
   }
 
-  // ---- rewards (mvmnt.py:160-179) + obs (mvmnt.py:181-222) -------------------------------------------
-  float rew = 0.0f;
-  if (act) {
-    const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
-    const float td2 = tdx * tdx + tdy * tdy;
-    const double d = sqrt((double)td2);
-    if (coll) rew = -1.0f;
-    else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
-    else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
-    rew_out[ag] = rew;
-    if (coll_out) coll_out[ag] = coll ? 1 : 0;
-    if (nbr_out) nbr_out[ag] = bj;
-    if (obs) {
-      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-      const float2 cb = recs[bj].c;
-      write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
+  // ---- TDM: state write-back, TDM.get_obs (combat.py:166-167, 206-227), done / winner (:171-182) --------
+  if constexpr (kT) {
+    if (tid < N) {
+      if (act) {
+        B.pos[ag] = make_float2(cx, cy);
+        B.vel[ag] = make_float2(vx, vy);
+        B.fat[ag] = fn;
+        B.sleep[ag] = ns;
+      }
+      s_slp[tid] = ang;  // the sleep clocks are dead: the angles for the observation
     }
-  }
-  int dummy;
-  const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
-  const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
-  if (act) {
-    B.pos[ag] = make_float2(cx, cy);
-    B.vel[ag] = make_float2(vx, vy);
-    B.angle[ag] = ang;
-    B.fat[ag] = fn;
-    B.sleep[ag] = ns;
-  }
-  if (tid == 0) {
-    const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz (mvmnt.py:134-136)
-    const uint8_t dn = tp > P.time_limit ? 1 : 0;
-    B.time_passed[e] = tp;
-    B.done[e] = dn;
-    if (done_out) done_out[e] = dn;
-    B.step_count[e] = step_count + 1;
-    B.ccount[nxt][e] = total;
-    if (status) {
-      B.status[e] |= status;
-      report_status(B, status);
+    __syncthreads();
+    const size_t rows = (size_t)e * N * (N - 1);
+    MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, livem, *TP,
+                     s_c, s_slp);
+    int alive_teams = 0, last_team = -1;
+    const int myteam = tdm_team_of(*TP, tid);
+    for (int t = 0; t < TP->n_teams; ++t)
+      if (__ballot(act && myteam == t)) {
+        ++alive_teams;
+        last_team = t;
+      }
+    if (tid == 0) {
+      const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz
+      uint8_t dn = tp > P.time_limit ? 1 : 0;
+      int win = TB->winner[e];
+      if (B.done[e]) dn = 1;  // done latches
+      if (alive_teams == 1) {
+        dn = 1;
+        win = last_team;
+      }
+      if (alive_teams == 0) dn = 1;
+      TB->winner[e] = win;
+      if (TB->winner_out) TB->winner_out[e] = win;
+      B.time_passed[e] = tp;
+      B.done[e] = dn;
+      if (done_out) done_out[e] = dn;
+      B.step_count[e] = step_count + 1;
+      B.ccount[nxt][e] = total;
+      if (status) {
+        B.status[e] |= status;
+        report_status(B, status);
+      }
+      B.env_counters[(size_t)e * 4 + 3] += (unsigned long long)dn;  // counters 0-2: the wave kernel
+      if (B.spill_count) B.spill_count[e] += 1u;
     }
-    unsigned long long* ec = B.env_counters + (size_t)e * 4;
-    ec[0] += (unsigned long long)N;
-    ec[1] += (unsigned long long)ncoll;
-    ec[2] += (unsigned long long)npos;
-    ec[3] += (unsigned long long)dn;
-    if (B.spill_count) B.spill_count[e] += 1u;
+  } else {
+    // ---- rewards (mvmnt.py:160-179) + obs (mvmnt.py:181-222) -------------------------------------------
+    float rew = 0.0f;
+    if (act) {
+      const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
+      const float td2 = tdx * tdx + tdy * tdy;
+      const double d = sqrt((double)td2);
+      if (coll) rew = -1.0f;
+      else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
+      else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
+      rew_out[ag] = rew;
+      if (coll_out) coll_out[ag] = coll ? 1 : 0;
+      if (nbr_out) nbr_out[ag] = bj;
+      if (obs) {
+        const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+        const float2 cb = recs[bj].c;
+        write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
+      }
+    }
+    int dummy;
+    const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
+    const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
+    if (act) {
+      B.pos[ag] = make_float2(cx, cy);
+      B.vel[ag] = make_float2(vx, vy);
+      B.angle[ag] = ang;
+      B.fat[ag] = fn;
+      B.sleep[ag] = ns;
+    }
+    if (tid == 0) {
+      const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz (mvmnt.py:134-136)
+      const uint8_t dn = tp > P.time_limit ? 1 : 0;
+      B.time_passed[e] = tp;
+      B.done[e] = dn;
+      if (done_out) done_out[e] = dn;
+      B.step_count[e] = step_count + 1;
+      B.ccount[nxt][e] = total;
+      if (status) {
+        B.status[e] |= status;
+        report_status(B, status);
+      }
+      unsigned long long* ec = B.env_counters + (size_t)e * 4;
+      ec[0] += (unsigned long long)N;
+      ec[1] += (unsigned long long)ncoll;
+      ec[2] += (unsigned long long)npos;
+      ec[3] += (unsigned long long)dn;
+      if (B.spill_count) B.spill_count[e] += 1u;
+    }
   }
   release_slot(B, slot);
 }

@@ -109,8 +109,6 @@ __device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Norm
   x *= inv;
   y *= inv;
 }
-__device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
-__device__ __forceinline__ double wrap_pi(double t) { return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t; }
 
 struct __align__(16) Rec {  // per-agent record for the pair sweep (48 B with float4 alignment)
   float4 fn;               // new fat AABB

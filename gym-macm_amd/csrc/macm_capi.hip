@@ -1011,12 +1011,15 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(MACM_E_INVALID, "device index out of range");
   DeviceGuard g(device);
+  size_t free_bytes = 0, total_bytes = 0;
+  HIP_TRY(hipMemGetInfo(&free_bytes, &total_bytes));
 
   macm_tdm* w = new macm_tdm();
   w->cfg = c;
   w->device = device;
   w->cur = 0;
   const int C = N * (N - 1) / 2;  // every pair: the list never overflows
+  const int64_t SL = default_capacity(N, n_envs, C, free_bytes).slots;  // spill working-set slots
   StepParams& P = w->P;
   memset(&P, 0, sizeof(P));
   P.n_envs = n_envs;
@@ -1066,7 +1069,14 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
       (rc = dalloc(A, &B.env_counters, E * 4)) || (rc = dalloc(A, &TB.health, EN)) ||
       (rc = dalloc(A, &TB.cd_atk, EN)) || (rc = dalloc(A, &TB.cd_mov, EN)) || (rc = dalloc(A, &TB.alive, EN)) ||
       (rc = dalloc(A, &TB.listener, E)) || (rc = dalloc(A, &TB.winner, E)) || (rc = dalloc(A, &w->bad, 1)) ||
-      (rc = dalloc(A, &w->mt, E * kMtStride)) || (rc = dalloc(A, &w->rmask, E))) {
+      (rc = dalloc(A, &w->mt, E * kMtStride)) || (rc = dalloc(A, &w->rmask, E)) ||
+      // the spill step's working set (an env with more than 256 touching contacts or 16 per body):
+      // C = every pair; its body records in HBM too (the TDM kernel's LDS pool holds the rest)
+      (rc = dalloc(A, &B.sp_tab, (size_t)SL * C)) || (rc = dalloc(A, &B.sp_adj, (size_t)SL * 2 * C)) ||
+      (rc = dalloc(A, &B.sp_ord, (size_t)SL * C)) || (rc = dalloc(A, &B.sp_cst, (size_t)SL * C)) ||
+      (rc = dalloc(A, &B.sp_cim, (size_t)SL * C)) || (rc = dalloc(A, &B.sp_lam, (size_t)SL * C)) ||
+      (rc = dalloc(A, (float4**)&B.sp_rec, (size_t)SL * N * 3)) ||  // 48-B records
+      (SL < n_envs && (rc = dalloc(A, &B.sp_lock, (size_t)SL))) || (rc = dalloc(A, &B.spill_count, E))) {
     free_tdm(w);
     delete w;
     return rc;
@@ -1079,6 +1089,9 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   hipError_t e = hipMemset(B.env_counters, 0, E * 4 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * E);
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * E);
+  if (e == hipSuccess) e = hipMemset(B.spill_count, 0, sizeof(uint32_t) * E);
+  B.sp_pool = SL < n_envs ? (int32_t)SL : 0;
+  if (e == hipSuccess && B.sp_lock) e = hipMemset(B.sp_lock, 0, sizeof(uint32_t) * SL);
   if (e != hipSuccess) {
     free_tdm(w);
     delete w;
@@ -1347,6 +1360,37 @@ int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream) {
   unsigned long long acc[4] = {0, 0, 0, 0};
   for (size_t i = 0; i < h.size(); ++i) acc[i & 3] += h[i];
   for (int i = 0; i < 4; ++i) out[i] = (int64_t)acc[i];
+  return MACM_OK;
+}
+
+int macm_tdm_spilled(macm_tdm* w, int64_t* env_steps, void* stream) {
+  if (!w || !env_steps) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  std::vector<uint32_t> h((size_t)w->P.n_envs);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(h.data(), w->B.spill_count, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  int64_t acc = 0;
+  for (uint32_t v : h) acc += v;
+  *env_steps = acc;
+  return MACM_OK;
+}
+
+int macm_tdm_set_debug(macm_tdm* w, int32_t flags) {
+  if (!w) return fail(MACM_E_INVALID, "world is NULL");
+  const int pool = (flags & MACM_DEBUG_SPILL_POOL) ? (flags >> 8) : 0;
+  flags &= 0xff;
+  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SPILL_POOL))
+    return fail(MACM_E_INVALID, "unknown debug flag (TDM: FORCE_SPILL, SPILL_POOL)");
+  if (flags & MACM_DEBUG_SPILL_POOL) {
+    const int have = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;  // slots allocated
+    if (pool < 1 || pool > have) return fail(MACM_E_INVALID, "SPILL_POOL: 1 <= slots <= the slots allocated");
+    DeviceGuard g(w->device);
+    if (!w->B.sp_lock && dalloc(w->allocs, &w->B.sp_lock, (size_t)have)) return MACM_E_OOM;
+    HIP_TRY(hipMemset(w->B.sp_lock, 0, sizeof(uint32_t) * have));
+    w->B.sp_pool = pool;
+  }
+  w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
   return MACM_OK;
 }
 

@@ -1,0 +1,141 @@
+// tdm_obs.hpp — TDM.get_obs (gym_macm/envs/combat.py:206-227) as fixed [N, N-1, 4] slots, written
+// by one 64-lane wave: shared by the wave kernel (flock_step_w64.hip) and the spill step
+// (flock_spill.hpp), which steps TDM envs beyond the wave kernel's contact capacities.
+#pragma once
+
+#include "flock_common.hpp"
+
+namespace macm {
+
+__device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
+
+// t = t - np.sign(t) * 2 * np.pi if np.abs(t) > np.pi else t      (mvmnt.py:199,214)
+__device__ __forceinline__ double wrap_pi(double t) {
+  return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t;
+}
+
+
+template <typename OT>
+__device__ __forceinline__ void store4(OT* o, double a, double b, double c, double d) {
+  if constexpr (sizeof(OT) == 4) {
+    *reinterpret_cast<float4*>(o) = make_float4((float)a, (float)b, (float)c, (float)d);
+  } else {
+    reinterpret_cast<double2*>(o)[0] = make_double2(a, b);
+    reinterpret_cast<double2*>(o)[1] = make_double2(c, d);
+  }
+}
+
+// TDM.get_obs (combat.py:206-227) as fixed slots: slot k of agent i is the other
+// agent j = k < i ? k : k + 1, holding (r, t, p, is_ally) with rel = other - agent
+// (float32), r = sqrt(b2DistanceSquared), t = atan2(rel) - angle_i and
+// p = angle_j - angle_i each wrapped once; mask = both alive, masked slots zero.
+// One unordered pair {i, j} (i < j) per lane: the lane writes slot (i, j) and slot (j, i).
+// Both directions share r (|rel| is the same), the ally flag, the mask and atan2's
+// reduction and polynomial (obs_atan2_core of |rel.x|, |rel.y|); each keeps its own
+// rel = other - agent (float32), quadrant, "- angle" and wrap, so every value is bit-identical
+// to evaluating the two slots separately, with half the f64 atan2 work.
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __restrict__ mask, int S, int i, int j,
+                                             unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                             const float* sa) {
+  const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
+  double r = 0.0, t1 = 0.0, t2 = 0.0, p1 = 0.0, p2 = 0.0, ty = 0.0;
+  if (m) {
+    const float2 ci = sc[i], cj = sc[j];
+    const float xi = ci.x, yi = ci.y, xj = cj.x, yj = cj.y, ai = sa[i], aj = sa[j];
+    const float rx = xj - xi, ry = yj - yi;  // row i: other.position - agent.position
+    const float qx = xi - xj, qy = yi - yj;  // row j
+    const float d2 = rx * rx + ry * ry;      // b2DistanceSquared (the same for row j)
+    r = obs_sqrt<OT>(d2);
+    const double core = obs_atan2_core(fabs((double)rx), fabs((double)ry));
+    t1 = wrap_pi(obs_atan2_finish(core, (double)ry, (double)rx) - (double)ai);
+    t2 = wrap_pi(obs_atan2_finish(core, (double)qy, (double)qx) - (double)aj);
+    p1 = wrap_pi((double)aj - (double)ai);
+    p2 = wrap_pi((double)ai - (double)aj);
+    ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
+  }
+  const size_t s1 = (size_t)i * S + (j - 1), s2 = (size_t)j * S + i;
+  if (obs) {
+    store4<OT>(obs + s1 * 4, r, t1, p1, ty);
+    store4<OT>(obs + s2 * 4, r, t2, p2, ty);
+  }
+  if (mask) {
+    mask[s1] = m ? 1 : 0;
+    mask[s2] = m ? 1 : 0;
+  }
+}
+
+// The pairs in 8 x 8 tiles (agent blocks I < J), one tile per pass: lane (a, b) = (lane / 8,
+// lane % 8) takes pair (8I + a, 8J + b). A store instruction then writes 8 runs of 8
+// consecutive slots for both directions (rows 8I + a, and rows 8J + b), so whole L2 lines fill
+// within one instruction; the row-major pair order left the (j, i) half as a column walk of
+// single 16-B slots, and lines left L2 partly written (+37% HBM writes). The diagonal tiles'
+// 28 pairs (a < b) go two tiles per pass.
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
+                                              unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                              const float* sa) {
+  const int S = N - 1;
+  const int nb = (N + 7) >> 3;
+  const int a = lane >> 3, b = lane & 7;
+  for (int I = 0; I < nb; ++I) {
+    const int i = 8 * I + a;
+    for (int J = I + 1; J < nb; ++J) {
+      const int j = 8 * J + b;
+      if (i < N && j < N) tdm_obs_pair<OT>(obs, mask, S, i, j, livem, TP, sc, sa);
+    }
+  }
+  // diagonal tiles: pair k < 28 of tile D (row-major over r < c) on lane 32 (D & 1) + k
+  const int k = lane & 31;
+  int r = 0, rem = k;
+  while (r < 7 && rem >= 7 - r) {
+    rem -= 7 - r;
+    ++r;
+  }
+  const int c = r + 1 + rem;
+  for (int D0 = 0; D0 < nb; D0 += 2) {
+    const int D = D0 + (lane >> 5);
+    const int i = 8 * D + r, j = 8 * D + c;
+    if (k < 28 && D < nb && j < N) tdm_obs_pair<OT>(obs, mask, S, i, j, livem, TP, sc, sa);
+  }
+}
+
+// The same slots in memory order: lane q of each pass writes slot q of the env's [N, N-1] block,
+// so one store instruction covers 64 consecutive slots (1 KB: whole 128-B lines; an env's block is
+// N (N-1) 16 B, a multiple of 128 B for N = 32) and the mask 64 consecutive bytes. Each slot
+// computes its own atan2 (no sharing between the two directions of a pair).
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_linear(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
+                                               unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                               const float* sa) {
+  const int S = N - 1, ns = N * S;
+  int i = lane / S, k = lane - i * S;  // slot q = i * S + k, advanced by 64 per pass
+  for (int q = lane; q < ns; q += 64) {
+    const int j = k < i ? k : k + 1;
+    const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
+    double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
+    if (m) {
+      const float2 ci = sc[i], cj = sc[j];
+      const float rx = cj.x - ci.x, ry = cj.y - ci.y;
+      r = obs_sqrt<OT>(rx * rx + ry * ry);
+      t = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)sa[i]);
+      p = wrap_pi((double)sa[j] - (double)sa[i]);
+      ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
+    }
+    if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
+    if (mask) mask[q] = m ? 1 : 0;
+    k += 64;
+    while (k >= S) {
+      k -= S;
+      ++i;
+    }
+  }
+}
+
+#ifdef MACM_TDM_OBS_LINEAR
+#define MACM_TDM_OBS tdm_obs_linear
+#else
+#define MACM_TDM_OBS tdm_obs_pairs
+#endif
+
+}  // namespace macm

@@ -258,12 +258,23 @@ class TdmWorld:
         return int(v.value)
 
     def check_status(self) -> None:
-        """Raise MacmOverflowError if any env overflowed the TDM kernel's contact capacities
-        (256 touching contacts, 16 per body; synchronises the stream)."""
+        """Raise MacmOverflowError if any env has a status bit set (synchronises the stream). Dense
+        envs take the spill step (no capacity bit); only a pooled working set's SPILL_WAIT remains."""
         st = self.status()
         if st:
             raise _abi.MacmOverflowError(_abi.E_OVERFLOW, "macm_tdm_status",
-                                         f"status bits {st}: an env outgrew the TDM kernel's contact capacities")
+                                         f"status bits {st}: an env was not stepped as the reference")
+
+    def spilled(self) -> int:
+        """Env-steps taken by the spill step (envs beyond 256 touching contacts or 16 per body)."""
+        v = ctypes.c_int64()
+        _abi.check(self.L.macm_tdm_spilled(self.h, ctypes.byref(v), self._stream()), "macm_tdm_spilled")
+        return int(v.value)
+
+    def set_debug(self, flags: int) -> None:
+        """Test hooks (macm_tdm_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the spill
+        step; DEBUG_SPILL_POOL | slots << 8 shares that many working-set slots."""
+        _abi.check(self.L.macm_tdm_set_debug(self.h, int(flags)), "macm_tdm_set_debug")
 
     def counters(self) -> np.ndarray:
         out = (ctypes.c_int64 * 4)()

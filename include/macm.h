@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 5
+#define MACM_ABI_VERSION 6
 
 enum {
   MACM_OK = 0,
@@ -53,10 +53,11 @@ enum { MACM_REWARD_BINARY = 0, MACM_REWARD_LINEAR = 1 };
 enum { MACM_COORD_POLAR = 0, MACM_COORD_CARTESIAN = 1 };
 
 /*
- * Status bits accumulated per env on the device (macm_world_status). Flock never sets
- * TOUCH/DEGREE: an env whose touching contacts exceed a fast kernel's LDS capacity is stepped
- * by the spill step (HBM working set sized by max_contacts) instead. CONTACT_OVERFLOW (the
- * fat-AABB pair list itself outgrew max_contacts) and TDM's TOUCH/DEGREE caps remain. Detection
+ * Status bits accumulated per env on the device (macm_world_status). TOUCH/DEGREE are no longer
+ * set (ABI 6): an env of either kind whose touching contacts exceed a fast kernel's LDS capacity
+ * is stepped by the spill step (HBM working set sized by max_contacts) instead. CONTACT_OVERFLOW
+ * (the fat-AABB pair list itself outgrew max_contacts; never for TDM, whose list holds every
+ * pair) and SPILL_WAIT remain. Detection
  * is eventual, not synchronous: the kernels store the bits into a host-mapped word, and each step /
  * rollout call reads it before launching, without synchronising, so steps already queued behind an
  * overflowing one still run (and a rollout keeps stepping the overflowed env for its K steps); the
@@ -66,14 +67,15 @@ enum { MACM_COORD_POLAR = 0, MACM_COORD_CARTESIAN = 1 };
  */
 enum {
   MACM_ST_CONTACT_OVERFLOW = 1, /* Ov(F_t) list exceeded max_contacts                   */
-  MACM_ST_TOUCH_OVERFLOW = 2,   /* TDM: touching contacts exceeded the solver capacity   */
-  MACM_ST_DEGREE_OVERFLOW = 4,  /* TDM: a body touched more bodies than the adjacency cap */
+  MACM_ST_TOUCH_OVERFLOW = 2,   /* (before ABI 6) TDM touching contacts beyond capacity  */
+  MACM_ST_DEGREE_OVERFLOW = 4,  /* (before ABI 6) TDM body degree beyond capacity        */
   MACM_ST_INVALID_ACTION = 8,   /* validate_actions: an action outside the action space  */
   MACM_ST_SPILL_WAIT = 16       /* a dense env found no free spill working-set slot for ~1 s
                                    (a pooled world: fewer slots than envs) and was not stepped */
 };
 
-/* macm_world_set_debug flags (test hooks; 0 = product behaviour). */
+/* macm_world_set_debug / macm_tdm_set_debug flags (test hooks; 0 = product behaviour; TDM takes
+ * FORCE_SPILL and SPILL_POOL). */
 enum {
   MACM_DEBUG_FORCE_SPILL = 1,     /* every env takes the spill step (parity tests of that path)  */
   MACM_DEBUG_SWEEP_CELLS = 2,     /* N > 64: pair sweep over strip cells at any N (else N >= 512) */
@@ -433,8 +435,10 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
 /*
  * One TDM.step for all E envs (combat.py:104-184). actions: device uint8
  * [E, N, 4] (MultiDiscrete([3,3,3,2]): forward, lateral, rotation, attack);
- * rows of dead agents are ignored. Returns MACM_E_OVERFLOW if a capacity (256 touching
- * contacts, 16 per body) overflowed in an earlier step; MACM_E_INVALID with validate_actions.
+ * rows of dead agents are ignored. An env with more than 256 touching contacts or a body touching
+ * more than 16 others (a crowded small world) is stepped by the spill step (HBM working set,
+ * every pair; after its actions, casts and deaths) with the same results. MACM_E_INVALID with
+ * validate_actions; MACM_E_OVERFLOW only after a SPILL_WAIT (pooled working set).
  */
 int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream);
 
@@ -466,6 +470,12 @@ int macm_tdm_status(macm_tdm* w, int32_t* status_or, void* stream);
 
 /* out[0] alive agent-steps, out[1] melee attacks, out[2] deaths, out[3] env-steps with done. */
 int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream);
+
+/* Env-steps taken by the spill step since creation (ABI 6). */
+int macm_tdm_spilled(macm_tdm* w, int64_t* env_steps, void* stream);
+
+/* Test hooks: MACM_DEBUG_FORCE_SPILL, MACM_DEBUG_SPILL_POOL (ABI 6). */
+int macm_tdm_set_debug(macm_tdm* w, int32_t flags);
 
 /* ---- scripted actors on the device (test_scripts/bots.py) ------------------
  * Read an observation tensor written by a step and write the next actions, so a

@@ -8,8 +8,8 @@ by max_contacts) inside the same launch. Bar: bit-exact against the oracle for >
 status 0, and the spill step must actually have run (macm_world_spilled > 0).
 
 Also here: the spill step forced for every env (MACM_DEBUG_FORCE_SPILL) at ordinary densities,
-loud errors for what can still overflow (an explicit small max_contacts; TDM's caps), set_state
-validation, and the opt-in action validation (mvmnt.py:94 / combat.py:118)."""
+loud errors for what can still overflow (an explicit small max_contacts), set_state validation,
+and the opt-in action validation (mvmnt.py:94 / combat.py:118). TDM's dense envs: test_gpu_tdm_spill.py."""
 import random
 
 import numpy as np
@@ -183,21 +183,6 @@ def test_reset_envs_clears_the_overflow_of_the_envs_it_resets():
     v.reset_envs(torch.tensor([0, 1], dtype=torch.uint8, device="cuda:0"))
     assert v.status() == 0
     v.step(a)  # the overflowed env was reset: stepping resumes
-
-
-def test_tdm_capacity_overflow_raises():
-    """TDM keeps the wave kernel's caps (no spill step): 64 agents spawned in a 3 x 3 m world
-    exceed 256 touching contacts and the next step raises instead of stepping on truncated data."""
-    from gym_macm.tdm_world import TdmWorld, tdm_config
-    w = TdmWorld(tdm_config([32, 32], world_width=3.0, world_height=3.0), 2, device="cuda:0")
-    w.reset(5)
-    a = torch.ones((2, 64, 4), dtype=torch.uint8, device="cuda:0")
-    a[..., 3] = 0
-    w.step(a)
-    torch.cuda.synchronize()
-    assert w.status() & (_abi.ST_TOUCH_OVERFLOW | _abi.ST_DEGREE_OVERFLOW)
-    with pytest.raises(_abi.MacmOverflowError):
-        w.step(a)
 
 
 def test_set_state_rejects_invalid_lists():
