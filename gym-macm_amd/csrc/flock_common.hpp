@@ -85,7 +85,7 @@ struct WorldBuffers {
   uint32_t* x_tab;               // [E, tcap] touching contacts in list order (a | b << 16)
   uint32_t* x_adj;               // [E, 2 tcap] CSR edges: touching index | other body << 16
   uint16_t* x_off;               // [E, N + 1] CSR offsets ([N] = 2 T)
-  uint32_t* x_dfs;               // [E, tcap] island order: touching index | level << 16
+  uint32_t* x_dfs;               // [E, tcap] island order: CSR edge slot (x_adj) | level << 16
   // Spill step (flock_spill.hpp): HBM working set for envs whose touching contacts exceed the fast
   // kernels' LDS capacities, capacity C = max_contacts per slot (touching contacts are in the list).
   // S slots: S = E (slot = env) when the memory budget allows, else a pool that a spilling env

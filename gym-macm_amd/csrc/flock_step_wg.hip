@@ -990,7 +990,7 @@ namespace wg {
 // per-body level bookkeeping, the stack, the unvisited-body and visited-contact bitmasks, the
 // island contact starts. The level counts of the records' counting sort reuse the edges.
 struct WgLayoutD {
-  int adj, off, last, stk, todo, cvis, ic, total;
+  int adj, off, last, stk, todo, pop, ic, total;
 };
 __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
   WgLayoutD L;
@@ -1000,12 +1000,12 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
     o = align16(o + bytes);
     return r;
   };
-  L.adj = take(8 * tcap);
+  L.adj = take(4 * tcap);  // 2 tcap edges: the other body (u16); reused as the level counts (u32)
   L.off = take(2 * (N + 1));
   L.last = take(2 * N);
   L.stk = take(2 * N);
   L.todo = take(8 * ((N + 63) / 64));
-  L.cvis = take(4 * ((tcap + 31) / 32));
+  L.pop = take(8 * ((N + 63) / 64));
   L.ic = take(2 * (N / 2 + 2));
   L.total = o;
   return L;
@@ -1015,8 +1015,10 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
 // Kernel A2 (dense envs): the island DFS in Box2D order by one wave (the wave-parallel walk of
 // kernel A: a popped body's edges one per lane, levels by a prefix maximum), then the Gauss-Seidel
 // levels' counting sort and the level-ordered records for kernel B. Same order, levels and records
-// as kernel A's walk; the edge carries its other body, so a popped body's contacts take one LDS
-// round trip fewer (edge -> {visited bit, todo bit, level, CSR range} instead of edge -> pair -> ...).
+// as kernel A's walk. An edge in LDS is only its other body (2 B: 26 KB of LDS at C5, 6 envs per CU
+// instead of 3 with 4-B edges and a visited bit per contact): a contact is new iff its other body
+// has not been popped yet (the first of its two bodies to be popped walks it), and the walk writes
+// the edge's CSR slot, which the record pass turns into the contact through x_adj.
 __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -1026,12 +1028,12 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   if (B.x_nisl[e] != kDfsPending) return;  // kernel A walked it, or the spill step stepped it
   WSTAMP(26);
   const WgLayoutD L = wg_layout_d(N, tcap);
-  uint32_t* s_adj = (uint32_t*)(lds + L.adj);
+  uint16_t* s_adj = (uint16_t*)(lds + L.adj);
   uint16_t* s_off = (uint16_t*)(lds + L.off);
   uint16_t* s_last = (uint16_t*)(lds + L.last);
   uint16_t* s_stk = (uint16_t*)(lds + L.stk);
   unsigned long long* s_todo = (unsigned long long*)(lds + L.todo);
-  uint32_t* s_cvis = (uint32_t*)(lds + L.cvis);
+  unsigned long long* s_pop = (unsigned long long*)(lds + L.pop);  // bodies popped
   uint16_t* s_ic = (uint16_t*)(lds + L.ic);
   const int IS = wg_isl_stride(N);
   const uint16_t* xoff = B.x_off + (size_t)e * (N + 1);
@@ -1041,9 +1043,9 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   uint16_t* xib = B.x_ib + (size_t)e * IS;
   const int T2 = xoff[N];
   for (int b = lane; b <= N; b += W) s_off[b] = xoff[b];
-  for (int q = lane; q < T2; q += W) s_adj[q] = xadj[q];
+  for (int q = lane; q < T2; q += W) s_adj[q] = (uint16_t)(xadj[q] >> 16);
   for (int b = lane; b < N; b += W) s_last[b] = 0;
-  for (int q = lane; q < (tcap + 31) / 32; q += W) s_cvis[q] = 0u;
+  for (int w = lane; w < (N + 63) / 64; w += W) s_pop[w] = 0ull;
   __syncthreads();
   for (int w = 0; w < (N + 63) / 64; ++w) {  // bodies with touching edges: DFS seeds / unvisited
     const int b = w * 64 + lane;
@@ -1086,31 +1088,30 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         xcur = s_last[bdy];
       }
       top_b = -1;
-      if (lane == 0) xibod[nb] = (uint16_t)bdy;
+      if (lane == 0) {
+        xibod[nb] = (uint16_t)bdy;
+        s_pop[bdy >> 6] |= 1ull << (bdy & 63);  // read by later pops only (no contact joins bdy to itself)
+      }
       ++nb;
       // levels of the new contacts c_1..c_m of bdy in order: X_i = i + max(X_0, max_{j<=i}(y_j - j + 1))
       // (see par_walk in kernel A)
       for (int q0 = e0; q0 < e1; q0 += W) {
         const int q = q0 + lane;
-        int t = 0, o = 0, lo = 0, oe0 = 0, oe1 = 0;
-        uint32_t cv = 0xffffffffu;
-        unsigned long long tw = 0ull;
+        int o = 0, lo = 0, oe0 = 0, oe1 = 0;
+        unsigned long long tw = 0ull, pw = ~0ull;
         if (q < e1) {  // one round of LDS reads after the edge's
-          const uint32_t ed = s_adj[q];
-          t = ed & 0xffffu;
-          o = ed >> 16;
-          cv = s_cvis[t >> 5];
+          o = s_adj[q];
+          pw = s_pop[o >> 6];
           tw = s_todo[o >> 6];
           lo = s_last[o];
           oe0 = s_off[o];
           oe1 = s_off[o + 1];
         }
-        const bool newc = !((cv >> (t & 31)) & 1u);
+        const bool newc = !((pw >> (o & 63)) & 1ull);  // the contact was walked iff o was popped
         const unsigned long long mc = __ballot(newc);
         int rank = 0, z = -0x3fffffff, xi = 0;
         bool push = false;
         if (newc) {
-          atomicOr(&s_cvis[t >> 5], 1u << (t & 31));
           rank = __popcll(mc & lt) + 1;
           push = (tw >> (o & 63)) & 1ull;
           z = lo - rank + 1;
@@ -1119,7 +1120,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         if (newc) {
           xi = rank + max(xcur, z);
           s_last[o] = (uint16_t)xi;
-          xdfs[nord + rank - 1] = (uint32_t)t | ((uint32_t)(xi - 1) << 16);
+          xdfs[nord + rank - 1] = (uint32_t)q | ((uint32_t)(xi - 1) << 16);  // CSR slot: < 2 tcap <= 9216
         }
         const int mnew = __popcll(mc);
         if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
@@ -1156,7 +1157,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   WSTAMP(27);
 
   // ---- Gauss-Seidel levels: counting sort into level order; the records for kernel B ------------
-  uint32_t* s_cnt = s_adj;  // [dmax + 1] (the edges are dead; dmax <= T <= tcap)
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_adj);  // [dmax + 1] (edges dead; dmax <= T <= tcap)
   for (int l = lane; l <= dmax; l += W) s_cnt[l] = 0u;
   __syncthreads();
   for (int k = lane; k < nord; k += W) atomicAdd(&s_cnt[xdfs[k] >> 16], 1u);
@@ -1187,7 +1188,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   const float2* pos = B.pos + (size_t)e * N;
   for (int k = lane; k < nord; k += W) {
     const uint32_t d = xdfs[k];
-    const int t = d & 0xffffu, lv = d >> 16;
+    const int t = xadj[d & 0xffffu] & 0xffffu, lv = d >> 16;  // CSR slot -> contact
     const uint32_t ab = xt[t];
     const int a = ab & 0xffffu, b = ab >> 16;
     const float2 pa = pos[a], pb = pos[b];  // the start-of-step positions (kernel C writes them back)

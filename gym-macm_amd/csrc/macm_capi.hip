@@ -634,7 +634,10 @@ static macm_outputs step_outputs(const macm_world* w, const macm_outputs* out, i
 // 481 with 3, but 744 with 4: with the caller's stream that is more streams than the process's 4
 // hardware queues (GPU_MAX_HW_QUEUES), and two slices sharing a queue serialise each other's
 // launches. C5 (N = 1024, 2048 envs) gained nothing (profiles/r02/rollout/).
-static constexpr int kSlices = 2, kSliceMinEnvs = 1024, kSliceMaxAgents = 512;
+#ifndef MACM_SLICE_MAX_AGENTS  // A/B knob
+#define MACM_SLICE_MAX_AGENTS 512
+#endif
+static constexpr int kSlices = 2, kSliceMinEnvs = 1024, kSliceMaxAgents = MACM_SLICE_MAX_AGENTS;
 // astride == 0: the closed loop (macm_world_rollout_bots): every step of a slice reads the bot's
 // action rows of its envs and the bots kernel writes the next ones from the slice's obs rows
 // (trajectory form: step k reads action row k and writes row k + 1 of [K + 1, E, N, 3]).

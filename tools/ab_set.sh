@@ -18,6 +18,7 @@ args() {
     c4) echo "--env tdm --steps 20 --warmup 5" ;;
     c4bots) echo "--env tdm --policy bots --steps 100 --warmup 100" ;;
     c5) echo "--envs 2048 --agents 1024 --steps 10 --warmup 2 --launch step" ;;
+    c5r) echo "--envs 2048 --agents 1024 --steps 10 --warmup 2" ;;            # rollout form (driver)
   esac
 }
 for r in 1 2; do
