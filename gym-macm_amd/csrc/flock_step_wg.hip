@@ -1000,7 +1000,11 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
     o = align16(o + bytes);
     return r;
   };
-  L.adj = take(4 * tcap);  // 2 tcap edges: the other body (u16); reused as the level counts (u32)
+  // 2 tcap edges, the other body (10 bits, N <= 1024) three to a word; adj..stk are reused as the
+  // level counts (u32 [T + 1], T <= tcap)
+  const int rest = align16(2 * (N + 1)) + align16(2 * N) + align16(2 * N);
+  const int packed = 4 * ((2 * tcap + 2) / 3);
+  L.adj = take(packed > 4 * (tcap + 1) - rest ? packed : 4 * (tcap + 1) - rest);
   L.off = take(2 * (N + 1));
   L.last = take(2 * N);
   L.stk = take(2 * N);
@@ -1015,10 +1019,11 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
 // Kernel A2 (dense envs): the island DFS in Box2D order by one wave (the wave-parallel walk of
 // kernel A: a popped body's edges one per lane, levels by a prefix maximum), then the Gauss-Seidel
 // levels' counting sort and the level-ordered records for kernel B. Same order, levels and records
-// as kernel A's walk. An edge in LDS is only its other body (2 B: 26 KB of LDS at C5, 6 envs per CU
-// instead of 3 with 4-B edges and a visited bit per contact): a contact is new iff its other body
-// has not been popped yet (the first of its two bodies to be popped walks it), and the walk writes
-// the edge's CSR slot, which the record pass turns into the contact through x_adj.
+// as kernel A's walk. An edge in LDS is only its other body, 10 bits, three to a word (19.3 KB of
+// LDS at C5: 8 envs per CU, all 2048 of a C5 shard resident; 4-B edges and a visited bit per
+// contact took 45 KB, 3 per CU): a contact is new iff its other body has not been popped yet (the
+// first of its two bodies to be popped walks it), and the walk writes the edge's CSR slot, which
+// the record pass turns into the contact through x_adj.
 __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -1028,7 +1033,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   if (B.x_nisl[e] != kDfsPending) return;  // kernel A walked it, or the spill step stepped it
   WSTAMP(26);
   const WgLayoutD L = wg_layout_d(N, tcap);
-  uint16_t* s_adj = (uint16_t*)(lds + L.adj);
+  uint32_t* s_adj = (uint32_t*)(lds + L.adj);
   uint16_t* s_off = (uint16_t*)(lds + L.off);
   uint16_t* s_last = (uint16_t*)(lds + L.last);
   uint16_t* s_stk = (uint16_t*)(lds + L.stk);
@@ -1043,7 +1048,11 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   uint16_t* xib = B.x_ib + (size_t)e * IS;
   const int T2 = xoff[N];
   for (int b = lane; b <= N; b += W) s_off[b] = xoff[b];
-  for (int q = lane; q < T2; q += W) s_adj[q] = (uint16_t)(xadj[q] >> 16);
+  for (int wq = lane; 3 * wq < T2; wq += W) {
+    const int q = 3 * wq;
+    const uint32_t o0 = xadj[q] >> 16, o1 = q + 1 < T2 ? xadj[q + 1] >> 16 : 0u, o2 = q + 2 < T2 ? xadj[q + 2] >> 16 : 0u;
+    s_adj[wq] = o0 | (o1 << 10) | (o2 << 20);
+  }
   for (int b = lane; b < N; b += W) s_last[b] = 0;
   for (int w = lane; w < (N + 63) / 64; w += W) s_pop[w] = 0ull;
   __syncthreads();
@@ -1100,7 +1109,8 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         int o = 0, lo = 0, oe0 = 0, oe1 = 0;
         unsigned long long tw = 0ull, pw = ~0ull;
         if (q < e1) {  // one round of LDS reads after the edge's
-          o = s_adj[q];
+          const uint32_t qw = (uint32_t)q / 3u;
+          o = (s_adj[qw] >> (10u * ((uint32_t)q - 3u * qw))) & 1023u;
           pw = s_pop[o >> 6];
           tw = s_todo[o >> 6];
           lo = s_last[o];
@@ -1157,7 +1167,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   WSTAMP(27);
 
   // ---- Gauss-Seidel levels: counting sort into level order; the records for kernel B ------------
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_adj);  // [dmax + 1] (edges dead; dmax <= T <= tcap)
+  uint32_t* s_cnt = s_adj;  // [dmax + 1] over adj..stk (dead after the walk; dmax <= T <= tcap)
   for (int l = lane; l <= dmax; l += W) s_cnt[l] = 0u;
   __syncthreads();
   for (int k = lane; k < nord; k += W) atomicAdd(&s_cnt[xdfs[k] >> 16], 1u);
