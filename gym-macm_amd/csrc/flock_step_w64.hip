@@ -96,6 +96,11 @@ constexpr bool kLevels = true;
 #ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
 #define MACM_PRIO2_T 3
 #endif
+#ifdef MACM_NO_TDM_OBS_STAGED  // A/B knob: TDM obs stored by the pair tiles (tdm_obs.hpp)
+constexpr bool kTdmObsStaged = false;
+#else
+constexpr bool kTdmObsStaged = true;
+#endif
 #ifdef MACM_NO_CHAIN_PRIORITY  // A/B knob: no s_setprio around the serial solver chain
 constexpr bool kChainPriority = false;
 #else
@@ -1791,8 +1796,15 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     s_ang[lane] = ang;
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
-    MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
-                     s_c, s_ang);
+    OT* const obs_e = obs ? obs + rows * 4 : nullptr;
+    uint8_t* const mask_e = TB.mask_out ? TB.mask_out + rows : nullptr;
+    bool staged = false;
+    if constexpr (sizeof(OT) == 4 && kTdmObsStaged) {
+      staged = tdm_obs_stage_bytes(N) <= (int)sizeof(Pool);  // the contact arrays are dead here
+      if (staged)
+        tdm_obs_staged<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<unsigned char*>(&s_pool));
+    }
+    if (!staged) MACM_TDM_OBS<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang);
   }
   STAMP(12);
 

@@ -132,6 +132,72 @@ __device__ __forceinline__ void tdm_obs_linear(OT* __restrict__ obs, uint8_t* __
   }
 }
 
+// The pair computation of tdm_obs_pairs with the stores of tdm_obs_linear: pass 1 evaluates, for
+// every unordered pair {i, j} (i < j) whose agents are both alive, the shared part of its two slots
+// (r and atan2's reduction and polynomial, obs_atan2_core) into LDS; pass 2 writes the slots in
+// memory order, lane q slot q, each finishing its own quadrant, "- angle" and wraps from the staged
+// core. Every value is bit-identical to tdm_obs_pairs (the same expressions on the same operands);
+// a store instruction covers 64 consecutive slots, so the env's block leaves L2 as whole lines
+// (the pair tiles' 8-slot runs straddle lines: rows are 496 B at N = 32). float32 obs only; stage:
+// 12 B per pair (N <= 32 in the wave kernel's 6 KB of contact arrays, dead by then).
+__host__ __device__ constexpr int tdm_obs_stage_bytes(int N) { return 12 * (N * (N - 1) / 2); }
+
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_staged(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
+                                               unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                               const float* sa, unsigned char* stage) {
+  static_assert(sizeof(OT) == 4, "the staged writer keeps r as float32");
+  const int S = N - 1, P = N * S / 2;
+  double* s_core = reinterpret_cast<double*>(stage);
+  float* s_r = reinterpret_cast<float*>(stage + 8 * P);
+  {  // pass 1: pair p = lane + 64 m in row-major order over i < j
+    int i = 0, rem = lane;
+    while (i < N - 1 && rem >= S - i) {
+      rem -= S - i;
+      ++i;
+    }
+    for (int p = lane; p < P; p += 64) {
+      const int j = i + 1 + rem;
+      if ((livem >> i) & (livem >> j) & 1ull) {
+        const float2 ci = sc[i], cj = sc[j];
+        const float rx = cj.x - ci.x, ry = cj.y - ci.y;
+        s_r[p] = (float)obs_sqrt<OT>(rx * rx + ry * ry);
+        s_core[p] = obs_atan2_core(fabs((double)rx), fabs((double)ry));
+      }
+      rem += 64;
+      while (i < N - 1 && rem >= S - i) {
+        rem -= S - i;
+        ++i;
+      }
+    }
+  }
+  __syncthreads();
+  const int ns = N * S;
+  int i = lane / S, k = lane - i * S;  // slot q = i * S + k, advanced by 64 per pass
+  for (int q = lane; q < ns; q += 64) {
+    const int j = k < i ? k : k + 1;
+    const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
+    double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
+    if (m) {
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int pp = lo * (2 * N - lo - 1) / 2 + (hi - lo - 1);
+      const float2 ci = sc[i], cj = sc[j];
+      const float rx = cj.x - ci.x, ry = cj.y - ci.y;  // other.position - agent.position
+      r = (double)s_r[pp];
+      t = wrap_pi(obs_atan2_finish(s_core[pp], (double)ry, (double)rx) - (double)sa[i]);
+      p = wrap_pi((double)sa[j] - (double)sa[i]);
+      ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
+    }
+    if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
+    if (mask) mask[q] = m ? 1 : 0;
+    k += 64;
+    while (k >= S) {
+      k -= S;
+      ++i;
+    }
+  }
+}
+
 #ifdef MACM_TDM_OBS_LINEAR
 #define MACM_TDM_OBS tdm_obs_linear
 #else
