@@ -142,6 +142,11 @@ __device__ __forceinline__ void tdm_obs_linear(OT* __restrict__ obs, uint8_t* __
 // 12 B per pair (N <= 32 in the wave kernel's 6 KB of contact arrays, dead by then).
 __host__ __device__ constexpr int tdm_obs_stage_bytes(int N) { return 12 * (N * (N - 1) / 2); }
 
+// team of agent x without a loop: team_end[t] = N for every t >= n_teams - 1
+__device__ __forceinline__ int tdm_team_nb(const TdmParams& T, int x) {
+  return (x >= T.team_end[0]) + (x >= T.team_end[1]) + (x >= T.team_end[2]);
+}
+
 template <typename OT>
 __device__ __forceinline__ void tdm_obs_staged(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
                                                unsigned long long livem, const TdmParams& TP, const float2* sc,
@@ -150,51 +155,68 @@ __device__ __forceinline__ void tdm_obs_staged(OT* __restrict__ obs, uint8_t* __
   const int S = N - 1, P = N * S / 2;
   double* s_core = reinterpret_cast<double*>(stage);
   float* s_r = reinterpret_cast<float*>(stage + 8 * P);
-  {  // pass 1: pair p = lane + 64 m in row-major order over i < j
-    int i = 0, rem = lane;
-    while (i < N - 1 && rem >= S - i) {
-      rem -= S - i;
-      ++i;
+  // pair (i < j) -> its stage index (row-major over i < j)
+  auto pidx = [N](int i, int j) { return ((i * (2 * N - i - 1)) >> 1) + (j - i - 1); };
+  auto stage_pair = [&](int i, int j) {
+    if ((livem >> i) & (livem >> j) & 1ull) {
+      const float2 ci = sc[i], cj = sc[j];
+      const float rx = cj.x - ci.x, ry = cj.y - ci.y;
+      const int pp = pidx(i, j);
+      s_r[pp] = (float)obs_sqrt<OT>(rx * rx + ry * ry);
+      s_core[pp] = obs_atan2_core(fabs((double)rx), fabs((double)ry));
     }
-    for (int p = lane; p < P; p += 64) {
-      const int j = i + 1 + rem;
-      if ((livem >> i) & (livem >> j) & 1ull) {
-        const float2 ci = sc[i], cj = sc[j];
-        const float rx = cj.x - ci.x, ry = cj.y - ci.y;
-        s_r[p] = (float)obs_sqrt<OT>(rx * rx + ry * ry);
-        s_core[p] = obs_atan2_core(fabs((double)rx), fabs((double)ry));
+  };
+  {  // pass 1 over the pair tiles of tdm_obs_pairs (uniform loops)
+    const int nb = (N + 7) >> 3;
+    const int a = lane >> 3, b = lane & 7;
+    for (int I = 0; I < nb; ++I) {
+      const int i = 8 * I + a;
+      for (int J = I + 1; J < nb; ++J) {
+        const int j = 8 * J + b;
+        if (i < N && j < N) stage_pair(i, j);
       }
-      rem += 64;
-      while (i < N - 1 && rem >= S - i) {
-        rem -= S - i;
-        ++i;
-      }
+    }
+    const int k = lane & 31;
+    int r = 0, rem = k;
+    while (r < 7 && rem >= 7 - r) {
+      rem -= 7 - r;
+      ++r;
+    }
+    const int c = r + 1 + rem;
+    for (int D0 = 0; D0 < nb; D0 += 2) {
+      const int D = D0 + (lane >> 5);
+      const int i = 8 * D + r, j = 8 * D + c;
+      if (k < 28 && D < nb && j < N) stage_pair(i, j);
     }
   }
   __syncthreads();
   const int ns = N * S;
-  int i = lane / S, k = lane - i * S;  // slot q = i * S + k, advanced by 64 per pass
+  const float invS = 1.0f / (float)S;
   for (int q = lane; q < ns; q += 64) {
+    int i = (int)((float)q * invS);  // q / S, then one exact correction
+    int k = q - i * S;
+    if (k < 0) {
+      --i;
+      k += S;
+    } else if (k >= S) {
+      ++i;
+      k -= S;
+    }
     const int j = k < i ? k : k + 1;
     const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
     double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
     if (m) {
-      const int lo = i < j ? i : j, hi = i < j ? j : i;
-      const int pp = lo * (2 * N - lo - 1) / 2 + (hi - lo - 1);
+      const int pp = i < j ? pidx(i, j) : pidx(j, i);
       const float2 ci = sc[i], cj = sc[j];
       const float rx = cj.x - ci.x, ry = cj.y - ci.y;  // other.position - agent.position
+      const float ai = sa[i], aj = sa[j];
       r = (double)s_r[pp];
-      t = wrap_pi(obs_atan2_finish(s_core[pp], (double)ry, (double)rx) - (double)sa[i]);
-      p = wrap_pi((double)sa[j] - (double)sa[i]);
-      ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
+      t = wrap_pi(obs_atan2_finish(s_core[pp], (double)ry, (double)rx) - (double)ai);
+      p = wrap_pi((double)aj - (double)ai);
+      ty = tdm_team_nb(TP, j) == tdm_team_nb(TP, i) ? 1.0 : 0.0;
     }
     if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
     if (mask) mask[q] = m ? 1 : 0;
-    k += 64;
-    while (k >= S) {
-      k -= S;
-      ++i;
-    }
   }
 }
 
