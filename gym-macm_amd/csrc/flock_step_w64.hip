@@ -96,10 +96,13 @@ constexpr bool kLevels = true;
 #ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
 #define MACM_PRIO2_T 3
 #endif
-#ifdef MACM_NO_TDM_OBS_STAGED  // A/B knob: TDM obs stored by the pair tiles (tdm_obs.hpp)
-constexpr bool kTdmObsStaged = false;
-#else
+// TDM obs through the staged writer (tdm_obs.hpp): whole-line stores, 709 B per agent-step of HBM
+// traffic instead of 864, but C4 34.1 us per step instead of 28.2 (profiles/r03/abtests/tdm_obs/):
+// off, the pair tiles stay (A/B knob)
+#ifdef MACM_TDM_OBS_STAGED
 constexpr bool kTdmObsStaged = true;
+#else
+constexpr bool kTdmObsStaged = false;
 #endif
 #ifdef MACM_NO_CHAIN_PRIORITY  // A/B knob: no s_setprio around the serial solver chain
 constexpr bool kChainPriority = false;
