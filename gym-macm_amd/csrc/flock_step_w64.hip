@@ -1039,6 +1039,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     }
 #endif
   } else {
+#ifndef MACM_AB_NO_SPILL
     // TDM: the same hand-over, after this step's actions, casts and deaths; the spill step does the
     // physics of the living bodies and TDM's env layer (its records in HBM: the pool is smaller)
     if (touch_over || (!fast_dfs && __builtin_amdgcn_ballot_w64(deg > DEG) != 0ull) || P.force_spill) {
@@ -1066,6 +1067,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
                                         reinterpret_cast<unsigned char*>(&s_pool), &TP, &TB, make_float2(Fx, Fy));
       return;
     }
+#endif
   }
   if (!fast_dfs && deg > DEG) {
     status |= MACM_ST_DEGREE_OVERFLOW;
