@@ -15,6 +15,11 @@ __device__ __forceinline__ double wrap_pi(double t) {
 }
 
 
+// team of agent x without a loop: team_end[t] = N for every t >= n_teams - 1
+__device__ __forceinline__ int tdm_team_nb(const TdmParams& T, int x) {
+  return (x >= T.team_end[0]) + (x >= T.team_end[1]) + (x >= T.team_end[2]);
+}
+
 template <typename OT>
 __device__ __forceinline__ void store4(OT* o, double a, double b, double c, double d) {
   if constexpr (sizeof(OT) == 4) {
@@ -51,8 +56,8 @@ __device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __re
     t1 = wrap_pi(obs_atan2_finish(core, (double)ry, (double)rx) - (double)ai);
     t2 = wrap_pi(obs_atan2_finish(core, (double)qy, (double)qx) - (double)aj);
     p1 = wrap_pi((double)aj - (double)ai);
-    p2 = wrap_pi((double)ai - (double)aj);
-    ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
+    p2 = -p1;  // = wrap_pi(ai - aj) exactly: a - b == -(b - a) and the wrap is odd in IEEE arithmetic
+    ty = tdm_team_nb(TP, j) == tdm_team_nb(TP, i) ? 1.0 : 0.0;
   }
   const size_t s1 = (size_t)i * S + (j - 1), s2 = (size_t)j * S + i;
   if (obs) {
@@ -141,11 +146,6 @@ __device__ __forceinline__ void tdm_obs_linear(OT* __restrict__ obs, uint8_t* __
 // (the pair tiles' 8-slot runs straddle lines: rows are 496 B at N = 32). float32 obs only; stage:
 // 12 B per pair (N <= 32 in the wave kernel's 6 KB of contact arrays, dead by then).
 __host__ __device__ constexpr int tdm_obs_stage_bytes(int N) { return 12 * (N * (N - 1) / 2); }
-
-// team of agent x without a loop: team_end[t] = N for every t >= n_teams - 1
-__device__ __forceinline__ int tdm_team_nb(const TdmParams& T, int x) {
-  return (x >= T.team_end[0]) + (x >= T.team_end[1]) + (x >= T.team_end[2]);
-}
 
 template <typename OT>
 __device__ __forceinline__ void tdm_obs_staged(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
