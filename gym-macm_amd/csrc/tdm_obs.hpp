@@ -10,8 +10,9 @@ namespace macm {
 __device__ __forceinline__ double sgn(double x) { return (double)((x > 0.0) - (x < 0.0)); }
 
 // t = t - np.sign(t) * 2 * np.pi if np.abs(t) > np.pi else t      (mvmnt.py:199,214)
+// |t| > pi implies t != 0, so sign(t) * 2 * pi is copysign(2 pi, t) (2 pi exact in double)
 __device__ __forceinline__ double wrap_pi(double t) {
-  return fabs(t) > M_PI ? t - sgn(t) * 2.0 * M_PI : t;
+  return fabs(t) > M_PI ? t - copysign(2.0 * M_PI, t) : t;
 }
 
 
