@@ -41,7 +41,7 @@ __host__ __device__ constexpr int a16(int x) { return (x + 15) & ~15; }
 
 // LDS layout of the per-body arrays (host: size check; device: carve). 16-B aligned offsets.
 struct Layout {
-  int c, v, slp, deg, flags, oldc, off, todo, ib, ibod, stk, ic, isolv, scan, misc, recs, total;
+  int c, v, slp, deg, flags, oldc, off, todo, ib, ibod, stk, ic, isolv, scan, misc, alive, recs, total;
 };
 
 __host__ __device__ constexpr Layout layout(int N, bool recs_in_lds) {
@@ -67,6 +67,8 @@ __host__ __device__ constexpr Layout layout(int N, bool recs_in_lds) {
   L.isolv = take(N / 2 + 2);           // uint8 island position-solved
   L.scan = take(4 * 32);               // block scan scratch (<= 16 waves)
   L.misc = take(4 * 8);                // nisl, status
+  // TDM above one wave (tdm_step_wg.hip): bitmap of the living bodies (one wave: a ballot mask)
+  L.alive = take(N > W ? 4 * ((N + 31) / 32) : 0);
   L.recs = recs_in_lds ? take((int)sizeof(Rec) * N) : o;
   L.total = o;
   return L;
@@ -169,9 +171,10 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 // thread of the block must call it). `lds` holds layout(N, RECS_LDS).total bytes; the caller's
 // LDS contents are dead (a barrier on entry orders its last accesses). RECS_LDS = false keeps the
 // pair records in HBM (B.sp_rec) for callers whose LDS is smaller than 88 B per body.
-// MODE kTdm (TDM.step, combat.py:104-184): called by the TDM wave kernel (64 threads) after it has
-// taken this step's actions, melee casts and deaths and committed them (angles, cooldowns, health,
-// alive flags, listener, counters 0-2); each lane passes its force `F`. The physics skips the bodies
+// MODE kTdm (TDM.step, combat.py:104-184): called by the TDM wave kernel (64 threads, dense envs) or
+// the workgroup TDM step (tdm_step_wg.hip, every env of more than 64 agents) after it has taken this
+// step's actions, melee casts and deaths and committed them (angles, cooldowns, health, alive
+// flags, listener, counters 0-2); each thread passes its force `F`. The physics skips the bodies
 // that are not alive (their contacts were destroyed with their proxies) and the env layer is TDM's:
 // the body state, the [N, N-1, 4] observation, done / winner, counter 3.
 template <typename OT, bool RECS_LDS, int MODE = kFlock>
@@ -187,6 +190,8 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const int N = P.n_agents;
   const int C = P.max_contacts;
   const bool act = tid < N && (!kT || TB->alive[(size_t)e * N + tid] != 0);  // in the physics step
+  // TDM: the living bodies, as the one wave's ballot (N <= 64, the wave kernel's hand-over) or as an
+  // LDS bitmap (N > 64, the workgroup TDM step; filled below, read after the actions' barrier)
   const unsigned long long livem = kT ? __ballot(act) : ~0ull;
   const size_t ag = (size_t)e * N + tid;
   const int nxt = cur ^ 1;
@@ -206,7 +211,20 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   uint8_t* s_isolv = (uint8_t*)(lds + L.isolv);
   int* s_scan = (int*)(lds + L.scan);
   int* s_misc = (int*)(lds + L.misc);
+  uint32_t* s_alivew = (uint32_t*)(lds + L.alive);
   __syncthreads();  // the caller's last LDS accesses are done before the arrays are reused
+  const bool wide = kT && N > W;
+  if (wide && (tid & (W - 1)) == 0) {  // wave w's ballot holds bodies 64w .. 64w + 63
+    const int q = 2 * (tid / W);
+    if (q < (N + 31) / 32) s_alivew[q] = (uint32_t)livem;
+    if (q + 1 < (N + 31) / 32) s_alivew[q + 1] = (uint32_t)(livem >> 32);
+  }
+  // both bodies of a pair take part in the physics (Flock: always)
+  auto live2 = [&](int a, int b) -> bool {
+    if (!kT) return true;
+    if (!wide) return ((livem >> a) & (livem >> b) & 1ull) != 0ull;
+    return ((s_alivew[a >> 5] >> (a & 31)) & (s_alivew[b >> 5] >> (b & 31)) & 1u) != 0u;
+  };
   // the HBM working set of this env's slot, capacity C (touching contacts are a subset of the list)
   const int slot = acquire_slot(B, e, s_misc + 7);
   if (slot < 0) {  // the pool stayed full for ~1 s: not stepped, reported
@@ -305,7 +323,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       lam = cimp[k];
       const int a = ab & 0xffffu, b = ab >> 16;
       // TDM: the contacts of a dead body were destroyed with its proxy (combat.py:162)
-      if (!kT || ((livem >> a) & (livem >> b) & 1ull)) {
+      if (live2(a, b)) {
         const float2 pa = s_c[a], pb = s_c[b];
         const float dx = pb.x - pa.x, dy = pb.y - pa.y;
         touch = !(dx * dx + dy * dy > rr);  // b2CollideCircles
@@ -649,7 +667,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       // touching at Collide, from the start-of-step positions (the state is not yet written back)
       const float2 pa = B.pos[(size_t)e * N + a], pb = B.pos[(size_t)e * N + b];
       const float dx = pb.x - pa.x, dy = pb.y - pa.y;
-      touch = !(dx * dx + dy * dy > rr) && (!kT || ((livem >> a) & (livem >> b) & 1ull));
+      touch = !(dx * dx + dy * dy > rr) && live2(a, b);
     }
     int tpos, kpos;
     const int tn = block_scan_excl(touch ? 1 : 0, tpos, s_scan);
@@ -684,12 +702,16 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     }
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
-    MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, livem, *TP,
-                     s_c, s_slp);
+    if (wide)
+      tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, s_alivew,
+                        *TP, s_c, s_slp);
+    else
+      MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, livem,
+                       *TP, s_c, s_slp);
     int alive_teams = 0, last_team = -1;
     const int myteam = tdm_team_of(*TP, tid);
     for (int t = 0; t < TP->n_teams; ++t)
-      if (__ballot(act && myteam == t)) {
+      if (__syncthreads_or(act && myteam == t)) {
         ++alive_teams;
         last_team = t;
       }

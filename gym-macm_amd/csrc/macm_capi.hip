@@ -43,6 +43,15 @@ hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const
                                hipStream_t s);
 hipError_t launch_draw_poses(const uint8_t* mask, uint32_t* mt, const PoseDraw& D, int n_envs, float2* pos,
                              float* angle, hipStream_t s);
+hipError_t launch_tdm_step_wg(const StepParams& P, const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB,
+                              int cur, const void* actions, void* obs, bool obs_f64, uint8_t* done, hipStream_t s);
+hipError_t launch_tdm_init_wg(const StepParams& P, const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB,
+                              int cur, void* obs, bool obs_f64, const uint8_t* mask, hipStream_t s);
+hipError_t launch_tdm_observe_wg(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                                 const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s);
+hipError_t tdm_wg_configure(int N);
+int tdm_wg_step_lds(int N);
+int tdm_wg_obs_lds(int N);
 hipError_t launch_tdm_observe_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s);
 hipError_t launch_bots_flock(const void* obs, bool obs_f64, int od, long long rows, uint8_t* act, hipStream_t s);
@@ -87,6 +96,7 @@ struct macm_tdm {
   TdmBuffers TB;  // state pointers; output pointers are filled per call
   int cur;
   int device;
+  bool wave;  // N <= 64: the wave kernel (env_step_w64<kTdm>); else the workgroup step (tdm_step_wg.hip)
   std::vector<int> team;  // agent -> team
   std::vector<void*> allocs;
   uint32_t* mt = nullptr;
@@ -1006,7 +1016,9 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   }
   if (N != c.n_agents) return fail(MACM_E_INVALID, "n_agents != sum(team_size)");
   if (N < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2");
-  if (N > 64) return fail(MACM_E_UNSUPPORTED, "TDM with more than 64 agents per env is not built");
+  // N > 64: the workgroup step (tdm_step_wg.hip), one thread per agent and 16-bit body ids in the
+  // contact list, as the Flock workgroup path
+  if (N > 1024) return fail(MACM_E_UNSUPPORTED, "TDM with more than 1024 agents per env is not built");
   if (!(c.hz > 0.0)) return fail(MACM_E_INVALID, "hz must be > 0");
   if (c.velocity_iterations < 0 || c.position_iterations < 0) return fail(MACM_E_INVALID, "iterations < 0");
   if (!(c.radius > 0.0f)) return fail(MACM_E_INVALID, "radius must be > 0");
@@ -1016,11 +1028,21 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   DeviceGuard g(device);
   size_t free_bytes = 0, total_bytes = 0;
   HIP_TRY(hipMemGetInfo(&free_bytes, &total_bytes));
+  if (N > 64) {
+    int max_lds = 0;
+    HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+    const int need = std::max(tdm_wg_step_lds(N), tdm_wg_obs_lds(N));
+    if (need > max_lds)
+      return fail(MACM_E_UNSUPPORTED, "TDM workgroup step needs " + std::to_string(need) + " B of LDS, device has " +
+                                          std::to_string(max_lds));
+    HIP_TRY(tdm_wg_configure(N));
+  }
 
   macm_tdm* w = new macm_tdm();
   w->cfg = c;
   w->device = device;
   w->cur = 0;
+  w->wave = N <= 64;
   const int C = N * (N - 1) / 2;  // every pair: the list never overflows
   const int64_t SL = default_capacity(N, n_envs, C, free_bytes).slots;  // spill working-set slots
   StepParams& P = w->P;
@@ -1124,13 +1146,24 @@ static TdmBuffers tdm_with_outputs(const macm_tdm* w, const macm_tdm_outputs* ou
   return TB;
 }
 
+static hipError_t tdm_launch_init(const macm_tdm* w, const TdmBuffers& TB, void* obs, const uint8_t* mask,
+                                  hipStream_t s) {
+  if (w->wave) return launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, obs, w->cfg.obs_f64 != 0, mask, s);
+  return launch_tdm_init_wg(w->P, w->B, w->TP, TB, w->cur, obs, w->cfg.obs_f64 != 0, mask, s);
+}
+
+static hipError_t tdm_launch_step(const macm_tdm* w, const TdmBuffers& TB, int cur, const void* actions, void* obs,
+                                  uint8_t* done, hipStream_t s) {
+  if (w->wave) return launch_tdm_step_w64(w->P, w->B, w->TP, TB, cur, actions, obs, w->cfg.obs_f64 != 0, done, s);
+  return launch_tdm_step_wg(w->P, w->B, w->TP, TB, cur, actions, obs, w->cfg.obs_f64 != 0, done, s);
+}
+
 static int tdm_init(macm_tdm* w, const macm_tdm_outputs* out, hipStream_t s) {
   HIP_TRY(hipStreamSynchronize(s));  // earlier steps' status stores land before the word is cleared
   clear_host_status(w->hstat);
   w->cur = 0;
   const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
-                              nullptr, s));
+  HIP_TRY(tdm_launch_init(w, TB, out ? out->obs : nullptr, nullptr, s));
   if (out && out->done) HIP_TRY(hipMemsetAsync(out->done, 0, (size_t)w->P.n_envs, s));
   return MACM_OK;
 }
@@ -1196,8 +1229,7 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
   D.TP = w->TP;
   HIP_TRY(launch_draw_poses(w->rmask, w->mt, D, w->P.n_envs, w->B.pos, w->B.angle, s));
   const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(launch_tdm_init_w64(w->P, w->B, w->TP, TB, w->cur, out ? out->obs : nullptr, w->cfg.obs_f64 != 0,
-                              w->rmask, s));
+  HIP_TRY(tdm_launch_init(w, TB, out ? out->obs : nullptr, w->rmask, s));
   return resync_host_status(w->hstat, w->B.status, w->P.n_envs, s);
 }
 
@@ -1210,8 +1242,8 @@ int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out,
     if (rc) return rc;
   }
   const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(launch_tdm_step_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
-                              w->cfg.obs_f64 != 0, out ? out->done : nullptr, (hipStream_t)stream));
+  HIP_TRY(tdm_launch_step(w, TB, w->cur, actions, out ? out->obs : nullptr, out ? out->done : nullptr,
+                          (hipStream_t)stream));
   w->cur ^= 1;
   return MACM_OK;
 }
@@ -1238,6 +1270,32 @@ static int tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm
   }
   const TdmBuffers TB = tdm_with_outputs(w, out);
   const unsigned long long astride = bots ? 0ull : (unsigned long long)w->P.n_envs * w->P.n_agents * 4;
+  if (!w->wave) {
+    // workgroup step (N > 64): one launch per step (and the bots kernel's), in order; trajectory
+    // form: step k's outputs in row k of [K, ...], the closed loop reading action row k and the bot
+    // writing row k + 1 of [K + 1, E, N, 4]
+    const size_t E = w->P.n_envs, N = w->P.n_agents, EN = E * N;
+    const size_t obytes = EN * (N - 1) * 4 * (w->cfg.obs_f64 ? sizeof(double) : sizeof(float));
+    const unsigned long long kstride = bots ? (traj ? EN * 4 : 0ull) : astride;
+    const unsigned char* act = static_cast<const unsigned char*>(actions);
+    for (int k = 0; k < n_steps; ++k) {
+      const size_t kr = traj ? (size_t)k : 0;
+      TdmBuffers TBk = TB;
+      auto row = [kr](auto* p, size_t per) { return p ? p + kr * per : p; };
+      TBk.mask_out = row(TB.mask_out, EN * (N - 1));
+      TBk.health_out = row(TB.health_out, EN);
+      TBk.alive_out = row(TB.alive_out, EN);
+      TBk.winner_out = row(TB.winner_out, E);
+      void* obs_k = out && out->obs ? static_cast<unsigned char*>(out->obs) + kr * obytes : nullptr;
+      const unsigned char* act_k = act + k * kstride;
+      HIP_TRY(tdm_launch_step(w, TBk, w->cur, act_k, obs_k, out ? row(out->done, E) : nullptr, s));
+      w->cur ^= 1;
+      if (bots)
+        HIP_TRY(launch_bots_combat(obs_k, TBk.mask_out, w->cfg.obs_f64 != 0, (int)N, (long long)EN,
+                                   const_cast<unsigned char*>(act_k) + (traj ? EN * 4 : 0), s));
+    }
+    return MACM_OK;
+  }
   HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
                                  w->cfg.obs_f64 != 0, out ? out->done : nullptr, s, n_steps, astride, traj ? 1 : 0));
   if (n_steps & 1) w->cur ^= 1;
@@ -1266,7 +1324,10 @@ int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream) {
   if (!w || !out) return fail(MACM_E_INVALID, "tdm/out is NULL");
   DeviceGuard g(w->device);
   const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(launch_tdm_observe_w64(w->P, w->B, w->TP, TB, out->obs, w->cfg.obs_f64 != 0, (hipStream_t)stream));
+  if (w->wave)
+    HIP_TRY(launch_tdm_observe_w64(w->P, w->B, w->TP, TB, out->obs, w->cfg.obs_f64 != 0, (hipStream_t)stream));
+  else
+    HIP_TRY(launch_tdm_observe_wg(w->P, w->B, w->TP, TB, out->obs, w->cfg.obs_f64 != 0, (hipStream_t)stream));
   hipStream_t s = (hipStream_t)stream;
   const size_t EN = (size_t)w->P.n_envs * w->P.n_agents, E = (size_t)w->P.n_envs;
   if (out->health) HIP_TRY(hipMemcpyAsync(out->health, w->TB.health, EN * sizeof(double), hipMemcpyDefault, s));

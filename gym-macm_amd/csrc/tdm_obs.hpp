@@ -1,5 +1,6 @@
 // tdm_obs.hpp — TDM.get_obs (gym_macm/envs/combat.py:206-227) as fixed [N, N-1, 4] slots, written
-// by one 64-lane wave: shared by the wave kernel (flock_step_w64.hip) and the spill step
+// by one 64-lane wave (tdm_obs_block: by a workgroup, any N): shared by the wave kernel
+// (flock_step_w64.hip), the workgroup TDM step (tdm_step_wg.hip) and the spill step
 // (flock_spill.hpp), which steps TDM envs beyond the wave kernel's contact capacities.
 #pragma once
 
@@ -40,11 +41,10 @@ __device__ __forceinline__ void store4(OT* o, double a, double b, double c, doub
 // reduction and polynomial (obs_atan2_core of |rel.x|, |rel.y|); each keeps its own
 // rel = other - agent (float32), quadrant, "- angle" and wrap, so every value is bit-identical
 // to evaluating the two slots separately, with half the f64 atan2 work.
+// m: both agents alive.
 template <typename OT>
-__device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __restrict__ mask, int S, int i, int j,
-                                             unsigned long long livem, const TdmParams& TP, const float2* sc,
-                                             const float* sa) {
-  const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
+__device__ __forceinline__ void tdm_obs_pair_m(OT* __restrict__ obs, uint8_t* __restrict__ mask, int S, int i, int j,
+                                               bool m, const TdmParams& TP, const float2* sc, const float* sa) {
   double r = 0.0, t1 = 0.0, t2 = 0.0, p1 = 0.0, p2 = 0.0, ty = 0.0;
   if (m) {
     const float2 ci = sc[i], cj = sc[j];
@@ -68,6 +68,31 @@ __device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __re
   if (mask) {
     mask[s1] = m ? 1 : 0;
     mask[s2] = m ? 1 : 0;
+  }
+}
+
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_pair(OT* __restrict__ obs, uint8_t* __restrict__ mask, int S, int i, int j,
+                                             unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                             const float* sa) {
+  tdm_obs_pair_m<OT>(obs, mask, S, i, j, ((livem >> i) & (livem >> j) & 1ull) != 0ull, TP, sc, sa);
+}
+
+// Any N, by a whole workgroup (the workgroup TDM step, N > 64; alive agents as an LDS bitmap): the
+// N(N-1)/2 unordered pairs as a round robin. Thread i takes {i, (i + d) mod N} for d = 1 ..
+// (N-1)/2, and for even N also d = N/2 when i < N/2: every pair exactly once, (N-1)/2 or N/2 pairs
+// per thread. Each pair is evaluated as tdm_obs_pair (both directions, one shared atan2 core).
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_block(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int tid,
+                                              const uint32_t* alivew, const TdmParams& TP, const float2* sc,
+                                              const float* sa) {
+  if (tid >= N) return;
+  const int D = (N - 1) / 2 + ((N % 2) == 0 && tid < N / 2 ? 1 : 0);
+  const bool li = ((alivew[tid >> 5] >> (tid & 31)) & 1u) != 0u;
+  for (int d = 1; d <= D; ++d) {
+    const int k = tid + d < N ? tid + d : tid + d - N;
+    const bool m = li && ((alivew[k >> 5] >> (k & 31)) & 1u) != 0u;
+    tdm_obs_pair_m<OT>(obs, mask, N - 1, tid < k ? tid : k, tid < k ? k : tid, m, TP, sc, sa);
   }
 }
 

@@ -128,7 +128,7 @@ typedef struct macm_config {
 typedef struct macm_tdm_config {
   int32_t n_teams;              /* len(n_agents)                      combat.py:70-73 */
   int32_t team_size[4];         /* n_agents[i]                                        */
-  int32_t n_agents;             /* sum(n_agents) (<= 64)                              */
+  int32_t n_agents;             /* sum(n_agents) (<= 1024; > 64: the workgroup step)   */
   int32_t velocity_iterations;  /* 8                                                  */
   int32_t position_iterations;  /* 3                                                  */
   int32_t warm_starting;        /* 1                                                  */
@@ -409,8 +409,12 @@ typedef struct macm_tdm macm_tdm;
 int macm_tdm_config_default(macm_tdm_config* cfg);
 
 /*
- * Create E TDM envs (N = sum(team_size) <= 64 agents). Replaces TDM.__init__'s
- * world + body creation (combat.py:61-102). State is undefined until reset/place.
+ * Create E TDM envs (N = sum(team_size) <= 1024 agents; MACM_E_UNSUPPORTED above). Replaces
+ * TDM.__init__'s world + body creation (combat.py:61-102). State is undefined until reset/place.
+ * N <= 64: one wave per env (the fast kernel, its spill step for crowded envs); N > 64: one
+ * workgroup per env (tdm_step_wg.hip: the action loop, then the spill step's physics with its HBM
+ * working set for every env; macm_tdm_spilled counts every such env-step). Rollouts on the
+ * workgroup path are one launch per step (and the bots kernel's), with the same results.
  */
 int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, macm_tdm** out);
 int macm_tdm_destroy(macm_tdm* w);

@@ -137,7 +137,9 @@ int to_n_agents(const to_batch* b) { return b->N; }
 static void env_obs(const to_batch* b, const to_env* en, double* obs, uint8_t* mask) {
   const int N = b->N;
   float s[7];
-  float X[64], Y[64], A[64];
+  float* X = (float*)malloc(sizeof(float) * 3 * (size_t)N); /* any team sizes (combat.py:82-83) */
+  float* Y = X + N;
+  float* A = Y + N;
   for (int i = 0; i < N; ++i) {
     b2l_body_get(en->w, i, s);
     X[i] = s[0]; Y[i] = s[1]; A[i] = s[2];
@@ -156,6 +158,7 @@ static void env_obs(const to_batch* b, const to_env* en, double* obs, uint8_t* m
       o[2] = wrap((double)A[j] - (double)A[i]);
       o[3] = (double)(b->team[i] == b->team[j]);
     }
+  free(X);
 }
 
 void to_observe(to_batch* b, double* obs, uint8_t* mask) {

@@ -61,12 +61,12 @@ def test_tdm_defaults_match_python_mirror():
     c = _abi.MacmTdmConfig()
     assert L.macm_tdm_config_default(ctypes.byref(c)) == 0
     assert bytes(c) == bytes(_abi.tdm_config_from_defaults())
-    c.team_size[0] = 40
-    c.team_size[1] = 40
-    c.n_agents = 80
+    c.team_size[0] = 513  # above the workgroup step's 1024 agents: refused before any HIP call
+    c.team_size[1] = 512
+    c.n_agents = 1025
     h = ctypes.c_void_p()
     assert L.macm_tdm_create(ctypes.byref(c), 4, 0, ctypes.byref(h)) == -4
-    c.n_agents = 79
+    c.n_agents = 1024
     assert L.macm_tdm_create(ctypes.byref(c), 4, 0, ctypes.byref(h)) == -1
 
 
