@@ -303,7 +303,9 @@ def main():
         achieved_gbs = b_alg * E * N / (kernel_ms * 1e-3) / 1e9
         ncap = 32 if N <= 32 else 64
         if args.env == "tdm":
-            kname = f"env_{'rollout' if rollout else 'step'}_w64<1, {ncap}, float, false>"
+            # N > 64: the workgroup TDM step (tdm_step_wg.hip), one launch per step in either form
+            kname = (f"env_{'rollout' if rollout else 'step'}_w64<1, {ncap}, float, false>" if N <= 64
+                     else "tdm_step_wg<float>")
             scal = "false"
         else:
             # N > 64: the workgroup path's three launches per step (split step; kernel_ms covers all)

@@ -5,7 +5,7 @@ set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; shift
 mkdir -p ab/build_$NAME
-SRC="flock_step_w64 flock_rollout_w64 flock_step_wg bots env_reset actions_check macm_capi"
+SRC="flock_step_w64 flock_rollout_w64 flock_step_wg tdm_step_wg bots env_reset actions_check macm_capi"
 for f in $SRC; do
   X=""; [ $f = flock_rollout_w64 ] && X="-mllvm -disable-machine-licm"  # as the Makefile
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-result $X "$@" \
