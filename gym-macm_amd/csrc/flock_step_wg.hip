@@ -55,6 +55,12 @@ constexpr bool kDfsKernel = false;
 #else
 constexpr bool kDfsKernel = true;
 #endif
+// Issue priority 3 for the island-first walks (sparse worlds, kIslandDfs). -DMACM_NO_ISL_PRIORITY: off.
+#ifdef MACM_NO_ISL_PRIORITY
+constexpr bool kIslPriority = false;
+#else
+constexpr bool kIslPriority = true;
+#endif
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
@@ -747,6 +753,9 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     const int slot = wid < nbw ? wid : nbw + tid - nbw * W;
     const uint2 job = slot < nisl ? s_work[slot] : make_uint2(0u, 0u);
     __syncthreads();
+    // the walks are latency chains while other blocks' waves share the SIMDs: issue priority, as
+    // for the serial walk below
+    if (kIslPriority) __builtin_amdgcn_s_setprio(3);
     if (wid < nbw) {
       const int sd = (int)job.x;
       int nord = (int)(job.y & 0xffffu), nb = (int)(job.y >> 16), dmax = 0;
@@ -805,6 +814,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       }
       atomicMax(&s_misc[1], dmax);
     }
+    if (kIslPriority) __builtin_amdgcn_s_setprio(0);
   }
   // The DFS is one latency chain on one wave while the block's other waves wait at the barrier
   // and other blocks' waves share the SIMD: raise its issue priority for the walk (as the wave
