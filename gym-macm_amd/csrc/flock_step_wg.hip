@@ -61,6 +61,12 @@ constexpr bool kIslPriority = false;
 #else
 constexpr bool kIslPriority = true;
 #endif
+// Kernel B: issue priority by the env's Gauss-Seidel depth. -DMACM_NO_SOLVE_PRIORITY: off.
+#ifdef MACM_NO_SOLVE_PRIORITY
+constexpr bool kSolvePriority = false;
+#else
+constexpr bool kSolvePriority = true;
+#endif
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
@@ -1320,6 +1326,14 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   const int nisl = B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
   const int nc = nisl > 0 ? (int)B.x_ic[(size_t)e * IS + nisl] : 0;
+  if (kSolvePriority) {
+    // The kernel ends with its deepest envs (C3 closed loop: 72 levels per pass on average, up to
+    // ~200): the waves with the longest level chains take the SIMD's issue first
+    const int nlvl = B.x_nlvl[e];
+    if (nlvl >= 128) __builtin_amdgcn_s_setprio(3);
+    else if (nlvl >= 64) __builtin_amdgcn_s_setprio(2);
+    else if (nlvl >= 32) __builtin_amdgcn_s_setprio(1);
+  }
   const int nch = (nc + W - 1) / W;
   const float4* cst = B.x_cst + (size_t)e * tcap;
   float2* cimp = B.x_cimp + (size_t)e * tcap;
