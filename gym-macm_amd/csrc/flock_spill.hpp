@@ -31,6 +31,14 @@ namespace spill {
 
 constexpr int W = 64;
 
+// TDM above one wave: the observation in memory order (whole-line stores, an atan2 per slot) or by
+// pairs (tdm_obs_block: one atan2 core per pair, scattered 16-B stores). -DMACM_TDM_BLOCK_OBS_PAIRS
+#ifdef MACM_TDM_BLOCK_OBS_PAIRS
+constexpr bool kTdmBlockObsLinear = false;
+#else
+constexpr bool kTdmBlockObsLinear = true;
+#endif
+
 struct __align__(16) Rec {  // per-agent pair-sweep record (48 B)
   float4 fn;               // fat AABB after SynchronizeFixtures
   float4 fo;               // fat AABB at the start of the step
@@ -702,7 +710,10 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     }
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
-    if (wide)
+    if (wide && kTdmBlockObsLinear)
+      tdm_obs_block_linear<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid,
+                               BS, s_alivew, *TP, s_c, s_slp);
+    else if (wide)
       tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, s_alivew,
                         *TP, s_c, s_slp);
     else

@@ -96,6 +96,40 @@ __device__ __forceinline__ void tdm_obs_block(OT* __restrict__ obs, uint8_t* __r
   }
 }
 
+// Any N, by a whole workgroup, in memory order: thread t of the block writes slots t, t + BS, ... of
+// the env's [N, N-1] block, so each store instruction covers 64 consecutive 16-B slots (whole 128-B
+// lines) and the mask 64 consecutive bytes; each slot evaluates its own atan2 (tdm_obs_linear's
+// arithmetic, bit-identical to the pair form).
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_block_linear(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int tid,
+                                                     int BS, const uint32_t* alivew, const TdmParams& TP,
+                                                     const float2* sc, const float* sa) {
+  const int S = N - 1, ns = N * S;
+  int i = tid / S, k = tid - i * S;  // slot q = i * S + k, advanced by BS per pass
+  const int di = BS / S, dk = BS - di * S;
+  for (int q = tid; q < ns; q += BS) {
+    const int j = k < i ? k : k + 1;
+    const bool m = ((alivew[i >> 5] >> (i & 31)) & (alivew[j >> 5] >> (j & 31)) & 1u) != 0u;
+    double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
+    if (m) {
+      const float2 ci = sc[i], cj = sc[j];
+      const float rx = cj.x - ci.x, ry = cj.y - ci.y;  // other.position - agent.position
+      r = obs_sqrt<OT>(rx * rx + ry * ry);
+      t = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)sa[i]);
+      p = wrap_pi((double)sa[j] - (double)sa[i]);
+      ty = tdm_team_nb(TP, j) == tdm_team_nb(TP, i) ? 1.0 : 0.0;
+    }
+    if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
+    if (mask) mask[q] = m ? 1 : 0;
+    i += di;
+    k += dk;
+    if (k >= S) {
+      k -= S;
+      ++i;
+    }
+  }
+}
+
 // The pairs in 8 x 8 tiles (agent blocks I < J), one tile per pass: lane (a, b) = (lane / 8,
 // lane % 8) takes pair (8I + a, 8J + b). A store instruction then writes 8 runs of 8
 // consecutive slots for both directions (rows 8I + a, and rows 8J + b), so whole L2 lines fill

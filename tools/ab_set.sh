@@ -15,6 +15,8 @@ args() {
     c2) echo "--envs 1024 --steps 1000 --warmup 100" ;;
     c3) echo "--agents 256 --flocks 4 --steps 20 --warmup 5" ;;
     c3bots) echo "--agents 256 --flocks 4 --policy bots --steps 50 --warmup 250" ;;
+    t128) echo "--env tdm --teams 64,64 --envs 1024 --steps 20 --warmup 5" ;;
+    t512) echo "--env tdm --teams 256,256 --envs 256 --steps 5 --warmup 2" ;;
     c3ss) echo "--agents 256 --flocks 4 --steps 100 --warmup 50" ;;
     c4) echo "--env tdm --steps 20 --warmup 5" ;;
     c4bots) echo "--env tdm --policy bots --steps 100 --warmup 100" ;;
