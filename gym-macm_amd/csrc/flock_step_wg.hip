@@ -17,6 +17,9 @@
 // The step is split in three launches (kernels A, B, C below). An env whose touching
 // contacts exceed kernel A's LDS capacity is stepped whole by the spill step
 // (flock_spill.hpp) inside kernel A, and B and C skip it.
+#include <map>
+#include <mutex>
+
 #include "flock_common.hpp"
 #include "flock_spill.hpp"
 #include "flock_grid.hpp"
@@ -1908,8 +1911,18 @@ int wg_lds_bytes(int N, int tcap) {
   return m;
 }
 
-// Raise the dynamic-LDS limit of the workgroup kernels once (world creation).
+// Raise the dynamic-LDS limit of the workgroup kernels (world creation). The limit is a property of
+// the kernel, not of a world: it only ever grows (per device), so creating a world of fewer agents
+// after a larger one cannot make the larger world's launches fail.
 hipError_t wg_configure(int N, int tcap) {
+  static std::mutex mu;
+  static std::map<int, int> high;  // device -> the largest N configured
+  std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  int& hw = high[dev];
+  if (N <= hw) return hipSuccess;
+  hw = N;
   hipError_t e = hipSuccess;
   const void* fi[] = {(const void*)flock_init_wg<float>, (const void*)flock_init_wg<double>};
   for (const void* f : fi)

@@ -12,11 +12,14 @@
 //   2. deaths (combat.py:157-165); the combat state is committed to HBM;
 //   3. the physics, TDM.get_obs, done / winner by the spill step (flock_spill.hpp, MODE kTdm): the
 //      touching-contact working set in HBM, the per-body arrays and pair records in LDS (88 B per
-//      body: 88 KB at N = 1024), the observation by tdm_obs_block (a round robin over the pairs).
+//      body: 88 KB at N = 1024), the observation in memory order (tdm_obs_block_linear).
 // The spill step's arithmetic and order are those of the fast kernels, so results are bit-exact
 // against the oracle (tests/test_gpu_tdm_wg.py). HBM per agent-step is dominated by the [N, N-1, 4]
 // observation (16 (N-1) B at float32), as in the wave kernel.
 #include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
 
 #include "flock_common.hpp"
 #include "tdm_obs.hpp"
@@ -329,7 +332,16 @@ __global__ __launch_bounds__(1024) void tdm_observe_wg(StepParams P, WorldBuffer
 // ---- host-side launchers (C++ linkage, used by macm_capi.hip) -------------------------------------
 static int tdm_wg_block(int N) { return ((N + 63) / 64) * 64; }
 
+// as wg_configure: the kernels' dynamic-LDS limits only grow (per device)
 hipError_t tdm_wg_configure(int N) {
+  static std::mutex mu;
+  static std::map<int, int> high;
+  std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  int& hw = high[dev];
+  if (N <= hw) return hipSuccess;
+  hw = N;
   const int ls = tdm_wg_step_lds(N), lo = tdm_wg_obs_lds(N);
   const void* fs[] = {(const void*)tdm_step_wg<float>, (const void*)tdm_step_wg<double>};
   const void* fo[] = {(const void*)tdm_init_wg<float>, (const void*)tdm_init_wg<double>,

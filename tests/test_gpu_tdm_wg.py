@@ -166,3 +166,25 @@ def test_tdm_wg_dict_api():
         obs = env.step(acts)
         for aid, o in obs.items():
             assert len(o["agents"]) == len(obs) - 1
+
+
+def test_lds_limits_only_grow():
+    """The workgroup kernels' dynamic-LDS limits are per kernel, not per world: creating a smaller
+    world after a larger one must not make the larger world's launches (88 KB at 1024 agents,
+    above the default 64 KB) fail. TDM and Flock."""
+    from gym_macm.vec import FlockVec
+    big = TdmWorld(tdm_config([512, 512]), 1, device="cuda:0")
+    big.reset(1)
+    small = TdmWorld(tdm_config([40, 40]), 1, device="cuda:0")
+    small.reset(2)
+    rng = np.random.default_rng(0)
+    big.step(torch.from_numpy(random_actions(rng, 1, 1024)).cuda())
+    small.step(torch.from_numpy(random_actions(rng, 1, 80)).cuda())
+    torch.cuda.synchronize()
+    assert big.status() == 0 and small.status() == 0
+    fbig = FlockVec(2, n_agents=[1024], seed=3, device="cuda:0")
+    fsmall = FlockVec(2, n_agents=[100], seed=4, device="cuda:0")
+    fbig.step(torch.ones((2, 1024, 3), dtype=torch.uint8, device="cuda:0"))
+    fsmall.step(torch.ones((2, 100, 3), dtype=torch.uint8, device="cuda:0"))
+    torch.cuda.synchronize()
+    assert fbig.status() == 0 and fsmall.status() == 0
