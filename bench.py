@@ -167,11 +167,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.dist_backend == "nccl":
+    # a launcher (torchrun) sets MASTER_ADDR: the process group exists then even for one rank, so
+    # `torchrun --nproc-per-node 1` runs the RCCL branch (init, barriers, device all-reduces) on a
+    # one-GPU box; a plain `python bench.py` (the driver's N=1 run) has no process group
+    launched = world > 1 or "MASTER_ADDR" in os.environ
+    if launched and args.dist_backend == "nccl":
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    elif world > 1:
+    elif launched:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group("gloo")
     else:
@@ -258,7 +262,7 @@ def main():
         torch.cuda.synchronize(dev)
         if args.env == "flock":
             world_h.reset_counters()
-        if world > 1:
+        if launched:
             dist.barrier()
         torch.cuda.synchronize(dev)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -276,7 +280,7 @@ def main():
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
-        if world > 1:
+        if launched:
             dist.barrier()
         return t1 - t0, ev0.elapsed_time(ev1)
 
@@ -357,7 +361,8 @@ def main():
                 "split": (f"strong: {args.total_envs} envs over {world} ranks (this rank: global envs "
                           f"{e_off}..{e_off + E - 1})") if strong else f"weak: {E} envs per GPU",
                 "parallelism": f"env-sharded x{world} (no data-path collective)"
-                               + ("" if world == 1 or args.dist_backend == "nccl" else ", gloo counters (test mode)"),
+                               + ("" if not launched else ", RCCL counters" if args.dist_backend == "nccl"
+                                  else ", gloo counters (test mode)"),
                 "obs": "float64" if args.obs_f64 else "float32",
                 # per-env contact-list capacity and spill working-set slots (macm_world_create's
                 # defaults from 1/8 of the device's free memory)
@@ -414,7 +419,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if launched:
         dist.destroy_process_group()
 
 

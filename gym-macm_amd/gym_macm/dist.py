@@ -47,7 +47,7 @@ def reduce_counters(counters, device=None, op="sum"):
     t = torch.as_tensor(np.asarray(counters, np.int64), dtype=torch.int64)
     if device is not None:
         t = t.to(device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():  # one rank too: the collective still runs
         dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
     return t.cpu().numpy()
 
@@ -55,7 +55,7 @@ def reduce_counters(counters, device=None, op="sum"):
 def reduce_max(value: float, device=None) -> float:
     """Max over ranks (the job's wall time is its slowest rank's)."""
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -1,8 +1,9 @@
 """bench.py's multi-process path on the GPU box: two ranks under torchrun (one process each,
 both on the box's one GPU, gloo for the counter all-reduce since RCCL needs one GPU per rank).
 Each rank steps its own shard of global env ids; the reduced counters must cover both shards
-and the line must report the whole job. The RCCL flavour of the same code runs in the driver's
-8-GPU scaling bench (`--dist-backend nccl`, the default)."""
+and the line must report the whole job. The RCCL flavour (`--dist-backend nccl`, the default) needs one GPU
+per rank, so on this box it runs as one rank under torchrun (test_rccl_single_rank_under_torchrun);
+its multi-rank form runs in the driver's 8-GPU scaling bench."""
 import json
 import os
 import socket
@@ -85,3 +86,22 @@ def test_strong_split_two_ranks_equal_single_process(tmp_path, extra):
             np.testing.assert_array_equal(pad(part[k]), pad(ref[k][o:o + n]), err_msg=f"rank {r} {k}")
         seen += n
     assert seen == T
+
+
+@pytest.mark.parametrize("extra", [[], ["--agents", "100"]])
+def test_rccl_single_rank_under_torchrun(extra):
+    """The RCCL branch of bench.py (`--dist-backend nccl`, the default) on the one-GPU box: torchrun
+    with one rank creates the nccl (= RCCL) process group, and the barriers around the timed window
+    and the device-tensor all-reduces of the counters and the elapsed time run through RCCL. The
+    reduced counters equal the plain single-process run's (same envs, same actions)."""
+    K, W, E = 4, 2, 96
+    base = [os.path.join(REPO, "bench.py"), "--steps", str(K), "--warmup", str(W), "--envs", str(E),
+            "--no-cpu-baseline"] + extra
+    one = _run([sys.executable] + base)
+    rccl = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + base +
+                ["--gpus", "1", "--dist-backend", "nccl"])
+    assert "RCCL counters" in rccl["config"]["parallelism"]
+    assert "RCCL" not in one["config"]["parallelism"]
+    assert rccl["counters"] == one["counters"]
+    assert rccl["n_gpus"] == 1 and rccl["value"] > 0
