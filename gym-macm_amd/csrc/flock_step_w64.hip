@@ -93,6 +93,12 @@ constexpr bool kLevels = false;
 #else
 constexpr bool kLevels = true;
 #endif
+#ifndef MACM_BRANCHFREE_WAVE_LEVELS  // A/B knob: 0 = an exec-masked branch per level step (T <= 64 levels)
+#define MACM_BRANCHFREE_WAVE_LEVELS 1
+#endif
+#ifndef MACM_BRANCHFREE_WAVE_POS  // A/B knob: 1 = branch-free position level steps too (T <= 64 levels)
+#define MACM_BRANCHFREE_WAVE_POS 0
+#endif
 #ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
 #define MACM_PRIO2_T 3
 #endif
@@ -726,6 +732,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   __shared__ uint8_t s_adj_tdm[kT ? W * DEG : 1];
   uint8_t* const s_adj = kT ? s_adj_tdm : reinterpret_cast<uint8_t*>(s_pool.tm);
   static_assert(kT || sizeof(uint32_t) * 2 * 2 * W >= W * DEG, "s_adj must fit in s_tm");
+  static_assert(sizeof(uint32_t) * 2 * TMW * W >= sizeof(float2) * W, "the level steps' dummy slots must fit in s_tm");
   __shared__ uint8_t s_ord[TCAP];
   __shared__ uint32_t s_cvis[TCAP / 32];
   __shared__ uint8_t s_deg[W], s_stack[W], s_ibodies[W], s_bisl[W];
@@ -1348,6 +1355,32 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       }
     } else if (lvl_path) {
       // the warm-start pass and the velocity passes as separate loops: no branch inside a level step
+#if MACM_BRANCHFREE_WAVE_LEVELS
+      // every lane runs every level step, the lanes outside the level on their own dummy slot in
+      // s_tm (the DFS masks: dead until the next step's Collide), so a level step has no exec-mask
+      // branch; only the level's lanes keep their impulses
+      float2* const pda = lhas ? s_v + la : reinterpret_cast<float2*>(s_tm) + lane;
+      float2* const pdb = lhas ? s_v + lb : reinterpret_cast<float2*>(s_tm) + lane;
+      float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
+      const int mylvl = lhas ? lvl : -1;
+      auto lpass = [&](auto warm) {
+        for (int l = 0; l < dmulti; ++l) {
+          const bool on = mylvl == l;
+          float2* const pa = on ? pda : pdd;
+          float2* const pb = on ? pdb : pdd;
+          const float2 vA0 = *pa, vB0 = *pb;
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+          float nl = lln, nt = llt;
+          if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB);
+          else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB, kmass, friction);
+          *pa = make_float2(vAx, vAy);
+          *pb = make_float2(vBx, vBy);
+          lln = on ? nl : lln;
+          llt = on ? nt : llt;
+          level_sync();
+        }
+      };
+#else
       auto lpass = [&](auto warm) {
         for (int l = 0; l < dmulti; ++l) {
           if (lhas && lvl == l) {
@@ -1361,6 +1394,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           level_sync();
         }
       };
+#endif
       if (P.warm_starting) lpass(BoolC<true>{});
       for (int it = 0; it < P.vel_iters; ++it) lpass(BoolC<false>{});
     }
@@ -1501,6 +1535,32 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         for (int it = 0; it < P.pos_iters && done != islm; ++it) {
           if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
           level_sync();
+#if MACM_BRANCHFREE_WAVE_POS
+          // branch-free level steps as in the velocity passes: the lanes outside the level (or of
+          // an island that has left) correct their own dummy slot in s_tm and take their minimum
+          // into its first word
+          const int mylvl = (lhas && !((done >> lisl) & 1ull)) ? lvl : -1;
+          float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
+          float2* const pda = lhas ? s_c + la : pdd;
+          float2* const pdb = lhas ? s_c + lb : pdd;
+          int* const pmd = reinterpret_cast<int*>(pdd);
+          int* const pmi = lhas ? s_pmin + lisl : pmd;
+          for (int l = 0; l < dmulti; ++l) {
+            const bool on = mylvl == l;
+            float2* const pa = on ? pda : pdd;
+            float2* const pb = on ? pdb : pdd;
+            int* const pm = on ? pmi : pmd;
+            const float2 cA0 = *pa, cB0 = *pb;
+            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+            *pa = make_float2(cAx, cAy);
+            *pb = make_float2(cBx, cBy);
+            // order-preserving int of the float for atomicMin
+            const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
+            atomicMin(pm, key);
+            level_sync();
+          }
+#else
           for (int l = 0; l < dmulti; ++l) {
             if (lhas && lvl == l && !((done >> lisl) & 1ull)) {
               const float2 cA0 = s_c[la], cB0 = s_c[lb];
@@ -1514,6 +1574,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
             }
             level_sync();
           }
+#endif
           int km = lane < nisl ? s_pmin[lane] : 0;
           km = km >= 0 ? km : (km ^ 0x7fffffff);
           done |= __builtin_amdgcn_ballot_w64(lane < nisl && !((done >> lane) & 1ull) &&

@@ -365,7 +365,12 @@ __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
 
 __host__ __device__ inline int wg_isl_stride(int N) { return N / 2 + 2; }
 // solver LDS: velocities + positions (16 B per body), record/impulse/ab rings, big-island list
-__host__ __device__ inline int wg_solve_lds(int N) { return 16 * N + 5 * wg_isl_stride(N) + 16; }
+// kernel B: velocities and positions (16 B per body), the islands' pass minima (which double as the
+// velocity passes' 64 dummy slots, so at least 512 B), their solved flags, slack
+__host__ __device__ inline int wg_solve_mins_bytes(int N) {
+  return 4 * wg_isl_stride(N) > 512 ? 4 * wg_isl_stride(N) : 512;
+}
+__host__ __device__ inline int wg_solve_lds(int N) { return 16 * N + wg_solve_mins_bytes(N) + wg_isl_stride(N) + 16; }
 
 template <typename OT>
 __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffers B, int cur, int tcap,
@@ -1316,6 +1321,9 @@ __device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0
 // passes are Box2D's: warm start, vel_iters velocity passes, StoreImpulses, position
 // integration, up to pos_iters position passes with each island leaving after the first pass
 // whose minimum separation is >= -3 linearSlop.
+#ifndef MACM_BRANCHFREE_LEVELS  // A/B knob: 0 = an exec-masked branch per velocity level step
+#define MACM_BRANCHFREE_LEVELS 1
+#endif
 __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -1324,7 +1332,9 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
   int* s_mins = (int*)(s_c + N);              // [IS] per island: minimum separation of the pass (key)
-  uint8_t* s_done = (uint8_t*)(s_mins + IS);  // [IS] per island: position-solved
+  uint8_t* s_done = (uint8_t*)s_mins + wg_solve_mins_bytes(N);  // [IS] per island: position-solved
+  float2* s_dum = (float2*)s_mins;  // [W] the velocity passes' dummy slots (s_mins is set per position pass)
+  (void)s_dum;
   const size_t en = (size_t)e * N;
   const int nisl = B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
@@ -1400,6 +1410,27 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       const uint32_t ab = __float_as_uint(cur.r.x);
       const int a = ab & 0xffffu, b = ab >> 16;
       float2 im = cur.m;
+#if MACM_BRANCHFREE_LEVELS
+      // every lane runs every level step, the lanes outside the level on their own dummy slot (no
+      // exec-mask branch per level); only the level's lanes keep their impulses
+      float2* const pa0 = s_v + a;
+      float2* const pb0 = s_v + b;
+      float2* const pd = s_dum + lane;
+      for (int lv = lv0; lv <= lv1; ++lv) {
+        const bool on = mylv == lv;
+        float2* const pa = on ? pa0 : pd;
+        float2* const pb = on ? pb0 : pd;
+        float2 va = *pa, vb = *pb;
+        float lx = im.x, ly = im.y;
+        if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB);
+        else gs_velocity(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB, kmass, friction);
+        *pa = va;
+        *pb = vb;
+        im.x = on ? lx : im.x;
+        im.y = on ? ly : im.y;
+        level_sync();
+      }
+#else
       for (int lv = lv0; lv <= lv1; ++lv) {
         if (mylv == lv) {
           float2 va = s_v[a], vb = s_v[b];
@@ -1410,6 +1441,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
         }
         level_sync();
       }
+#endif
       const int k = c * W + lane;
       if (!warm && k < nc) {
         if (last) g_lam[cur.o] = im;
