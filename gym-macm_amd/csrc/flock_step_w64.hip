@@ -96,8 +96,8 @@ constexpr bool kLevels = true;
 #ifndef MACM_BRANCHFREE_WAVE_LEVELS  // A/B knob: 0 = an exec-masked branch per level step (T <= 64 levels)
 #define MACM_BRANCHFREE_WAVE_LEVELS 1
 #endif
-#ifndef MACM_BRANCHFREE_WAVE_POS  // A/B knob: 1 = branch-free position level steps too (T <= 64 levels)
-#define MACM_BRANCHFREE_WAVE_POS 0
+#ifndef MACM_BRANCHFREE_WAVE_POS  // A/B knob: 0 = exec-masked position level steps (T <= 64 levels)
+#define MACM_BRANCHFREE_WAVE_POS 1
 #endif
 #ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
 #define MACM_PRIO2_T 3

@@ -1321,6 +1321,9 @@ __device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0
 // passes are Box2D's: warm start, vel_iters velocity passes, StoreImpulses, position
 // integration, up to pos_iters position passes with each island leaving after the first pass
 // whose minimum separation is >= -3 linearSlop.
+#ifndef MACM_BRANCHFREE_POS  // A/B knob: 1 = branch-free position level steps in kernel B too
+#define MACM_BRANCHFREE_POS 0
+#endif
 #ifndef MACM_BRANCHFREE_LEVELS  // A/B knob: 0 = an exec-masked branch per velocity level step
 #define MACM_BRANCHFREE_LEVELS 1
 #endif
@@ -1489,6 +1492,27 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       const uint32_t ab = __float_as_uint(cur.r.x);
       const int a = ab & 0xffffu, b = ab >> 16;
       const bool live = !s_done[I];
+#if MACM_BRANCHFREE_POS
+      // branch-free level steps as in the velocity passes; the dummy slots are in s_v (dead after
+      // the position integration), a dummy lane's minimum goes to its slot's first word
+      float2* const pdd = s_v + lane;
+      const int mylvp = live ? mylv : -1;
+      float2* const pca = s_c + a;
+      float2* const pcb = s_c + b;
+      int* const pmi = s_mins + I;
+      for (int lv = lv0; lv <= lv1; ++lv) {
+        const bool on = mylvp == lv;
+        float2* const pa = on ? pca : pdd;
+        float2* const pb = on ? pcb : pdd;
+        int* const pm = on ? pmi : reinterpret_cast<int*>(pdd);
+        float2 ca = *pa, cb = *pb;
+        const float sep = gs_position(ca, cb, P.radius, mA, mB);
+        *pa = ca;
+        *pb = cb;
+        atomicMin(pm, sep_key(sep));
+        level_sync();
+      }
+#else
       for (int lv = lv0; lv <= lv1; ++lv) {
         if (live && mylv == lv) {
           float2 ca = s_c[a], cb = s_c[b];
@@ -1499,6 +1523,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
         }
         level_sync();
       }
+#endif
       wait_vm();
       cur = nxt;
     }
