@@ -1321,8 +1321,8 @@ __device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0
 // passes are Box2D's: warm start, vel_iters velocity passes, StoreImpulses, position
 // integration, up to pos_iters position passes with each island leaving after the first pass
 // whose minimum separation is >= -3 linearSlop.
-#ifndef MACM_BRANCHFREE_POS  // A/B knob: 1 = branch-free position level steps in kernel B too
-#define MACM_BRANCHFREE_POS 0
+#ifndef MACM_BRANCHFREE_POS  // A/B knob: 0 = exec-masked position level steps in kernel B
+#define MACM_BRANCHFREE_POS 1
 #endif
 #ifndef MACM_BRANCHFREE_LEVELS  // A/B knob: 0 = an exec-masked branch per velocity level step
 #define MACM_BRANCHFREE_LEVELS 1
