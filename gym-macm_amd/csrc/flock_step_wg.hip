@@ -1321,6 +1321,9 @@ __device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0
 // passes are Box2D's: warm start, vel_iters velocity passes, StoreImpulses, position
 // integration, up to pos_iters position passes with each island leaving after the first pass
 // whose minimum separation is >= -3 linearSlop.
+#ifndef MACM_LEVEL_ADDR_AHEAD  // A/B knob: 0 = select a level's LDS addresses at the start of its step
+#define MACM_LEVEL_ADDR_AHEAD 1
+#endif
 #ifndef MACM_BRANCHFREE_POS  // A/B knob: 0 = exec-masked position level steps in kernel B
 #define MACM_BRANCHFREE_POS 1
 #endif
@@ -1419,6 +1422,29 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       float2* const pa0 = s_v + a;
       float2* const pb0 = s_v + b;
       float2* const pd = s_dum + lane;
+#if MACM_LEVEL_ADDR_AHEAD
+      // the next level's addresses are selected while this level solves (off the read's path)
+      bool on = mylv == lv0;
+      float2* pa = on ? pa0 : pd;
+      float2* pb = on ? pb0 : pd;
+      for (int lv = lv0; lv <= lv1; ++lv) {
+        float2 va = *pa, vb = *pb;
+        const bool onc = on;
+        on = mylv == lv + 1;
+        float2* const na = on ? pa0 : pd;
+        float2* const nb = on ? pb0 : pd;
+        float lx = im.x, ly = im.y;
+        if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB);
+        else gs_velocity(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB, kmass, friction);
+        *pa = va;
+        *pb = vb;
+        im.x = onc ? lx : im.x;
+        im.y = onc ? ly : im.y;
+        pa = na;
+        pb = nb;
+        level_sync();
+      }
+#else
       for (int lv = lv0; lv <= lv1; ++lv) {
         const bool on = mylv == lv;
         float2* const pa = on ? pa0 : pd;
@@ -1433,6 +1459,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
         im.y = on ? ly : im.y;
         level_sync();
       }
+#endif
 #else
       for (int lv = lv0; lv <= lv1; ++lv) {
         if (mylv == lv) {
@@ -1500,6 +1527,27 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       float2* const pca = s_c + a;
       float2* const pcb = s_c + b;
       int* const pmi = s_mins + I;
+#if MACM_LEVEL_ADDR_AHEAD
+      bool on = mylvp == lv0;
+      float2* pa = on ? pca : pdd;
+      float2* pb = on ? pcb : pdd;
+      int* pm = on ? pmi : reinterpret_cast<int*>(pdd);
+      for (int lv = lv0; lv <= lv1; ++lv) {
+        float2 ca = *pa, cb = *pb;
+        on = mylvp == lv + 1;
+        float2* const na = on ? pca : pdd;
+        float2* const nb = on ? pcb : pdd;
+        int* const nm = on ? pmi : reinterpret_cast<int*>(pdd);
+        const float sep = gs_position(ca, cb, P.radius, mA, mB);
+        *pa = ca;
+        *pb = cb;
+        atomicMin(pm, sep_key(sep));
+        pa = na;
+        pb = nb;
+        pm = nm;
+        level_sync();
+      }
+#else
       for (int lv = lv0; lv <= lv1; ++lv) {
         const bool on = mylvp == lv;
         float2* const pa = on ? pca : pdd;
@@ -1512,6 +1560,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
         atomicMin(pm, sep_key(sep));
         level_sync();
       }
+#endif
 #else
       for (int lv = lv0; lv <= lv1; ++lv) {
         if (live && mylv == lv) {
