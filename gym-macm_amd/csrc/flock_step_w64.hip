@@ -99,6 +99,9 @@ constexpr bool kLevels = true;
 #ifndef MACM_BRANCHFREE_WAVE_POS  // A/B knob: 0 = exec-masked position level steps (T <= 64 levels)
 #define MACM_BRANCHFREE_WAVE_POS 1
 #endif
+#ifndef MACM_WAVE_LEVEL_ADDR_AHEAD  // A/B knob: 0 = select a level's LDS addresses at the start of its step
+#define MACM_WAVE_LEVEL_ADDR_AHEAD 1
+#endif
 #ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
 #define MACM_PRIO2_T 3
 #endif
@@ -1364,6 +1367,30 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
       const int mylvl = lhas ? lvl : -1;
       auto lpass = [&](auto warm) {
+#if MACM_WAVE_LEVEL_ADDR_AHEAD
+        // the next level's addresses are selected while this level solves (off the read's path)
+        bool on = mylvl == 0;
+        float2* pa = on ? pda : pdd;
+        float2* pb = on ? pdb : pdd;
+        for (int l = 0; l < dmulti; ++l) {
+          const float2 vA0 = *pa, vB0 = *pb;
+          const bool onc = on;
+          on = mylvl == l + 1;
+          float2* const na = on ? pda : pdd;
+          float2* const nb = on ? pdb : pdd;
+          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
+          float nl = lln, nt = llt;
+          if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB);
+          else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB, kmass, friction);
+          *pa = make_float2(vAx, vAy);
+          *pb = make_float2(vBx, vBy);
+          lln = onc ? nl : lln;
+          llt = onc ? nt : llt;
+          pa = na;
+          pb = nb;
+          level_sync();
+        }
+#else
         for (int l = 0; l < dmulti; ++l) {
           const bool on = mylvl == l;
           float2* const pa = on ? pda : pdd;
@@ -1379,6 +1406,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           llt = on ? nt : llt;
           level_sync();
         }
+#endif
       };
 #else
       auto lpass = [&](auto warm) {
@@ -1545,6 +1573,30 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           float2* const pdb = lhas ? s_c + lb : pdd;
           int* const pmd = reinterpret_cast<int*>(pdd);
           int* const pmi = lhas ? s_pmin + lisl : pmd;
+#if MACM_WAVE_LEVEL_ADDR_AHEAD
+          bool on = mylvl == 0;
+          float2* pa = on ? pda : pdd;
+          float2* pb = on ? pdb : pdd;
+          int* pm = on ? pmi : pmd;
+          for (int l = 0; l < dmulti; ++l) {
+            const float2 cA0 = *pa, cB0 = *pb;
+            on = mylvl == l + 1;
+            float2* const na = on ? pda : pdd;
+            float2* const nb = on ? pdb : pdd;
+            int* const nm = on ? pmi : pmd;
+            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+            *pa = make_float2(cAx, cAy);
+            *pb = make_float2(cBx, cBy);
+            // order-preserving int of the float for atomicMin
+            const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
+            atomicMin(pm, key);
+            pa = na;
+            pb = nb;
+            pm = nm;
+            level_sync();
+          }
+#else
           for (int l = 0; l < dmulti; ++l) {
             const bool on = mylvl == l;
             float2* const pa = on ? pda : pdd;
@@ -1560,6 +1612,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
             atomicMin(pm, key);
             level_sync();
           }
+#endif
 #else
           for (int l = 0; l < dmulti; ++l) {
             if (lhas && lvl == l && !((done >> lisl) & 1ull)) {
