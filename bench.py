@@ -120,6 +120,15 @@ def load_traffic(path):
     return j
 
 
+def lib_sha256():
+    """sha256 of the HIP library this process loaded (gym_macm._abi.LIB_PATH): a PMC summary is
+    quoted as `traffic` only when it was measured on this very binary."""
+    import hashlib
+    from gym_macm import _abi
+    with open(_abi.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +166,10 @@ def main():
     ap.add_argument("--trajectory", action="store_true",
                     help="random policy, rollout launch: keep every step's outputs ([K, E, N, ...] buffers, "
                          "macm_world_rollout_traj), as the reference returns (obs, rewards) from every env.step")
+    ap.add_argument("--host-wait", choices=("default", "spin"), default="default",
+                    help="spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is initialised, so "
+                         "the host polls for completion instead of waiting for an interrupt (A/B of the host "
+                         "gap around the timed launch)")
     ap.add_argument("--dump-final", default=None,
                     help="test hook: every rank writes its final state and counters to PATH.rank<r>.npz")
     args = ap.parse_args()
@@ -164,6 +177,12 @@ def main():
         args.traffic_json = os.path.join(REPO, "profiles", "pmc_flock_step.json" if args.env == "flock"
                                          else "pmc_tdm_step.json")
 
+    if args.host_wait == "spin":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)  # torch's HIP runtime (already loaded)
+        rc = hip.hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
+        if rc != 0:
+            raise SystemExit(f"hipSetDeviceFlags(hipDeviceScheduleSpin) failed: {rc}")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -187,6 +206,9 @@ def main():
 
     K, W = args.steps, args.warmup
     strong = args.total_envs > 0
+    if strong and args.total_envs < world:
+        # a rank with no env could not create a world and the others would wait at the first barrier
+        raise SystemExit(f"--total-envs {args.total_envs} < {world} ranks: every rank needs at least one env")
     if strong:  # this rank's contiguous share of the job's envs
         e_off, E = gdist.strong_split(args.total_envs, world, rank)
     else:  # weak: --envs per GPU
@@ -197,6 +219,9 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 1 + (0 if strong else rank))
 
+    # strong: every rank draws the whole job's actions and keeps its rows, so each env sees the same
+    # actions at any rank count; that is (W + K) x total_envs x N x A bytes per rank (BASELINE C5,
+    # 16,384 x 1024 agents x 3 B, 12 steps: 0.6 GB), freed once the rank's slice is copied
     def draw(shape, high=3):  # uniform uint8 in [0, high); strong: the whole job's draw, this rank's rows
         if not strong:
             return torch.randint(0, high, shape, dtype=torch.uint8, device=dev, generator=gen)
@@ -262,6 +287,7 @@ def main():
         torch.cuda.synchronize(dev)
         if args.env == "flock":
             world_h.reset_counters()
+        spilled0 = world_h.spilled()
         if launched:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -282,13 +308,14 @@ def main():
         t1 = time.perf_counter()
         if launched:
             dist.barrier()
-        return t1 - t0, ev0.elapsed_time(ev1)
+        return t1 - t0, ev0.elapsed_time(ev1), world_h.spilled() - spilled0
 
-    elapsed, ev_ms = timed_window(rollout)
+    elapsed, ev_ms, spilled = timed_window(rollout)
     kernel_ms = ev_ms / K  # per step on the launch stream (a rollout launch covers all K steps)
     # one small RCCL all-reduce of counters after the timed region (no data-path collective)
     status = int(gdist.reduce_counters([world_h.status()], device=red_dev, op="max")[0])
     cnt = gdist.reduce_counters(world_h.counters(), device=red_dev)
+    spilled = int(gdist.reduce_counters([spilled], device=red_dev)[0])
     elapsed = gdist.reduce_max(elapsed, device=red_dev)
     total_agent_steps = (args.total_envs if strong else world * E) * N * K
     if args.env == "flock":
@@ -322,10 +349,17 @@ def main():
         tj = load_traffic(args.traffic_json)
         if args.obs_f64:  # the scalar sweep exists only in the float32-obs instantiation
             kname = kname.replace("float", "double").replace("double, true>", "double, false>")
+        spl = K if (rollout and N <= 64) else 1  # env steps per launch of the priced kernel
+        traffic_src = None
         if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
-                and tj.get("policy", "random") == args.policy):
-            # per step (a rollout launch's bytes over its steps), like achieved
-            traffic = tj.get("hbm_bytes_per_launch") / tj.get("steps_per_launch", 1)
+                and tj.get("policy", "random") == args.policy and tj.get("steps_per_launch", 1) == spl):
+            if tj.get("lib_sha256") and tj["lib_sha256"] == lib_sha256():
+                # per step (a rollout launch's bytes over its steps), like achieved
+                traffic = tj.get("hbm_bytes_per_launch") / tj.get("steps_per_launch", 1)
+                traffic_src = f"{os.path.relpath(args.traffic_json, REPO)} (commit {tj.get('commit')})"
+            else:
+                traffic_src = (f"{os.path.relpath(args.traffic_json, REPO)} was measured on another build "
+                               f"(lib sha256 {str(tj.get('lib_sha256'))[:12]}): not quoted")
         hbm_frac = None if traffic is None else traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
@@ -386,10 +420,15 @@ def main():
                 "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                 # the PMC-measured HBM bytes over the same time: how far from HBM-bound the kernel is
                 "hbm_frac_measured": hbm_frac,
+                "traffic_source": traffic_src,
                 "kernel": kname, "kernel_ms": kernel_ms,  # per step
-                "steps_per_launch": K if (rollout and N <= 64) else 1,
-                "bytes_alg_per_launch": b_alg * E * N,
+                "steps_per_launch": spl,
+                "bytes_alg_per_step": b_alg * E * N,
+                "bytes_alg_per_launch": b_alg * E * N * spl,
             },
+            # env-steps taken by the spill step (dense envs past the fast kernels' LDS capacities) in
+            # the timed window: capacities follow the box's free memory (macm_world_create)
+            "spilled_env_steps": spilled,
         }
         if args.env == "flock":
             out["counters"] = {"agent_steps": int(cnt[0]), "collided_agent_steps": int(cnt[1]),
@@ -405,7 +444,7 @@ def main():
                 world_h.reset(args.seed, e_off)
             if args.policy == "bots":
                 policy()  # the first actions from the initial obs again
-            el2, ev2 = timed_window(False)
+            el2, ev2, _ = timed_window(False)
             out["per_step_launch"] = {"value": E * N * K / el2, "ms_per_step": el2 / K * 1e3,
                                       "kernel_ms_per_step": ev2 / K}
         if world == 1 and not args.no_cpu_baseline:

@@ -191,7 +191,8 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
                                          int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
                                          uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out,
                                          unsigned char* lds, const TdmParams* TP = nullptr,
-                                         const TdmBuffers* TB = nullptr, float2 F = make_float2(0.0f, 0.0f)) {
+                                         const TdmBuffers* TB = nullptr, float2 F = make_float2(0.0f, 0.0f),
+                                         int held_slot = -1) {
   constexpr bool kT = MODE == kTdm;
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
@@ -233,8 +234,9 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     if (!wide) return ((livem >> a) & (livem >> b) & 1ull) != 0ull;
     return ((s_alivew[a >> 5] >> (a & 31)) & (s_alivew[b >> 5] >> (b & 31)) & 1u) != 0u;
   };
-  // the HBM working set of this env's slot, capacity C (touching contacts are a subset of the list)
-  const int slot = acquire_slot(B, e, s_misc + 7);
+  // the HBM working set of this env's slot, capacity C (touching contacts are a subset of the list);
+  // held_slot >= 0: the caller took it before committing anything (the workgroup TDM step)
+  const int slot = held_slot >= 0 ? held_slot : acquire_slot(B, e, s_misc + 7);
   if (slot < 0) {  // the pool stayed full for ~1 s: not stepped, reported
     if (tid == 0) {
       B.status[e] |= MACM_ST_SPILL_WAIT;
@@ -708,6 +710,9 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       }
       s_slp[tid] = ang;  // the sleep clocks are dead: the angles for the observation
     }
+    // the observation reads only LDS: the slot goes back to the pool before the O(N^2) obs writes
+    // (release_slot's barrier also orders the s_slp writes before the obs reads)
+    release_slot(B, slot);
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
     if (wide && kTdmBlockObsLinear)
@@ -798,8 +803,8 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       ec[3] += (unsigned long long)dn;
       if (B.spill_count) B.spill_count[e] += 1u;
     }
+    release_slot(B, slot);  // the observation above reads recs (HBM when !RECS_LDS)
   }
-  release_slot(B, slot);
 }
 
 }  // namespace spill

@@ -86,6 +86,8 @@ struct macm_world {
   // workgroup-path rollouts: env slices on streams of their own (created on first use)
   std::vector<hipStream_t> slice_streams;
   std::vector<hipEvent_t> slice_events;  // [0] fork, [1 + s] join of slice s
+  int slots_alloc = 0;  // spill working-set slots allocated (== E: one per env)
+  int pool0 = 0;        // B.sp_pool as created (0: one slot per env), restored by set_debug
 };
 
 struct macm_tdm {
@@ -104,6 +106,8 @@ struct macm_tdm {
   bool mt_valid = false;
   uint32_t* hstat = nullptr;
   unsigned long long* bad = nullptr;
+  int slots_alloc = 0;  // as macm_world
+  int pool0 = 0;
 };
 
 static thread_local std::string g_last_error;
@@ -283,8 +287,8 @@ void save_stream(std::vector<uint32_t>& host, int e, const PyMT19937& r) {
 extern "C" {
 
 const char* macm_version(void) {
-  return "macm-hip 0.4.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernels N<=1024, "
-         "spill step for dense envs; TDM: wave-per-env kernel N<=64)";
+  return "macm-hip 0.5.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernels N<=1024, "
+         "spill step for dense envs; TDM: wave-per-env kernel N<=64, workgroup step N<=1024)";
 }
 int macm_abi_version(void) { return MACM_ABI_VERSION; }
 const char* macm_last_error(void) { return g_last_error.c_str(); }
@@ -439,6 +443,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.spill_count, 0, sizeof(uint32_t) * n_envs);
   B.sp_pool = SL < n_envs ? (int32_t)SL : 0;
+  w->slots_alloc = (int)SL;
+  w->pool0 = B.sp_pool;
   if (e == hipSuccess && B.sp_lock) e = hipMemset(B.sp_lock, 0, sizeof(uint32_t) * SL);
   if (e == hipSuccess && !w->wave) {
     hipDeviceProp_t prop;
@@ -941,22 +947,35 @@ int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream) {
   return MACM_OK;
 }
 
+// MACM_DEBUG_SPILL_POOL (a test hook): share `pool` of the slots allocated at creation; a call
+// without the flag brings back the world's own pool (or one slot per env). The locks are cleared
+// only after the device has finished every step that could hold one.
+extern "C++" template <typename Wt>
+static int set_spill_pool(Wt* w, int32_t flags, int pool) {
+  const bool want = (flags & MACM_DEBUG_SPILL_POOL) != 0;
+  if (want && (pool < 1 || pool > w->slots_alloc))
+    return fail(MACM_E_INVALID, "SPILL_POOL: 1 <= slots <= the " + std::to_string(w->slots_alloc) + " allocated");
+  const int target = want ? pool : w->pool0;
+  if (target == w->B.sp_pool) return MACM_OK;
+  DeviceGuard g(w->device);
+  HIP_TRY(hipDeviceSynchronize());
+  if (target > 0) {
+    if (!w->B.sp_lock && dalloc(w->allocs, &w->B.sp_lock, (size_t)w->slots_alloc)) return MACM_E_OOM;
+    HIP_TRY(hipMemset(w->B.sp_lock, 0, sizeof(uint32_t) * w->slots_alloc));
+  }
+  w->B.sp_pool = target;
+  return MACM_OK;
+}
+
 int macm_world_set_debug(macm_world* w, int32_t flags) {
   if (!w) return fail(MACM_E_INVALID, "world is NULL");
   const int pool = (flags & MACM_DEBUG_SPILL_POOL) ? (flags >> 8) : 0;
   flags &= 0xff;
   if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SWEEP_CELLS | MACM_DEBUG_SWEEP_ALL_PAIRS | MACM_DEBUG_SPILL_POOL))
     return fail(MACM_E_INVALID, "unknown debug flag");
-  if (flags & MACM_DEBUG_SPILL_POOL) {
-    const int have = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;  // slots allocated
-    if (pool < 1 || pool > have) return fail(MACM_E_INVALID, "SPILL_POOL: 1 <= slots <= the slots allocated");
-    DeviceGuard g(w->device);
-    if (!w->B.sp_lock && dalloc(w, &w->B.sp_lock, (size_t)have)) return MACM_E_OOM;
-    HIP_TRY(hipMemset(w->B.sp_lock, 0, sizeof(uint32_t) * have));
-    w->B.sp_pool = pool;
-  }
   if ((flags & MACM_DEBUG_SWEEP_CELLS) && (flags & MACM_DEBUG_SWEEP_ALL_PAIRS))
     return fail(MACM_E_INVALID, "SWEEP_CELLS and SWEEP_ALL_PAIRS exclude each other");
+  if (int rc = set_spill_pool(w, flags, pool)) return rc;
   w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
   w->P.sweep = (flags & MACM_DEBUG_SWEEP_CELLS) ? 1 : (flags & MACM_DEBUG_SWEEP_ALL_PAIRS) ? 2 : 0;
   return MACM_OK;
@@ -1044,7 +1063,10 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   w->cur = 0;
   w->wave = N <= 64;
   const int C = N * (N - 1) / 2;  // every pair: the list never overflows
-  const int64_t SL = default_capacity(N, n_envs, C, free_bytes).slots;  // spill working-set slots
+  // spill working-set slots. The wave kernel (N <= 64) hands a crowded env to the spill step after
+  // it has committed the step's combat state, so it gets one slot per env (<= 100 KB each: a pool
+  // wait must never leave an env half-stepped); the workgroup step takes its slot before committing
+  const int64_t SL = N <= 64 ? (int64_t)n_envs : default_capacity(N, n_envs, C, free_bytes).slots;
   StepParams& P = w->P;
   memset(&P, 0, sizeof(P));
   P.n_envs = n_envs;
@@ -1116,6 +1138,8 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * E);
   if (e == hipSuccess) e = hipMemset(B.spill_count, 0, sizeof(uint32_t) * E);
   B.sp_pool = SL < n_envs ? (int32_t)SL : 0;
+  w->slots_alloc = (int)SL;
+  w->pool0 = B.sp_pool;
   if (e == hipSuccess && B.sp_lock) e = hipMemset(B.sp_lock, 0, sizeof(uint32_t) * SL);
   if (e != hipSuccess) {
     free_tdm(w);
@@ -1339,9 +1363,12 @@ int macm_tdm_observe(macm_tdm* w, const macm_tdm_outputs* out, void* stream) {
 
 static int tdm_copy_state(macm_tdm* w, const macm_tdm_state* st, void* stream, bool to_device) {
   if (!w || !st) return fail(MACM_E_INVALID, "tdm/state is NULL");
+  if (st->contact_stride < 0) return fail(MACM_E_INVALID, "contact_stride must be >= 0");
   DeviceGuard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   const size_t E = w->P.n_envs, N = w->P.n_agents, C = w->P.max_contacts;
+  const size_t Cs = st->contact_stride > 0 ? (size_t)st->contact_stride : C;  // the caller's row length
+  const size_t Cw = Cs < C ? Cs : C;                                           // entries moved per row
   struct Item {
     void* user;
     void* dev;
@@ -1366,15 +1393,17 @@ static int tdm_copy_state(macm_tdm* w, const macm_tdm_state* st, void* stream, b
     if (st->contact_count)
       HIP_TRY(hipMemcpyAsync(st->contact_count, w->B.ccount[w->cur], E * sizeof(int32_t), hipMemcpyDefault, s));
     if (st->contact_ab)
-      HIP_TRY(hipMemcpyAsync(st->contact_ab, w->B.cab[w->cur], E * C * sizeof(uint32_t), hipMemcpyDefault, s));
+      HIP_TRY(copy_rows(st->contact_ab, Cs * sizeof(uint32_t), w->B.cab[w->cur], C * sizeof(uint32_t),
+                        Cw * sizeof(uint32_t), E, s));
     if (st->contact_imp)
-      HIP_TRY(hipMemcpyAsync(st->contact_imp, w->B.cimp[w->cur], E * C * sizeof(float2), hipMemcpyDefault, s));
+      HIP_TRY(copy_rows(st->contact_imp, Cs * sizeof(float2), w->B.cimp[w->cur], C * sizeof(float2),
+                        Cw * sizeof(float2), E, s));
   }
   if (to_device) {
     if (!st->contact_count != !st->contact_ab)
       return fail(MACM_E_INVALID, "contact_count and contact_ab must be given together");
     if (st->contact_count) {
-      const int rc = stage_lists(w->B, w->cur, w->bad, E, C, C, (int)N, st->contact_count, st->contact_ab,
+      const int rc = stage_lists(w->B, w->cur, w->bad, E, C, Cs, (int)N, st->contact_count, st->contact_ab,
                                  st->contact_imp, s);
       if (rc) return rc;
       w->cur ^= 1;
@@ -1446,14 +1475,7 @@ int macm_tdm_set_debug(macm_tdm* w, int32_t flags) {
   flags &= 0xff;
   if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SPILL_POOL))
     return fail(MACM_E_INVALID, "unknown debug flag (TDM: FORCE_SPILL, SPILL_POOL)");
-  if (flags & MACM_DEBUG_SPILL_POOL) {
-    const int have = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;  // slots allocated
-    if (pool < 1 || pool > have) return fail(MACM_E_INVALID, "SPILL_POOL: 1 <= slots <= the slots allocated");
-    DeviceGuard g(w->device);
-    if (!w->B.sp_lock && dalloc(w->allocs, &w->B.sp_lock, (size_t)have)) return MACM_E_OOM;
-    HIP_TRY(hipMemset(w->B.sp_lock, 0, sizeof(uint32_t) * have));
-    w->B.sp_pool = pool;
-  }
+  if (int rc = set_spill_pool(w, flags, pool)) return rc;
   w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
   return MACM_OK;
 }

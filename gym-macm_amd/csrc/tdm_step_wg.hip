@@ -99,6 +99,17 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
   uint32_t* s_aw = (uint32_t*)(lds + L.aw);
   uint32_t* s_atw = (uint32_t*)(lds + L.atw);
 
+  // The spill working-set slot is taken before anything of this step is committed: a pool that
+  // stays full (~1 s) leaves the env wholly unstepped and reported, never half-stepped
+  __shared__ int s_slot;
+  const int slot = spill::acquire_slot(B, e, &s_slot);
+  if (slot < 0) {
+    if (tid == 0) {
+      B.status[e] |= MACM_ST_SPILL_WAIT;
+      report_status(B, MACM_ST_SPILL_WAIT);
+    }
+    return;
+  }
   bool act = false;
   float2 p = make_float2(0.0f, 0.0f);
   float ang = 0.0f;
@@ -229,7 +240,7 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
   __threadfence_block();
   // ---- Box2D step of the living bodies, TDM.get_obs, done / winner --------------------------------
   spill::step_env<OT, true, kTdm>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out, lds, &TP, &TB,
-                                  make_float2(Fx, Fy));
+                                  make_float2(Fx, Fy), slot);
 }
 
 // TDM world creation (combat.py:78-102) for N > 64: every body active with init_health, zero

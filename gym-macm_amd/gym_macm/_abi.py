@@ -128,7 +128,7 @@ TDM_STATE_FIELDS = ("pos", "vel", "angle", "fat", "sleep", "health", "cd_atk", "
 
 
 class MacmTdmState(Structure):
-    _fields_ = [(n, c_void_p) for n in TDM_STATE_FIELDS]
+    _fields_ = [(n, c_void_p) for n in TDM_STATE_FIELDS] + [("contact_stride", ctypes.c_int64)]
 
 
 def tdm_config_from_defaults() -> "MacmTdmConfig":

@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _abi
-from .world import _ptr
+from .world import _ptr, check_traj
 
 
 def tdm_config(n_agents=(1, 1), obs_f64=False, fresh_raycast=False, decay_mov_penalty=False, validate_actions=False,
@@ -166,10 +166,11 @@ class TdmWorld:
 
     def _traj_call(self, fn, name, actions, K, traj):
         traj = self.trajectory_buffers(K) if traj is None else traj
-        for k, t in traj.items():
-            if t is not None and (t.device != self.device or not t.is_contiguous() or t.shape[0] < K):
-                raise ValueError(f"trajectory buffer {k!r} must be a contiguous [>= {K}, ...] tensor on {self.device}")
-        out = _abi.MacmTdmOutputs(*[_ptr(traj.get(k)) for k in self._TRAJ_KEYS])
+        odt = torch.float64 if self.cfg.obs_f64 else torch.float32
+        E, N = self.E, self.N
+        spec = dict(obs=(odt, (E, N, N - 1, 4)), mask=(torch.uint8, (E, N, N - 1)), health=(torch.float64, (E, N)),
+                    alive=(torch.uint8, (E, N)), done=(torch.uint8, (E,)), winner=(torch.int32, (E,)))
+        out = _abi.MacmTdmOutputs(*[_ptr(t) for t in check_traj(traj, spec, K, self.device, self._TRAJ_KEYS)])
         _abi.check(fn(self.h, _ptr(actions), K, ctypes.byref(out), self._stream()), name)
         if K > 0:  # the world's own buffers keep the current step's outputs
             for k in self._TRAJ_KEYS:
@@ -220,8 +221,11 @@ class TdmWorld:
         _abi.check(self.L.macm_tdm_observe(self.h, ctypes.byref(self._out), self._stream()), "macm_tdm_observe")
         return self.outputs()
 
-    def state_buffers(self):
-        E, N, C = self.E, self.N, self.C
+    def state_buffers(self, stride=None):
+        """Host arrays of get_state's layout; contact_ab / contact_imp rows of `stride` entries
+        (default: C = every pair)."""
+        E, N = self.E, self.N
+        C = self.C if stride is None else int(stride)
         return dict(pos=np.zeros((E, N, 2), np.float32), vel=np.zeros((E, N, 2), np.float32),
                     angle=np.zeros((E, N), np.float32), fat=np.zeros((E, N, 4), np.float32),
                     sleep=np.zeros((E, N), np.float32), health=np.zeros((E, N), np.float64),
@@ -232,25 +236,44 @@ class TdmWorld:
                     time_passed=np.zeros((E,), np.float64), done=np.zeros((E,), np.uint8),
                     winner=np.zeros((E,), np.int32))
 
+    @staticmethod
+    def _state_struct(arrs, stride):
+        return _abi.MacmTdmState(*[ctypes.c_void_p(arrs[k].ctypes.data) if arrs.get(k) is not None else None
+                                   for k in _abi.TDM_STATE_FIELDS], int(stride))
+
     def get_state(self) -> dict:
-        s = self.state_buffers()
-        st = _abi.MacmTdmState(*[ctypes.c_void_p(s[k].ctypes.data) for k in _abi.TDM_STATE_FIELDS])
-        _abi.check(self.L.macm_tdm_get_state(self.h, ctypes.byref(st), self._stream()), "macm_tdm_get_state")
-        idx = np.arange(self.C)[None, :] >= s["contact_count"][:, None]
+        """The world's state as host arrays. The contact lists' rows hold max(contact_count) entries
+        (at least 1), not C = N(N-1)/2: only their used part crosses the bus (C is
+        523,776 at N = 1024); entries past an env's count are zero."""
+        cnt = np.zeros((self.E,), np.int32)
+        _abi.check(self.L.macm_tdm_get_state(self.h, ctypes.byref(self._state_struct({"contact_count": cnt}, 0)),
+                                             self._stream()), "macm_tdm_get_state")
+        stride = max(1, int(cnt.max(initial=0)))
+        s = self.state_buffers(stride)
+        _abi.check(self.L.macm_tdm_get_state(self.h, ctypes.byref(self._state_struct(s, stride)), self._stream()),
+                   "macm_tdm_get_state")
+        idx = np.arange(stride)[None, :] >= s["contact_count"][:, None]
         s["contact_ab"][idx] = 0
         s["contact_imp"][idx] = 0
         return s
 
     def set_state(self, s: dict) -> None:
-        ref = self.state_buffers()
+        """Inject a state (get_state's layout; the contact rows may have any length >= the counts);
+        the library validates the pairs on the device and takes nothing if any is invalid."""
+        counts = np.asarray(s["contact_count"], dtype=np.int32)
+        if counts.shape == (self.E,) and (counts.max(initial=0) > self.C or counts.min(initial=0) < 0):
+            raise ValueError(f"contact_count must lie in [0, {self.C}]")
+        ab = np.asarray(s["contact_ab"])
+        stride = ab.shape[1] if ab.ndim == 2 else self.C
+        ref = self.state_buffers(stride)
         arrs = {}
         for k, v in ref.items():
             a = np.ascontiguousarray(np.asarray(s[k], dtype=v.dtype))
             if a.shape != v.shape:
                 raise ValueError(f"state[{k!r}] has shape {a.shape}, expected {v.shape}")
             arrs[k] = a
-        st = _abi.MacmTdmState(*[ctypes.c_void_p(arrs[k].ctypes.data) for k in _abi.TDM_STATE_FIELDS])
-        _abi.check(self.L.macm_tdm_set_state(self.h, ctypes.byref(st), self._stream()), "macm_tdm_set_state")
+        _abi.check(self.L.macm_tdm_set_state(self.h, ctypes.byref(self._state_struct(arrs, stride)), self._stream()),
+                   "macm_tdm_set_state")
 
     def status(self) -> int:
         v = ctypes.c_int32()

@@ -19,6 +19,27 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def check_traj(traj: dict, spec: dict, K: int, device, keys) -> list:
+    """The caller's trajectory buffers in `keys` order (None where absent), each checked against
+    spec[key] = (dtype, per-step shape) before any kernel writes K rows into it: a buffer of the
+    wrong dtype, env count or agent count would be overrun on the device."""
+    unknown = set(traj) - set(spec)
+    if unknown:
+        raise ValueError(f"unknown trajectory buffers {sorted(unknown)}; expected a subset of {list(keys)}")
+    out = []
+    for k in keys:
+        t = traj.get(k)
+        if t is not None:
+            dt, shp = spec[k]
+            if (not isinstance(t, torch.Tensor) or t.device != device or not t.is_contiguous() or t.dim() < 1
+                    or t.shape[0] < K or t.dtype != dt or tuple(t.shape[1:]) != tuple(shp)):
+                got = (f"{tuple(t.shape)} {t.dtype} on {t.device}" if isinstance(t, torch.Tensor) else type(t).__name__)
+                raise ValueError(f"trajectory buffer {k!r} must be a contiguous {dt} tensor [>= {K}, "
+                                 f"{', '.join(map(str, shp))}] on {device}; got {got}")
+        out.append(t)
+    return out
+
+
 class World:
     """E independent envs of one Flock configuration on one GPU.
 
@@ -163,10 +184,14 @@ class World:
                     done=torch.empty((K, E), dtype=torch.uint8, device=d))
 
     def _traj_out(self, traj: dict, K: int):
-        for k, t in traj.items():
-            if t is not None and (t.device != self.device or not t.is_contiguous() or t.shape[0] < K):
-                raise ValueError(f"trajectory buffer {k!r} must be a contiguous [>= {K}, ...] tensor on {self.device}")
-        return _abi.MacmOutputs(*[_ptr(traj.get(k)) for k in ("obs", "nbr_id", "reward", "collided", "done")])
+        return _abi.MacmOutputs(*[_ptr(t) for t in check_traj(traj, self._traj_spec(), K, self.device,
+                                                              ("obs", "nbr_id", "reward", "collided", "done"))])
+
+    def _traj_spec(self) -> dict:
+        odt = torch.float64 if self.cfg.obs_f64 else torch.float32
+        E, N = self.E, self.N
+        return dict(obs=(odt, (E, N, self.OD)), nbr_id=(torch.int32, (E, N)), reward=(torch.float32, (E, N)),
+                    collided=(torch.uint8, (E, N)), done=(torch.uint8, (E,)))
 
     def _keep_last(self, traj: dict, K: int) -> None:
         # the world's own buffers keep "the current step's outputs", as after step() / rollout()

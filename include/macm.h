@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 6
+#define MACM_ABI_VERSION 7
 
 enum {
   MACM_OK = 0,
@@ -181,6 +181,9 @@ typedef struct macm_tdm_outputs {
  *   alive                  [E, N] uint8
  *   listener               [E, 2] int32     (RayCastClosestCallback.hit, body of .fixture or -1)
  *   done [E] uint8, winner [E] int32
+ *   contact_stride         entries per env row of the caller's contact_ab / contact_imp, as
+ *                          macm_state (0 = C = N(N-1)/2; ABI 7: a stride of max(contact_count)
+ *                          moves only the lists' used part, C is 523,776 at N = 1024)
  */
 typedef struct macm_tdm_state {
   void* pos;
@@ -200,6 +203,7 @@ typedef struct macm_tdm_state {
   void* time_passed;
   void* done;
   void* winner;
+  int64_t contact_stride;
 } macm_tdm_state;
 
 /*

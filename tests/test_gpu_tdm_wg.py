@@ -188,3 +188,56 @@ def test_lds_limits_only_grow():
     fsmall.step(torch.ones((2, 100, 3), dtype=torch.uint8, device="cuda:0"))
     torch.cuda.synchronize()
     assert fbig.status() == 0 and fsmall.status() == 0
+
+
+def test_tdm_wg_pooled_slots_match_one_slot_per_env():
+    """above 64 agents every TDM env-step takes the spill step, so a pooled working set
+    (fewer slots than envs) is on the main path. The workgroup step takes its slot before it commits
+    anything and returns it before the O(N^2) observation. 12 envs sharing 3 slots (and then 1) over
+    several steps equal the world with a slot per env, bit for bit, status 0; clearing the flag brings
+    back the world's own slots."""
+    E, teams, K = 12, [40, 40], 12
+    N = sum(teams)
+    kw = dict(world_width=14.0, world_height=14.0)
+    a = TdmWorld(tdm_config(teams, **kw), E, device="cuda:0")
+    b = TdmWorld(tdm_config(teams, **kw), E, device="cuda:0")
+    for x in (a, b):
+        x.reset(17, 0)
+    rng = np.random.default_rng(3)
+    for k in range(K):
+        b.set_debug(_abi.DEBUG_SPILL_POOL | ((3 if k < K // 2 else 1) << 8))
+        acts = torch.from_numpy(random_actions(rng, E, N, p_attack=0.5)).cuda()
+        a.step(acts)
+        b.step(acts)
+        for x, y in zip(a.outputs(), b.outputs()):
+            assert torch.equal(x, y), f"step {k}"
+    b.set_debug(0)
+    assert b.status() == 0 and a.status() == 0
+    sa, sb = a.get_state(), b.get_state()
+    for key in sa:
+        np.testing.assert_array_equal(sa[key], sb[key], err_msg=f"state[{key}]")
+    np.testing.assert_array_equal(a.counters(), b.counters())
+    with pytest.raises(_abi.MacmError):  # more slots than allocated
+        b.set_debug(_abi.DEBUG_SPILL_POOL | ((E + 1) << 8))
+
+
+def test_tdm_wg_state_moves_only_the_used_lists():
+    """get_state's contact rows hold max(contact_count) entries (ABI 7 contact_stride),
+    not C = N(N-1)/2 (523,776 at 1024 agents), and set_state takes such rows back."""
+    E, teams = 2, [512, 512]
+    w, orc = make_pair(E, teams, seed=5)
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        w.step(torch.from_numpy(random_actions(rng, E, 1024)).cuda())
+    st = w.get_state()
+    n = int(st["contact_count"].max())
+    assert 0 < n < w.C // 100 and st["contact_ab"].shape == (E, n) and st["contact_imp"].shape == (E, n, 2)
+    twin = TdmWorld(tdm_config(teams), E, device="cuda:0")
+    twin.reset(99, 0)
+    twin.set_state(st)
+    acts = torch.from_numpy(random_actions(rng, E, 1024)).cuda()
+    w.step(acts)
+    twin.step(acts)
+    s1, s2 = w.get_state(), twin.get_state()
+    for key in s1:
+        np.testing.assert_array_equal(s1[key], s2[key], err_msg=f"state[{key}]")

@@ -159,3 +159,30 @@ def test_trajectory_argument_checks():
         v.rollout_bots(torch.zeros((3, 4, 16, 3), dtype=torch.uint8, device="cuda:0"), 3, trajectory=True)
     out = v.rollout(acts[:0], trajectory=True)  # K = 0: nothing is stepped
     assert out["reward"].shape == (0, 4, 16)
+
+
+def test_trajectory_buffers_are_checked_before_the_launch():
+    """a caller buffer of the wrong dtype, env or agent count is refused (ValueError)
+    before any kernel writes into it, for Flock and TDM."""
+    E, N, K = 8, 16, 3
+    v = FlockVec(E, n_agents=[N], seed=1, device="cuda:0")
+    acts = flock_actions(K, E, N, 3, False)
+    good = v.world.trajectory_buffers(K)
+    bad = [dict(good, obs=good["obs"].double()),                        # f64 obs in an f32 world
+           dict(good, reward=torch.empty((K, E - 1, N), device="cuda:0")),  # fewer envs
+           dict(good, nbr_id=torch.empty((K, E, N - 1), dtype=torch.int32, device="cuda:0")),
+           dict(good, done=torch.empty((K - 1, E), dtype=torch.uint8, device="cuda:0")),  # fewer steps
+           dict(good, extra=good["done"])]
+    for t in bad:
+        with pytest.raises(ValueError):
+            v.world.rollout_traj(acts, t)
+    v.world.rollout_traj(acts, good)  # the right buffers still work
+    w = TdmWorld(tdm_config([4, 4]), E, device="cuda:0")
+    w.reset(2, 0)
+    ta = torch.randint(0, 2, (K, E, 8, 4), dtype=torch.uint8, device="cuda:0")
+    tg = w.trajectory_buffers(K)
+    for t in (dict(tg, health=tg["health"].float()), dict(tg, obs=torch.empty((K, E, 8, 8, 4), device="cuda:0")),
+              dict(tg, winner=tg["winner"].to(torch.int64))):
+        with pytest.raises(ValueError):
+            w.rollout_traj(ta, t)
+    w.rollout_traj(ta, tg)

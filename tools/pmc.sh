@@ -15,6 +15,8 @@ run() {  # $1 = pass name, rest = counters
   return $rc
 }
 BENCH_ARGS=("$@")
+# the library these passes measure (tools/pmc_summary.py records it; bench.py checks it)
+sha256sum "${MACM_LIB:-$REPO/gym-macm_amd/libmacm_hip.so}" > "$REPO/$OUT/lib.sha256"
 run fetch FETCH_SIZE && run write WRITE_SIZE && \
 run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY && \
 run sq2 SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INSTS_FLAT GRBM_GUI_ACTIVE

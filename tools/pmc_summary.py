@@ -43,8 +43,16 @@ def main():
     ap.add_argument("--steps-per-launch", type=int, default=1,
                     help="env steps one launch of the kernel takes (a rollout launch: its K)")
     ap.add_argument("--last", action="store_true", help="the kernel's last dispatch only")
+    ap.add_argument("--commit", default="", help="the commit the profiled library was built from")
     ap.add_argument("-o", "--out", default="")
     a = ap.parse_args()
+    # the library the passes ran (lib.sha256, written on the box by tools/pmc.sh): bench.py quotes the
+    # traffic only while it loads a library with this hash (no stale PMC in the line)
+    lib_sha = None
+    sp = os.path.join(a.dir, "lib.sha256")
+    if os.path.exists(sp):
+        with open(sp) as f:
+            lib_sha = f.read().split()[0]
     res = {}
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
         p = os.path.join(a.dir, sub, "run_counter_collection.csv")
@@ -62,6 +70,8 @@ def main():
         "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE",
         "per_wave": {k: v / res.get("SQ_WAVES", 1.0) for k, v in res.items() if k.startswith("SQ_")},
         "source": a.dir,
+        "lib_sha256": lib_sha,
+        "commit": a.commit or None,
     }
     s = json.dumps(out, indent=1)
     print(s)

@@ -1,0 +1,235 @@
+// Microbenchmark of one Gauss-Seidel level step (kernel B's velocity level loop) in isolation:
+// cycles per level step for several instruction forms, one wave per block, 1 block (a wave alone on
+// its SIMD) or 2048 blocks (2 waves per SIMD, the C5 shard's residency).
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -o tools/build/ubench_level tools/ubench_level.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void gsv(float2& va, float2& vb, float nx, float ny, float& ln, float& ltg, float mA,
+                                    float mB, float kmass, float friction) {
+  const float tx = ny, ty = -nx;
+  {
+    const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+    const float vt = dvx * tx + dvy * ty;
+    float lambda = kmass * (-vt);
+    const float maxf = friction * ln;
+    const float ni = __builtin_amdgcn_fmed3f(ltg + lambda, -maxf, maxf);
+    lambda = ni - ltg;
+    ltg = ni;
+    const float Px = lambda * tx, Py = lambda * ty;
+    va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+    vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+  }
+  {
+    const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+    const float vn = dvx * nx + dvy * ny;
+    float lambda = -kmass * vn;
+    const float ni = fmaxf(ln + lambda, 0.0f);
+    lambda = ni - ln;
+    ln = ni;
+    const float Px = lambda * nx, Py = lambda * ny;
+    va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+    vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+  }
+}
+
+// packed form: the same IEEE ops on (x, y) pairs
+__device__ __forceinline__ void gsv_pk(f2v& va, f2v& vb, f2v n, f2v t, float& ln, float& ltg, float mA,
+                                       float kmass, float friction) {
+  {
+    const f2v dv = vb - va;
+    const f2v pr = dv * t;
+    const float vt = pr.x + pr.y;
+    float lambda = kmass * (-vt);
+    const float maxf = friction * ln;
+    const float ni = __builtin_amdgcn_fmed3f(ltg + lambda, -maxf, maxf);
+    lambda = ni - ltg;
+    ltg = ni;
+    const f2v P = lambda * t;
+    const f2v mP = mA * P;
+    va = va - mP;
+    vb = vb + mP;
+  }
+  {
+    const f2v dv = vb - va;
+    const f2v pr = dv * n;
+    const float vn = pr.x + pr.y;
+    float lambda = -kmass * vn;
+    const float ni = fmaxf(ln + lambda, 0.0f);
+    lambda = ni - ln;
+    ln = ni;
+    const f2v P = lambda * n;
+    const f2v mP = mA * P;
+    va = va - mP;
+    vb = vb + mP;
+  }
+}
+
+template <int VAR>
+__global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev, int iters, float mA, float fr) {
+  __shared__ float2 s_v[1024 + 64];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 1024 + 64; i += 64) s_v[i] = make_float2(0.01f * i, -0.02f * i);
+  __syncthreads();
+  // two contacts per level: lanes 2l, 2l+1 at level l (disjoint bodies)
+  const int mylv = lane >> 1;
+  const int a = (lane * 7) & 1023, b = (lane * 7 + 3) & 1023;
+  const float nx = 0.6f, ny = 0.8f;
+  const float kmass = 1.0f / (mA + mA);
+  float ln = 0.1f * lane, lt = 0.01f;
+  float2* const pa0 = s_v + a;
+  float2* const pb0 = s_v + b;
+  float2* const pd = s_v + 1024 + lane;
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (VAR == 0) {  // kernel B's form: branch-free, dummy slots, addresses a step ahead
+      bool on = mylv == 0;
+      float2* pa = on ? pa0 : pd;
+      float2* pb = on ? pb0 : pd;
+      for (int lv = 0; lv < nlev; ++lv) {
+        float2 va = *pa, vb = *pb;
+        const bool onc = on;
+        on = mylv == lv + 1;
+        float2* const na = on ? pa0 : pd;
+        float2* const nb = on ? pb0 : pd;
+        float x = ln, y = lt;
+        gsv(va, vb, nx, ny, x, y, mA, mA, kmass, fr);
+        *pa = va;
+        *pb = vb;
+        ln = onc ? x : ln;
+        lt = onc ? y : lt;
+        pa = na;
+        pb = nb;
+        wave_lds_sync();
+      }
+    } else if constexpr (VAR == 1) {  // exec-masked branch per level
+      for (int lv = 0; lv < nlev; ++lv) {
+        if (mylv == lv) {
+          float2 va = *pa0, vb = *pb0;
+          gsv(va, vb, nx, ny, ln, lt, mA, mA, kmass, fr);
+          *pa0 = va;
+          *pb0 = vb;
+        }
+        wave_lds_sync();
+      }
+    } else if constexpr (VAR == 2) {  // packed math, branch-free
+      bool on = mylv == 0;
+      f2v* pa = (f2v*)(on ? pa0 : pd);
+      f2v* pb = (f2v*)(on ? pb0 : pd);
+      const f2v n = {nx, ny}, t = {ny, -nx};
+      for (int lv = 0; lv < nlev; ++lv) {
+        f2v va = *pa, vb = *pb;
+        const bool onc = on;
+        on = mylv == lv + 1;
+        f2v* const na = (f2v*)(on ? pa0 : pd);
+        f2v* const nb = (f2v*)(on ? pb0 : pd);
+        float x = ln, y = lt;
+        gsv_pk(va, vb, n, t, x, y, mA, kmass, fr);
+        *pa = va;
+        *pb = vb;
+        ln = onc ? x : ln;
+        lt = onc ? y : lt;
+        pa = na;
+        pb = nb;
+        wave_lds_sync();
+      }
+    } else if constexpr (VAR == 3) {  // the VALU chain alone (bodies in registers, no LDS)
+      float2 va = *pa0, vb = *pb0;
+      for (int lv = 0; lv < nlev; ++lv) {
+        const bool on = mylv == lv;
+        float x = ln, y = lt;
+        gsv(va, vb, nx, ny, x, y, mA, mA, kmass, fr);
+        ln = on ? x : ln;
+        lt = on ? y : lt;
+      }
+      *pa0 = va;
+      *pb0 = vb;
+    } else if constexpr (VAR == 4) {  // the LDS round trip alone (read, one add, write)
+      bool on = mylv == 0;
+      float2* pa = on ? pa0 : pd;
+      float2* pb = on ? pb0 : pd;
+      for (int lv = 0; lv < nlev; ++lv) {
+        float2 va = *pa, vb = *pb;
+        on = mylv == lv + 1;
+        float2* const na = on ? pa0 : pd;
+        float2* const nb = on ? pb0 : pd;
+        va.x += vb.y;
+        vb.x += va.y;
+        *pa = va;
+        *pb = vb;
+        pa = na;
+        pb = nb;
+        wave_lds_sync();
+      }
+    } else if constexpr (VAR == 5) {  // packed VALU chain alone
+      f2v va = *(f2v*)pa0, vb = *(f2v*)pb0;
+      const f2v n = {nx, ny}, t = {ny, -nx};
+      for (int lv = 0; lv < nlev; ++lv) {
+        const bool on = mylv == lv;
+        float x = ln, y = lt;
+        gsv_pk(va, vb, n, t, x, y, mA, kmass, fr);
+        ln = on ? x : ln;
+        lt = on ? y : lt;
+      }
+      *(f2v*)pa0 = va;
+      *(f2v*)pb0 = vb;
+    }
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  __syncthreads();
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+  out[blockIdx.x * 64 + lane] = s_v[lane] + make_float2(ln, lt);
+}
+
+template <int VAR>
+static void run(const char* name, int blocks, int nlev, int iters) {
+  float2* out;
+  long long* cyc;
+  hipMalloc(&out, sizeof(float2) * 64 * blocks);
+  hipMalloc(&cyc, sizeof(long long) * blocks);
+  lvl<VAR><<<blocks, 64>>>(out, cyc, nlev, iters, 1.2732395f, 0.3f);  // warm
+  hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  lvl<VAR><<<blocks, 64>>>(out, cyc, nlev, iters, 1.2732395f, 0.3f);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  std::vector<long long> h(blocks);
+  hipMemcpy(h.data(), cyc, sizeof(long long) * blocks, hipMemcpyDeviceToHost);
+  std::sort(h.begin(), h.end());
+  const double steps = (double)nlev * iters;
+  // s_memtime counts shader clocks; the event time gives the wall clock per step
+  printf("%-28s blocks %5d: median %7.1f cyc/step, max %7.1f cyc/step, wall %7.1f ns/step\n", name, blocks,
+         h[blocks / 2] / steps, h[blocks - 1] / steps, ms * 1e6 / steps);
+  hipFree(out);
+  hipFree(cyc);
+}
+
+int main() {
+  const int nlev = 32, iters = 400;
+  for (int blocks : {1, 2048, 4096}) {
+    run<0>("V0 branch-free (kernel B)", blocks, nlev, iters);
+    run<1>("V1 exec-masked branch", blocks, nlev, iters);
+    run<2>("V2 packed, branch-free", blocks, nlev, iters);
+    run<3>("V3 VALU chain only", blocks, nlev, iters);
+    run<5>("V5 packed VALU chain only", blocks, nlev, iters);
+    run<4>("V4 LDS round trip only", blocks, nlev, iters);
+  }
+  return 0;
+}
