@@ -394,6 +394,10 @@ def main():
                 "total_envs": args.total_envs if strong else E * world,
                 "split": (f"strong: {args.total_envs} envs over {world} ranks (this rank: global envs "
                           f"{e_off}..{e_off + E - 1})") if strong else f"weak: {E} envs per GPU",
+                # every rank's contiguous shard [first global env id, env count]: the counters above
+                # are their all-reduced totals
+                "shards": ([list(gdist.strong_split(args.total_envs, world, r)) for r in range(world)] if strong
+                           else [[gdist.env_offset(r, E), E] for r in range(world)]),
                 "parallelism": f"env-sharded x{world} (no data-path collective)"
                                + ("" if not launched else ", RCCL counters" if args.dist_backend == "nccl"
                                   else ", gloo counters (test mode)"),

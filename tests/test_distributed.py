@@ -99,3 +99,75 @@ def test_strong_split_partitions_the_job(total, world):
     np.testing.assert_array_equal(ids, np.arange(total))
     sizes = [n for _, n in parts]
     assert max(sizes) - min(sizes) <= 1
+
+
+TOTAL8, N8, STEPS8 = 29, 12, 12  # 29 envs over 8 ranks: shards of 4 4 4 4 4 3 3 3
+
+
+def _strong_actions():
+    rng = np.random.default_rng(11)
+    return rng.integers(0, 3, size=(STEPS8, TOTAL8, N8, 3)).astype(np.uint8)
+
+
+def _strong_worker(rank, world, port, outdir):
+    """bench.py --total-envs on `world` ranks, gloo: rank r steps only its contiguous shard
+    (gym_macm.dist.strong_split) with the whole job's actions, the counters all-reduced."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "gym-macm_amd"), os.path.join(repo, "oracle")]
+    import torch.distributed as dist
+    from gym_macm import dist as gdist
+    from gym_macm.settings import flockSettings, to_config
+    from oracle import OracleFlock
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, n = gdist.strong_split(TOTAL8, world, rank)
+    acts = _strong_actions()[:, off:off + n]
+    orc = OracleFlock(to_config(flockSettings(start_spread=6), N8, 1, obs_f64=True), None, n, SEED, off)
+    ctr = np.zeros(4, np.int64)
+    for t in range(STEPS8):
+        r = orc.step(acts[t])
+        ctr += gdist.step_counters(r["reward"], r["collided"], r["done"])
+    total = gdist.reduce_counters(ctr)
+    st = orc.get_state(64 * N8)
+    np.savez(os.path.join(outdir, f"strong{rank}.npz"), off=off, n=n, total=total, pos=st["pos"], vel=st["vel"],
+             count=st["contact_count"], ab=st["contact_ab"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_eight_rank_strong_split_matches_single_process(tmp_path):
+    """the strong split the driver's 8-GPU run uses (BASELINE C4: 4096 envs over 8,
+    C5: 16,384 over 8) at a reduced, uneven total on 8 gloo ranks: contiguous shards that cover every
+    global env once, every env's final state (positions, velocities, the ordered contact list) equal
+    to the single-process run of the whole job, and the all-reduced counters equal its totals."""
+    from gym_macm import dist as gdist
+    from gym_macm.settings import flockSettings, to_config
+    from oracle import OracleFlock
+
+    world = 8
+    mp.start_processes(_strong_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    full = OracleFlock(to_config(flockSettings(start_spread=6), N8, 1, obs_f64=True), None, TOTAL8, SEED, 0)
+    acts = _strong_actions()
+    ctr = np.zeros(4, np.int64)
+    for t in range(STEPS8):
+        r = full.step(acts[t])
+        ctr += gdist.step_counters(r["reward"], r["collided"], r["done"])
+    ref = full.get_state(64 * N8)
+    seen = []
+    for rank in range(world):
+        z = np.load(tmp_path / f"strong{rank}.npz")
+        off, n = int(z["off"]), int(z["n"])
+        assert (off, n) == gdist.strong_split(TOTAL8, world, rank)
+        seen += list(range(off, off + n))
+        np.testing.assert_array_equal(z["total"], ctr, err_msg=f"rank {rank} all-reduced counters")
+        for k, rk in (("pos", "pos"), ("vel", "vel"), ("count", "contact_count")):
+            np.testing.assert_array_equal(z[k], ref[rk][off:off + n], err_msg=f"rank {rank} {k}")
+        for e in range(n):
+            c = int(z["count"][e])
+            np.testing.assert_array_equal(z["ab"][e, :c], ref["contact_ab"][off + e, :c], err_msg=f"env {off + e}")
+    assert seen == list(range(TOTAL8))
+    assert ctr[0] == STEPS8 * TOTAL8 * N8 and ctr[1] > 0

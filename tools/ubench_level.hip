@@ -94,10 +94,11 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
   __syncthreads();
   const long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
-    if constexpr (VAR == 0) {  // kernel B's form: branch-free, dummy slots, addresses a step ahead
+    if constexpr (VAR == 0 || VAR == 9) {  // kernel B's form: branch-free, dummy slots, addresses a step ahead
       bool on = mylv == 0;
       float2* pa = on ? pa0 : pd;
       float2* pb = on ? pb0 : pd;
+#pragma unroll(VAR == 9 ? 2 : 1)
       for (int lv = 0; lv < nlev; ++lv) {
         float2 va = *pa, vb = *pb;
         const bool onc = on;
@@ -173,6 +174,50 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
         pb = nb;
         wave_lds_sync();
       }
+    } else if constexpr (VAR == 6) {  // packed math under an exec-masked branch per level
+      const f2v n = {nx, ny}, t = {ny, -nx};
+      for (int lv = 0; lv < nlev; ++lv) {
+        if (mylv == lv) {
+          f2v va = *(f2v*)pa0, vb = *(f2v*)pb0;
+          gsv_pk(va, vb, n, t, ln, lt, mA, kmass, fr);
+          *(f2v*)pa0 = va;
+          *(f2v*)pb0 = vb;
+        }
+        wave_lds_sync();
+      }
+    } else if constexpr (VAR == 7 || VAR == 8) {
+      // chain lanes: lanes 0, 1 hold a chain each (one contact per level); body a is the chain's
+      // (forwarded in registers from the lane's previous contact), body b comes from LDS: VAR 7
+      // prefetched one level ahead (issued before this level's writes), VAR 8 read at the step's
+      // start and waited for (an "X" level). Lanes >= 2 run the same instructions on dummy slots.
+      const bool chain = lane < 2;
+      float2* const pself = chain ? s_v + lane : pd;
+      float2 va = *pself;
+      const int cm = chain ? -1 : 0;  // branch-free: dummy lanes' b is their dummy slot
+      auto bbody = [&](int l) -> float2* {
+        const int idx = 2 + ((lane * 509 + l * 2 + (l & 1)) & 1021);
+        return s_v + ((idx & cm) | ((1024 + lane) & ~cm));
+      };
+      float2 vbn = *bbody(0);
+      __builtin_amdgcn_s_waitcnt(0);  // the loop's first step finds its operands in registers
+      for (int lv = 0; lv < nlev; ++lv) {
+        float2* const pb = bbody(lv);
+        float2 vb;
+        if constexpr (VAR == 7) {
+          vb = vbn;
+          vbn = *bbody(lv + 1);  // before this level's writes: valid for bodies not written now
+          __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to the step's end
+        } else {
+          vb = *pb;
+        }
+        float x = ln, y = lt;
+        gsv(va, vb, nx, ny, x, y, mA, mA, kmass, fr);
+        *pself = va;
+        *pb = vb;
+        ln = chain ? x : ln;
+        lt = chain ? y : lt;
+        if constexpr (VAR == 8) wave_lds_sync();
+      }
     } else if constexpr (VAR == 5) {  // packed VALU chain alone
       f2v va = *(f2v*)pa0, vb = *(f2v*)pb0;
       const f2v n = {nx, ny}, t = {ny, -nx};
@@ -227,6 +272,10 @@ int main() {
     run<0>("V0 branch-free (kernel B)", blocks, nlev, iters);
     run<1>("V1 exec-masked branch", blocks, nlev, iters);
     run<2>("V2 packed, branch-free", blocks, nlev, iters);
+    run<6>("V6 packed, exec-masked branch", blocks, nlev, iters);
+    run<9>("V9 = V0 unrolled x2", blocks, nlev, iters);
+    run<7>("V7 chain lanes, prefetched b", blocks, nlev, iters);
+    run<8>("V8 chain lanes, b read+wait", blocks, nlev, iters);
     run<3>("V3 VALU chain only", blocks, nlev, iters);
     run<5>("V5 packed VALU chain only", blocks, nlev, iters);
     run<4>("V4 LDS round trip only", blocks, nlev, iters);
