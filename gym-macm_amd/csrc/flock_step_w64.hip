@@ -96,6 +96,9 @@ constexpr bool kLevels = true;
 #ifndef MACM_BRANCHFREE_WAVE_LEVELS  // A/B knob: 0 = an exec-masked branch per level step (T <= 64 levels)
 #define MACM_BRANCHFREE_WAVE_LEVELS 1
 #endif
+#ifndef MACM_WAVE_LEVEL_UNROLL  // A/B knob: level steps per loop iteration in the one-slot level path (1, 2)
+#define MACM_WAVE_LEVEL_UNROLL 2
+#endif
 #ifndef MACM_BRANCHFREE_WAVE_POS  // A/B knob: 0 = exec-masked position level steps (T <= 64 levels)
 #define MACM_BRANCHFREE_WAVE_POS 1
 #endif
@@ -1368,16 +1371,14 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       const int mylvl = lhas ? lvl : -1;
       auto lpass = [&](auto warm) {
 #if MACM_WAVE_LEVEL_ADDR_AHEAD
-        // the next level's addresses are selected while this level solves (off the read's path)
-        bool on = mylvl == 0;
-        float2* pa = on ? pda : pdd;
-        float2* pb = on ? pdb : pdd;
-        for (int l = 0; l < dmulti; ++l) {
+        // the next level's addresses are selected while this level solves (off the read's path);
+        // two level steps per iteration (no register rotation or back-edge per level, as kernel B)
+        float2* pa = mylvl == 0 ? pda : pdd;
+        float2* pb = mylvl == 0 ? pdb : pdd;
+        auto step = [&](bool onc, bool onn) {
           const float2 vA0 = *pa, vB0 = *pb;
-          const bool onc = on;
-          on = mylvl == l + 1;
-          float2* const na = on ? pda : pdd;
-          float2* const nb = on ? pdb : pdd;
+          float2* const na = onn ? pda : pdd;
+          float2* const nb = onn ? pdb : pdd;
           float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
           float nl = lln, nt = llt;
           if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB);
@@ -1389,7 +1390,15 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           pa = na;
           pb = nb;
           level_sync();
+        };
+        int l = 0;
+#if MACM_WAVE_LEVEL_UNROLL == 2
+        for (; l + 1 < dmulti; l += 2) {
+          step(mylvl == l, mylvl == l + 1);
+          step(mylvl == l + 1, mylvl == l + 2);
         }
+#endif
+        for (; l < dmulti; ++l) step(mylvl == l, mylvl == l + 1);
 #else
         for (int l = 0; l < dmulti; ++l) {
           const bool on = mylvl == l;
@@ -1574,16 +1583,14 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           int* const pmd = reinterpret_cast<int*>(pdd);
           int* const pmi = lhas ? s_pmin + lisl : pmd;
 #if MACM_WAVE_LEVEL_ADDR_AHEAD
-          bool on = mylvl == 0;
-          float2* pa = on ? pda : pdd;
-          float2* pb = on ? pdb : pdd;
-          int* pm = on ? pmi : pmd;
-          for (int l = 0; l < dmulti; ++l) {
+          float2* pa = mylvl == 0 ? pda : pdd;
+          float2* pb = mylvl == 0 ? pdb : pdd;
+          int* pm = mylvl == 0 ? pmi : pmd;
+          auto pstep = [&](bool onn) {
             const float2 cA0 = *pa, cB0 = *pb;
-            on = mylvl == l + 1;
-            float2* const na = on ? pda : pdd;
-            float2* const nb = on ? pdb : pdd;
-            int* const nm = on ? pmi : pmd;
+            float2* const na = onn ? pda : pdd;
+            float2* const nb = onn ? pdb : pdd;
+            int* const nm = onn ? pmi : pmd;
             float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
             const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
             *pa = make_float2(cAx, cAy);
@@ -1595,7 +1602,15 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
             pb = nb;
             pm = nm;
             level_sync();
+          };
+          int l = 0;
+#if MACM_WAVE_LEVEL_UNROLL == 2
+          for (; l + 1 < dmulti; l += 2) {
+            pstep(mylvl == l + 1);
+            pstep(mylvl == l + 2);
           }
+#endif
+          for (; l < dmulti; ++l) pstep(mylvl == l + 1);
 #else
           for (int l = 0; l < dmulti; ++l) {
             const bool on = mylvl == l;

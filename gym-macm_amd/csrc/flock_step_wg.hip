@@ -71,6 +71,10 @@ constexpr bool kSolvePriority = false;
 constexpr bool kSolvePriority = true;
 #endif
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
+#ifndef MACM_DFS_BATCH  // A/B knob: contacts per lane whose loads flock_dfs_wg's record pass issues together
+#define MACM_DFS_BATCH 4
+#endif
+constexpr int kDfsBatch = MACM_DFS_BATCH;
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
 // block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
@@ -1192,9 +1196,21 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
 
   // ---- Gauss-Seidel levels: counting sort into level order; the records for kernel B ------------
   uint32_t* s_cnt = s_adj;  // [dmax + 1] over adj..stk (dead after the walk; dmax <= T <= tcap)
+  // Both passes over the walk's contacts take kDfsBatch of them per lane at a time, every global
+  // load of the batch issued before the first is used: a contact's record is a chain of dependent
+  // L2 reads (x_dfs -> x_adj -> x_tab -> pos), which one contact at a time left exposed
+  // (round 3: 0.53 M cycles per C5 env for the sort and the records)
+  constexpr int U = kDfsBatch;
   for (int l = lane; l <= dmax; l += W) s_cnt[l] = 0u;
   __syncthreads();
-  for (int k = lane; k < nord; k += W) atomicAdd(&s_cnt[xdfs[k] >> 16], 1u);
+  for (int k0 = 0; k0 < nord; k0 += U * W) {
+    uint32_t dl[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) dl[j] = xdfs[min(k0 + j * W + lane, nord - 1)];
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (k0 + j * W + lane < nord) atomicAdd(&s_cnt[dl[j] >> 16], 1u);
+  }
   __syncthreads();
   {  // exclusive scan over the levels: lane L owns levels [L per, (L + 1) per)
     const int per = (dmax + W - 1) / W;
@@ -1220,28 +1236,48 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   float2* xi = B.x_cimp + (size_t)e * tcap;
   uint16_t* xo = B.x_ord + (size_t)e * tcap;
   const float2* pos = B.pos + (size_t)e * N;
-  for (int k = lane; k < nord; k += W) {
-    const uint32_t d = xdfs[k];
-    const int t = xadj[d & 0xffffu] & 0xffffu, lv = d >> 16;  // CSR slot -> contact
-    const uint32_t ab = xt[t];
-    const int a = ab & 0xffffu, b = ab >> 16;
-    const float2 pa = pos[a], pb = pos[b];  // the start-of-step positions (kernel C writes them back)
-    float nx = 1.0f, ny = 0.0f;             // InitializeVelocityConstraints: (1, 0) when the centres coincide
-    const float ddx = pa.x - pb.x, ddy = pa.y - pb.y;
-    if (ddx * ddx + ddy * ddy > kEps * kEps) {
-      nx = pb.x - pa.x;
-      ny = pb.y - pa.y;
-      normalize(nx, ny);
+  for (int k0 = 0; k0 < nord; k0 += U * W) {
+    uint32_t dl[U], abl[U];
+    int tl[U];
+    float2 pal[U], pbl[U], laml[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) dl[j] = xdfs[min(k0 + j * W + lane, nord - 1)];
+#pragma unroll
+    for (int j = 0; j < U; ++j) tl[j] = xadj[dl[j] & 0xffffu] & 0xffffu;  // CSR slot -> contact
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      abl[j] = xt[tl[j]];
+      laml[j] = g_lam[tl[j]];
     }
-    int lo = 0, hi = nisl - 1;  // the island of contact k
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if ((int)s_ic[mid] <= k) lo = mid; else hi = mid - 1;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      pal[j] = pos[abl[j] & 0xffffu];  // the start-of-step positions (kernel C writes them back)
+      pbl[j] = pos[abl[j] >> 16];
     }
-    const int p = (int)atomicAdd(&s_cnt[lv], 1u);  // any slot of its level: a level's contacts share no body
-    xc[p] = make_float4(__uint_as_float(ab), nx, ny, __int_as_float((lv << 16) | lo));
-    xi[p] = g_lam[t];
-    xo[p] = (uint16_t)t;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int k = k0 + j * W + lane;
+      if (k >= nord) break;
+      const uint32_t ab = abl[j];
+      const int lv = dl[j] >> 16;
+      const float2 pa = pal[j], pb = pbl[j];
+      float nx = 1.0f, ny = 0.0f;  // InitializeVelocityConstraints: (1, 0) when the centres coincide
+      const float ddx = pa.x - pb.x, ddy = pa.y - pb.y;
+      if (ddx * ddx + ddy * ddy > kEps * kEps) {
+        nx = pb.x - pa.x;
+        ny = pb.y - pa.y;
+        normalize(nx, ny);
+      }
+      int lo = 0, hi = nisl - 1;  // the island of contact k
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)s_ic[mid] <= k) lo = mid; else hi = mid - 1;
+      }
+      const int p = (int)atomicAdd(&s_cnt[lv], 1u);  // any slot of its level: a level's contacts share no body
+      xc[p] = make_float4(__uint_as_float(ab), nx, ny, __int_as_float((lv << 16) | lo));
+      xi[p] = laml[j];
+      xo[p] = (uint16_t)tl[j];
+    }
   }
   for (int q = lane; q <= nisl; q += W) B.x_ic[(size_t)e * IS + q] = s_ic[q];
   if (lane == 0) {
@@ -1294,13 +1330,15 @@ __device__ __forceinline__ void gs_warm(float2& va, float2& vb, float nx, float 
 }
 
 // b2PositionSolverManifold + one position-constraint correction; returns the separation.
+// KPOS: K = mA + mB is known to be > 0 (else the impulse is 0, b2ContactSolver's K > 0 test).
+template <bool KPOS = false>
 __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radius, float mA, float mB) {
   float nx = cb.x - ca.x, ny = cb.y - ca.y;
   normalize(nx, ny);
   const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
   const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
   const float K = mA + mB;
-  const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
+  const float imp = KPOS ? div_by_invariant(-Cc, K) : K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
   const float Px = imp * nx, Py = imp * ny;
   ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
   cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
@@ -1309,11 +1347,6 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
 
 }  // namespace wg
 
-__device__ __forceinline__ int sep_key(float f) {  // order-preserving int of a float (atomicMin)
-  const int i = __float_as_int(f);
-  return i >= 0 ? i : (i ^ 0x7fffffff);
-}
-__device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0 ? k : (k ^ 0x7fffffff)); }
 
 // Kernel B: one wave per env solves all its islands together, level by level (kernel A's
 // Gauss-Seidel levels): a level's contacts touch disjoint bodies, so lanes solve them at once
@@ -1321,14 +1354,14 @@ __device__ __forceinline__ float sep_unkey(int k) { return __int_as_float(k >= 0
 // passes are Box2D's: warm start, vel_iters velocity passes, StoreImpulses, position
 // integration, up to pos_iters position passes with each island leaving after the first pass
 // whose minimum separation is >= -3 linearSlop.
-#ifndef MACM_LEVEL_ADDR_AHEAD  // A/B knob: 0 = select a level's LDS addresses at the start of its step
-#define MACM_LEVEL_ADDR_AHEAD 1
-#endif
-#ifndef MACM_BRANCHFREE_POS  // A/B knob: 0 = exec-masked position level steps in kernel B
-#define MACM_BRANCHFREE_POS 1
-#endif
-#ifndef MACM_BRANCHFREE_LEVELS  // A/B knob: 0 = an exec-masked branch per velocity level step
-#define MACM_BRANCHFREE_LEVELS 1
+//
+// A level step is one straight block: every lane runs it, the lanes outside the level on a dummy
+// LDS slot of their own (no exec-mask branch), the next level's addresses selected while this
+// level solves. Level steps are issue- and latency-bound (one wave per SIMD pair at C5:
+// tools/ubench_level.hip), so the loops run two levels per iteration (no register rotation or
+// back-edge per level) and the position passes keep no uniform K > 0 branch inside the loop.
+#ifndef MACM_LEVEL_UNROLL  // A/B knob: level steps per loop iteration (1 or 2)
+#define MACM_LEVEL_UNROLL 2
 #endif
 __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
@@ -1337,10 +1370,9 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   const int IS = wg_isl_stride(N);
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
-  int* s_mins = (int*)(s_c + N);              // [IS] per island: minimum separation of the pass (key)
+  float* s_mins = (float*)(s_c + N);          // [IS] per island: minimum separation of the pass
   uint8_t* s_done = (uint8_t*)s_mins + wg_solve_mins_bytes(N);  // [IS] per island: position-solved
   float2* s_dum = (float2*)s_mins;  // [W] the velocity passes' dummy slots (s_mins is set per position pass)
-  (void)s_dum;
   const size_t en = (size_t)e * N;
   const int nisl = B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
@@ -1400,6 +1432,32 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
     lv0 = __builtin_amdgcn_readfirstlane(mylv);
     lv1 = __builtin_amdgcn_readlane(mylv, last);
   };
+  // Steps levels lv0..lv1 of a chunk: step(lv, on) with the addresses it reads / writes chosen one
+  // step ahead by addr(on) (on: this lane's record is at that level); two steps per iteration
+  auto level_loop = [&](int lv0, int lv1, int mylv, auto&& step) {
+    bool on = mylv == lv0;
+    int lv = lv0;
+#if MACM_LEVEL_UNROLL == 2
+    for (; lv < lv1; lv += 2) {
+      step(lv, on, mylv == lv + 1);
+      level_sync();
+      step(lv + 1, mylv == lv + 1, mylv == lv + 2);
+      level_sync();
+      on = mylv == lv + 2;
+    }
+    if (lv == lv1) {
+      step(lv, on, false);
+      level_sync();
+    }
+#else
+    for (; lv <= lv1; ++lv) {
+      const bool nx = mylv == lv + 1;
+      step(lv, on, nx);
+      on = nx;
+      level_sync();
+    }
+#endif
+  };
 
   // Warm start and velocity passes. last: the final impulses go straight to list order (g_lam).
   // warm is a compile-time flag (BoolC-like): no branch inside a level step
@@ -1416,23 +1474,18 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       const uint32_t ab = __float_as_uint(cur.r.x);
       const int a = ab & 0xffffu, b = ab >> 16;
       float2 im = cur.m;
-#if MACM_BRANCHFREE_LEVELS
       // every lane runs every level step, the lanes outside the level on their own dummy slot (no
       // exec-mask branch per level); only the level's lanes keep their impulses
       float2* const pa0 = s_v + a;
       float2* const pb0 = s_v + b;
       float2* const pd = s_dum + lane;
-#if MACM_LEVEL_ADDR_AHEAD
-      // the next level's addresses are selected while this level solves (off the read's path)
-      bool on = mylv == lv0;
-      float2* pa = on ? pa0 : pd;
-      float2* pb = on ? pb0 : pd;
-      for (int lv = lv0; lv <= lv1; ++lv) {
+      float2* pa = mylv == lv0 ? pa0 : pd;
+      float2* pb = mylv == lv0 ? pb0 : pd;
+      level_loop(lv0, lv1, mylv, [&](int, bool onc, bool onn) {
         float2 va = *pa, vb = *pb;
-        const bool onc = on;
-        on = mylv == lv + 1;
-        float2* const na = on ? pa0 : pd;
-        float2* const nb = on ? pb0 : pd;
+        // the next level's addresses are selected while this level solves (off the read's path)
+        float2* const na = onn ? pa0 : pd;
+        float2* const nb = onn ? pb0 : pd;
         float lx = im.x, ly = im.y;
         if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB);
         else gs_velocity(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB, kmass, friction);
@@ -1442,36 +1495,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
         im.y = onc ? ly : im.y;
         pa = na;
         pb = nb;
-        level_sync();
-      }
-#else
-      for (int lv = lv0; lv <= lv1; ++lv) {
-        const bool on = mylv == lv;
-        float2* const pa = on ? pa0 : pd;
-        float2* const pb = on ? pb0 : pd;
-        float2 va = *pa, vb = *pb;
-        float lx = im.x, ly = im.y;
-        if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB);
-        else gs_velocity(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB, kmass, friction);
-        *pa = va;
-        *pb = vb;
-        im.x = on ? lx : im.x;
-        im.y = on ? ly : im.y;
-        level_sync();
-      }
-#endif
-#else
-      for (int lv = lv0; lv <= lv1; ++lv) {
-        if (mylv == lv) {
-          float2 va = s_v[a], vb = s_v[b];
-          if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB);
-          else gs_velocity(va, vb, cur.r.y, cur.r.z, im.x, im.y, mA, mB, kmass, friction);
-          s_v[a] = va;
-          s_v[b] = vb;
-        }
-        level_sync();
-      }
-#endif
+      });
       const int k = c * W + lane;
       if (!warm && k < nc) {
         if (last) g_lam[cur.o] = im;
@@ -1504,89 +1528,68 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   __syncthreads();
 
   // ---- position passes: every island not yet solved, level by level; an island is solved after
-  //      the first pass whose minimum separation (starting at 0) is >= -3 linearSlop ------------
-  for (int it = 0; it < P.pos_iters; ++it) {
-    for (int I = lane; I < nisl; I += W) s_mins[I] = sep_key(0.0f);
-    __syncthreads();
-    Slot cur, nxt;
-    if (nch > 0) load(0, cur);
-    wait_vm();
-    for (int c = 0; c < nch; ++c) {
-      load(c + 1, nxt);
-      int mylv, lv0, lv1;
-      chunk_levels(c, cur, mylv, lv0, lv1);
-      const int I = __float_as_int(cur.r.w) & 0xffff;
-      const uint32_t ab = __float_as_uint(cur.r.x);
-      const int a = ab & 0xffffu, b = ab >> 16;
-      const bool live = !s_done[I];
-#if MACM_BRANCHFREE_POS
-      // branch-free level steps as in the velocity passes; the dummy slots are in s_v (dead after
-      // the position integration), a dummy lane's minimum goes to its slot's first word
-      float2* const pdd = s_v + lane;
-      const int mylvp = live ? mylv : -1;
-      float2* const pca = s_c + a;
-      float2* const pcb = s_c + b;
-      int* const pmi = s_mins + I;
-#if MACM_LEVEL_ADDR_AHEAD
-      bool on = mylvp == lv0;
-      float2* pa = on ? pca : pdd;
-      float2* pb = on ? pcb : pdd;
-      int* pm = on ? pmi : reinterpret_cast<int*>(pdd);
-      for (int lv = lv0; lv <= lv1; ++lv) {
-        float2 ca = *pa, cb = *pb;
-        on = mylvp == lv + 1;
-        float2* const na = on ? pca : pdd;
-        float2* const nb = on ? pcb : pdd;
-        int* const nm = on ? pmi : reinterpret_cast<int*>(pdd);
-        const float sep = gs_position(ca, cb, P.radius, mA, mB);
-        *pa = ca;
-        *pb = cb;
-        atomicMin(pm, sep_key(sep));
-        pa = na;
-        pb = nb;
-        pm = nm;
-        level_sync();
-      }
-#else
-      for (int lv = lv0; lv <= lv1; ++lv) {
-        const bool on = mylvp == lv;
-        float2* const pa = on ? pca : pdd;
-        float2* const pb = on ? pcb : pdd;
-        int* const pm = on ? pmi : reinterpret_cast<int*>(pdd);
-        float2 ca = *pa, cb = *pb;
-        const float sep = gs_position(ca, cb, P.radius, mA, mB);
-        *pa = ca;
-        *pb = cb;
-        atomicMin(pm, sep_key(sep));
-        level_sync();
-      }
-#endif
-#else
-      for (int lv = lv0; lv <= lv1; ++lv) {
-        if (live && mylv == lv) {
-          float2 ca = s_c[a], cb = s_c[b];
-          const float sep = gs_position(ca, cb, P.radius, mA, mB);
-          s_c[a] = ca;
-          s_c[b] = cb;
-          atomicMin(&s_mins[I], sep_key(sep));
-        }
-        level_sync();
-      }
-#endif
+  //      the first pass whose minimum separation (starting at 0) is >= -3 linearSlop. The minimum
+  //      is an LDS float min (ds_min_f32): the separations are finite, a NaN one would be ignored
+  //      as by the order-preserving integer keys it replaces (round 3) ----------------------------
+  // K = mA + mB > 0 for every dynamic body (fill_body_params: a zero mass becomes 1); the K <= 0
+  // form (b2ContactSolver's `K > 0 ? -C / K : 0`) exists for an infinite density only and keeps
+  // the test out of the level step.
+  auto pos_passes = [&](auto kpos_c) {
+    constexpr bool kpos = decltype(kpos_c)::value;
+    for (int it = 0; it < P.pos_iters; ++it) {
+      for (int I = lane; I < nisl; I += W) s_mins[I] = 0.0f;
+      __syncthreads();
+      Slot cur, nxt;
+      if (nch > 0) load(0, cur);
       wait_vm();
-      cur = nxt;
+      for (int c = 0; c < nch; ++c) {
+        load(c + 1, nxt);
+        int mylv, lv0, lv1;
+        chunk_levels(c, cur, mylv, lv0, lv1);
+        const int I = __float_as_int(cur.r.w) & 0xffff;
+        const uint32_t ab = __float_as_uint(cur.r.x);
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const bool live = !s_done[I];
+        // branch-free level steps as in the velocity passes; the dummy slots are in s_v (dead after
+        // the position integration), a dummy lane's minimum goes to its slot's first word
+        float2* const pdd = s_v + lane;
+        const int mylvp = live ? mylv : -1;
+        float2* const pca = s_c + a;
+        float2* const pcb = s_c + b;
+        float* const pmi = s_mins + I;
+        float2* pa = mylvp == lv0 ? pca : pdd;
+        float2* pb = mylvp == lv0 ? pcb : pdd;
+        float* pm = mylvp == lv0 ? pmi : reinterpret_cast<float*>(pdd);
+        level_loop(lv0, lv1, mylvp, [&](int, bool, bool onn) {
+          float2 ca = *pa, cb = *pb;
+          float2* const na = onn ? pca : pdd;
+          float2* const nb = onn ? pcb : pdd;
+          float* const nm = onn ? pmi : reinterpret_cast<float*>(pdd);
+          const float sep = gs_position<kpos>(ca, cb, P.radius, mA, mB);
+          *pa = ca;
+          *pb = cb;
+          __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          pa = na;
+          pb = nb;
+          pm = nm;
+        });
+        wait_vm();
+        cur = nxt;
+      }
+      __syncthreads();
+      bool open = false;
+      for (int I = lane; I < nisl; I += W) {
+        if (s_done[I]) continue;
+        if (s_mins[I] >= -3.0f * kLinearSlop) s_done[I] = 1;
+        else open = true;
+      }
+      const bool any_open = __ballot(open) != 0ull;
+      __syncthreads();
+      if (!any_open) break;
     }
-    __syncthreads();
-    bool open = false;
-    for (int I = lane; I < nisl; I += W) {
-      if (s_done[I]) continue;
-      if (sep_unkey(s_mins[I]) >= -3.0f * kLinearSlop) s_done[I] = 1;
-      else open = true;
-    }
-    const bool any_open = __ballot(open) != 0ull;
-    __syncthreads();
-    if (!any_open) break;
-  }
+  };
+  if (mA + mB > 0.0f) pos_passes(std::true_type{});
+  else pos_passes(std::false_type{});
   uint8_t* isolv = B.x_isolv + (size_t)e * IS;
   for (int I = lane; I < nisl; I += W) isolv[I] = s_done[I];
   WSTAMP(15);

@@ -135,3 +135,104 @@ def test_c4_tdm_full_size_4096x2x16():
     check_contact_lists(s, N)
     for e in envs:
         assert_tdm_state_equal(env_slice(s, e, E), orcs[e].get_state(), f"env {e}")
+
+
+# ---- the thinly sampled configs, at their own batch sizes and launch forms ------------
+
+def sampled_oracles(cfg, tidx, envs, seed=SEED):
+    return {e: oracle_for(cfg, tidx, 1, seed, env_offset=e) for e in envs}
+
+
+def check_sampled_final(vec, orcs, last, E, ctx):
+    """Final state and last outputs of the sampled envs equal their lone oracle runs."""
+    s = vec.get_state()
+    check_contact_lists(s, vec.N)
+    obs, nbr, rew = vec.world.obs.cpu().numpy(), vec.world.nbr_id.cpu().numpy(), vec.world.reward.cpu().numpy()
+    coll = vec.world.collided.cpu().numpy()
+    for e, o in orcs.items():
+        assert_state_equal(env_slice(s, e, E), o.get_state(vec.world.C), f"{ctx} env {e}")
+        r = last[e]
+        np.testing.assert_array_equal(rew[e:e + 1], r["reward"].astype(np.float32), err_msg=f"{ctx} rew env {e}")
+        np.testing.assert_array_equal(nbr[e:e + 1], r["nbr_id"], err_msg=f"{ctx} nbr env {e}")
+        np.testing.assert_array_equal(coll[e:e + 1], r["collided"], err_msg=f"{ctx} coll env {e}")
+        f32_obs_mismatch(obs[e:e + 1], r["obs"])
+
+
+def test_c5_shard_driver_launch_form_2048x1024():
+    """The C5 shard as bench.py launches it: a W = 2 step rollout from reset, then a 30-step rollout
+    (macm_world_rollout: kernel A, the dense envs' DFS kernel, the level solver and kernel C per
+    step), against the lone oracle runs of 6 sampled envs over all 32 steps from reset."""
+    E, N, W, K = 2048, 1024, 2, 30
+    vec = FlockVec(E, n_agents=[N], seed=SEED, device="cuda:0")
+    cfg = to_config(flockSettings(), N, 1, obs_f64=True)
+    rng = np.random.default_rng(55)
+    envs = sample_envs(E, rng, 2)
+    assert len(envs) >= 4
+    orcs = sampled_oracles(cfg, vec.targets_idx, envs)
+    acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device="cuda:0",
+                         generator=torch.Generator(device="cuda:0").manual_seed(7))
+    vec.world.rollout(acts[:W].contiguous())
+    vec.world.reset_counters()
+    vec.world.rollout(acts[W:].contiguous())
+    a = acts.cpu().numpy()
+    last = {}
+    for e, o in orcs.items():
+        for k in range(W + K):
+            last[e] = o.step(a[k, e:e + 1])
+    assert vec.status() == 0 and int(vec.counters()[0]) == E * N * K
+    check_sampled_final(vec, orcs, last, E, "C5 driver form")
+
+
+@pytest.mark.parametrize("launch", ["step", "rollout"])
+def test_c2_full_size_1024x64(launch):
+    """C2 (cm-flock-v0, 64 agents x 1024 envs) at its own batch size: below the scalar-sweep
+    threshold, so the packed-sweep instantiations run (env_step_w64 / env_rollout_w64<0, 64,
+    float, false>); 8 sampled envs against their lone oracle runs over 60 steps from reset."""
+    E, N, K = 1024, 64, 60
+    if launch == "step":
+        flock_full(E, N, K, n_sample=4)
+        return
+    vec = FlockVec(E, n_agents=[N], seed=SEED, device="cuda:0")
+    cfg = to_config(flockSettings(), N, 1, obs_f64=True)
+    rng = np.random.default_rng(21)
+    envs = sample_envs(E, rng, 4)
+    orcs = sampled_oracles(cfg, vec.targets_idx, envs)
+    a = rng.integers(0, 3, size=(K, E, N, 3)).astype(np.uint8)
+    vec.world.rollout(torch.from_numpy(a).cuda())
+    last = {e: None for e in envs}
+    for e, o in orcs.items():
+        for k in range(K):
+            last[e] = o.step(a[k, e:e + 1])
+    assert vec.status() == 0 and int(vec.counters()[0]) == E * N * K
+    check_sampled_final(vec, orcs, last, E, "C2 rollout")
+
+
+def test_c3_closed_loop_bots_full_size_4096x256():
+    """C3 (256 agents, 4 flocks, 4096 envs) in the closed loop with the device bots.flock (the
+    workgroup path, per-step launches and the bot kernel, in env slices) for 150 steps from reset:
+    6 sampled envs against the oracle driven by the reference bot (test_scripts/bots.py:37-61) on
+    its own observations rounded to the world's float32, final state and the bot's next actions."""
+    from gym_macm.bots import flock_actions
+    from parity import flock_bot
+    E, N, K = 4096, 256, 150
+    tg = [i // 64 for i in range(N)]
+    vec = FlockVec(E, n_agents=[N], targets=tg, seed=SEED, device="cuda:0", max_contacts=4096)
+    cfg = to_config(flockSettings(), N, vec.n_targets, obs_f64=True)
+    rng = np.random.default_rng(31)
+    envs = sample_envs(E, rng, 2)
+    orcs = sampled_oracles(cfg, vec.targets_idx, envs)
+    loop = flock_actions(vec.obs)
+    vec.world.rollout_bots(loop, K)
+    torch.cuda.synchronize()
+    last = {}
+    for e, o in orcs.items():
+        obs, _ = o.observe()
+        for k in range(K):
+            last[e] = o.step(flock_bot(obs.astype(np.float32).astype(np.float64)))
+            obs = last[e]["obs"]
+    assert vec.status() == 0 and int(vec.counters()[0]) == E * N * K
+    check_sampled_final(vec, orcs, last, E, "C3 closed loop")
+    nxt = loop.cpu().numpy()
+    for e in envs:
+        np.testing.assert_array_equal(nxt[e:e + 1], flock_bot(last[e]["obs"].astype(np.float32).astype(np.float64)),
+                                      err_msg=f"the bot's next actions, env {e}")
