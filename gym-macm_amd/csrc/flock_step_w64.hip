@@ -111,6 +111,11 @@ constexpr bool kLevels = true;
 // TDM obs through the staged writer (tdm_obs.hpp): whole-line stores, 709 B per agent-step of HBM
 // traffic instead of 864, but C4 34.1 us per step instead of 28.2 (profiles/r03/abtests/tdm_obs/):
 // off, the pair tiles stay (A/B knob)
+#ifdef MACM_NO_TDM_MASK_STAGED  // A/B knob: the pair tiles write the mask bytes straight to HBM
+constexpr bool kTdmMaskStaged = false;
+#else
+constexpr bool kTdmMaskStaged = true;
+#endif
 #ifdef MACM_TDM_OBS_STAGED
 constexpr bool kTdmObsStaged = true;
 #else
@@ -1938,7 +1943,12 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       if (staged)
         tdm_obs_staged<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<unsigned char*>(&s_pool));
     }
-    if (!staged) MACM_TDM_OBS<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang);
+    if (!staged) {
+      if (kTdmMaskStaged && N * (N - 1) <= (int)sizeof(Pool))  // the contact arrays are dead here
+        tdm_obs_pairs_smask<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<uint8_t*>(&s_pool));
+      else
+        MACM_TDM_OBS<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang);
+    }
   }
   STAMP(12);
 

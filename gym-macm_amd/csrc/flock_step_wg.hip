@@ -75,6 +75,10 @@ constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
 #define MACM_DFS_BATCH 4
 #endif
 constexpr int kDfsBatch = MACM_DFS_BATCH;
+#ifndef MACM_DFS_PREFETCH  // A/B knob: flock_dfs_wg reads the next stack entry ahead (1) or at its pop (0)
+#define MACM_DFS_PREFETCH 0
+#endif
+constexpr bool kDfsPrefetch = MACM_DFS_PREFETCH != 0;
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
 // block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
@@ -339,7 +343,7 @@ __host__ __device__ inline WgLayoutA wg_layout_a(int N, int tcap) {
 }
 
 struct WgLayoutC {
-  int slp, flags, oldc, scan, misc, fn, fo, c, gred, gpar, gstart, gent, pk, bjv, total;
+  int slp, flags, oldc, scan, misc, fn, fo, c, gred, gpar, gstart, gsext, gent, pk, bjv, total;
 };
 __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
   WgLayoutC L;
@@ -360,6 +364,7 @@ __host__ __device__ inline WgLayoutC wg_layout_c(int N) {
   L.gred = take(4 * 4 * 16);
   L.gpar = take(4 * 8);
   L.gstart = take(4 * (grid::buckets(N) + 1) > 2 * N + 4 ? 4 * (grid::buckets(N) + 1) : 2 * N + 4);
+  L.gsext = take(4 * grid::buckets(N));
   L.gent = take(16 * N);
   L.pk = take(4 * N);   // per body: collided bit 31 | new-pair count (sweep)
   L.bjv = take(2 * N);  // per body: nearest neighbour (sweep); then new-pair segment starts
@@ -1110,6 +1115,11 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
     int sp = 1;
     int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;  // the last push of the previous pop
     __builtin_amdgcn_wave_barrier();
+    // The stack entry below the top, with its CSR range and level, read while the popped body is
+    // processed: when that body pushes nothing (common in dense worlds), the next pop finds them
+    // in registers instead of two dependent LDS round trips. Its level is refreshed from the lane
+    // that gives it a new contact in between (the only writer of s_last[that body]).
+    int pf_b = -1, pf_e0 = 0, pf_e1 = 0, pf_last = 0;
     while (sp > 0) {
       int bdy, e0, e1, xcur;
       --sp;
@@ -1118,6 +1128,11 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         e0 = top_e0;
         e1 = top_e1;
         xcur = top_last;
+      } else if (pf_b >= 0) {
+        bdy = pf_b;
+        e0 = pf_e0;
+        e1 = pf_e1;
+        xcur = pf_last;
       } else {
         bdy = s_stk[sp];
         e0 = s_off[bdy];
@@ -1125,9 +1140,17 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         xcur = s_last[bdy];
       }
       top_b = -1;
+      pf_b = -1;
+      if (kDfsPrefetch && sp > 0) {
+        pf_b = s_stk[sp - 1];
+        pf_e0 = s_off[pf_b];
+        pf_e1 = s_off[pf_b + 1];
+        pf_last = s_last[pf_b];
+      }
       if (lane == 0) {
         xibod[nb] = (uint16_t)bdy;
-        s_pop[bdy >> 6] |= 1ull << (bdy & 63);  // read by later pops only (no contact joins bdy to itself)
+        // read by later pops only (no contact joins bdy to itself): no wait for the old word
+        __hip_atomic_fetch_or(&s_pop[bdy >> 6], 1ull << (bdy & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       }
       ++nb;
       // levels of the new contacts c_1..c_m of bdy in order: X_i = i + max(X_0, max_{j<=i}(y_j - j + 1))
@@ -1163,6 +1186,10 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         const int mnew = __popcll(mc);
         if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
         nord += mnew;
+        if (kDfsPrefetch) {  // the prefetched entry just got a new contact: its level is xi
+          const unsigned long long mf = __ballot(newc && o == pf_b);
+          if (mf) pf_last = __builtin_amdgcn_readlane(xi, __ffsll((long long)mf) - 1);
+        }
         const unsigned long long mp = __ballot(push);
         if (push) {
           atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
@@ -1737,13 +1764,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   //      neighbour. Candidates of a body are the bodies of the 3 x 3 cell block around it; an env
   //      whose positions or extents the hash cannot bin takes the all-pairs sweep.
   const grid::Lds G{(float*)(lds + L.gred), (float*)(lds + L.gpar), (uint32_t*)(lds + L.gstart),
-                    (float4*)(lds + L.gent), grid::buckets(N)};
+                    (float4*)(lds + L.gent), (uint32_t*)(lds + L.gsext), grid::buckets(N)};
   bool coll = act && ((s_oldc[tid >> 5] >> (tid & 31)) & 1u);
   int newcnt = 0;
   float best = __builtin_inff();
   int bj = tid == 0 ? 1 : 0;
-  // strip cells from N = 512 (at C5's 1024 they halve the candidates and match the all-pairs
-  // sweep's time; at 256 the all-pairs sweep is 15% faster: DESIGN.md §3)
+  // strip cells from N = 256 (grid::kCellsMinAgents): with per-strip extent pruning (round 4) they
+  // walk ~290 of C5's 1024 bodies per body and beat the all-pairs sweep at C3 too
 #ifdef MACM_AB_ALL_PAIRS
   const bool cells = false;
 #else
@@ -1755,41 +1782,62 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   // strips [s0, s1], walked with broadcast reads. Results go to LDS per body (s_pk: collided bit
   // 31 | new-pair count, s_slp: best d2, s_bjv: neighbour), read back by the owning thread.
   int ti = 0, ts0 = 1, ts1 = 0;
+  bool ti_over = false;  // the swept body (ti) has more new partners than np2 holds
+  uint32_t np2 = 0u;     // this thread's body's last two new partners (cells path)
   if (gok) {
     const float4 E = act ? G.ent[tid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int i = __float_as_int(E.z);
     const float px = E.x, py = E.y;
     const float4 fni = s_fn[i], foi = s_fo[i];
-    int s0, s1;
-    grid::tile(G, act, px, s0, s1);
+    grid::Tile T;
+    grid::tile(G, act, px, fmaxf(fmaxf(px - fni.x, fni.z - px), 0.0f), T);
     ti = i;
-    ts0 = s0;
-    ts1 = s1;
+    ts0 = T.s0;
+    ts1 = T.s1;
     float bst = __builtin_inff();
     int bjj = i == 0 ? 1 : 0;
     bool col = false;
     int nc = 0;
-    const int q0 = s0 <= s1 ? (int)G.start[s0] : 0, q1 = s0 <= s1 ? (int)G.start[s1 + 1] : 0;
-    for (int q = q0; q < q1; ++q) {
-      const float4 Eq = G.ent[q];
-      const int j = __float_as_int(Eq.z);
-      const bool ovn = !(sep_max(fni, s_fn[j]) > 0.0f);
-      const float dx = Eq.x - px, dy = Eq.y - py;
-      const bool other = j != i;
-      if (other) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
-      col |= other && ovn;
-      if (j > i && ovn && sep_max(foi, s_fo[j]) > 0.0f) ++nc;
+    np2 = 0u;  // the last two new partners j > i, 10 bits each (most bodies have none)
+#ifdef MACM_STAMPS
+    int ncand = 0;
+#endif
+    // the walked strips in runs of consecutive strips (a run is one range of sorted entries)
+    for (int b = 0; 64 * b <= T.s1 - T.s0; ++b) {
+      unsigned long long m = grid::batch(G, T, b);
+      while (m) {
+        const int a = __ffsll((long long)m) - 1;
+        const unsigned long long rest = ~(m >> a);  // the run ends at the first 0 bit from a
+        const int len = rest == 0ull ? 64 - a : __ffsll((long long)rest) - 1;
+        m = (a + len >= 64) ? 0ull : (m & ~((1ull << (a + len)) - 1ull));
+        const int sa = T.s0 + 64 * b + a;
+        const int q0 = (int)G.start[sa], q1 = (int)G.start[sa + len];
+#ifdef MACM_STAMPS
+        ncand += q1 - q0;
+#endif
+        for (int q = q0; q < q1; ++q) {
+          const float4 Eq = G.ent[q];
+          const int j = __float_as_int(Eq.z);
+          const bool ovn = !(sep_max(fni, s_fn[j]) > 0.0f);
+          const float dx = Eq.x - px, dy = Eq.y - py;
+          const bool other = j != i;
+          if (other) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
+          col |= other && ovn;
+          const bool nw = j > i && ovn && sep_max(foi, s_fo[j]) > 0.0f;
+          np2 = nw ? (np2 << 10) | (uint32_t)j : np2;
+          nc += nw ? 1 : 0;
+        }
+      }
     }
-    // nearest neighbours the tile cannot certify: the wave walks the other strips for them
-    const bool need = act && !grid::certified(G, px, s0, s1, bst);
+    // nearest neighbours the walked strips cannot certify (a body outside the core [c0, c1] may be
+    // nearer): the wave walks every entry for them (the ones already seen change nothing)
+    const bool need = act && !grid::certified(G, px, T.c0, T.c1, bst);
     if (__ballot(need)) {
 #ifdef MACM_STAMPS
       if (need) atomicAdd(&s_misc[3], 1);
 #endif
       const int qn = (int)G.start[G.H];
       for (int q = 0; q < qn; ++q) {
-        if (q == q0) q = q1;
-        if (q >= qn) break;
         const float4 Eq = G.ent[q];
         const int j = __float_as_int(Eq.z);
         const float dx = Eq.x - px, dy = Eq.y - py;
@@ -1797,18 +1845,21 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       }
     }
 #ifdef MACM_STAMPS
-    if (act) atomicAdd(&s_misc[2], q1 - q0);
+    if (act) atomicAdd(&s_misc[2], ncand);
 #endif
     if (act) {
       s_slp[i] = bst;
       s_bjv[i] = (uint16_t)bjj;
-      s_pk[i] = (col ? 0x80000000u : 0u) | (uint32_t)nc;
+      // collided bit 31 | new-pair count (11 bits, <= N - 1) | the last two new partners
+      s_pk[i] = (col ? 0x80000000u : 0u) | ((uint32_t)nc << 20) | (np2 & 0xfffffu);
     }
+    ti_over = act && nc > 2;
     __syncthreads();
     if (act) {
       const uint32_t pk = s_pk[tid];
       coll |= (pk >> 31) != 0;
-      newcnt = (int)(pk & 0x7fffffffu);
+      newcnt = (int)((pk >> 20) & 0x7ffu);
+      np2 = pk & 0xfffffu;
       best = s_slp[tid];
       bj = s_bjv[tid];
     }
@@ -1856,24 +1907,40 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   int excl;
   const int nnew = block_scan_excl(newcnt, excl, s_scan);
   if (gok && nnew <= 2 * N) {
-    // The partners again, same mapping and tiles, into each body's segment of an LDS scratch
-    // (the dead sleep-clock array: 2N u16 slots; s_bjv holds the segment starts), then each
-    // owner sorts its segment descending and writes it out.
+    // Bodies with one or two new partners have them in np2 (the sweep kept them). For the rare
+    // body with more, its wave walks its tile again (same mapping), collecting the partners into
+    // the body's segment of an LDS scratch (the dead sleep-clock array: 2N u16 slots; s_bjv holds
+    // the segment starts), which the owner sorts descending. About 50 of a C5 env's 1024 bodies get
+    // a new pair per step, and a body with more than two is a few per step: the walk of every wave
+    // (round 3) was 28% of kernel C at C5.
     uint16_t* s_np = (uint16_t*)s_slp;
     if (act) s_bjv[tid] = (uint16_t)excl;
     __syncthreads();
-    {
+    if (__ballot(ti_over)) {
       const int i = ti;
       const float4 fni = s_fn[i], foi = s_fo[i];
       const int q0 = ts0 <= ts1 ? (int)G.start[ts0] : 0, q1 = ts0 <= ts1 ? (int)G.start[ts1 + 1] : 0;
-      int w = act ? (int)s_bjv[i] : 0;
+      int w = ti_over ? (int)s_bjv[i] : 0;
       for (int q = q0; q < q1; ++q) {
         const int j = __float_as_int(G.ent[q].z);
-        if (j > i && !(sep_max(fni, s_fn[j]) > 0.0f) && sep_max(foi, s_fo[j]) > 0.0f) s_np[w++] = (uint16_t)j;
+        if (ti_over && j > i && !(sep_max(fni, s_fn[j]) > 0.0f) && sep_max(foi, s_fo[j]) > 0.0f)
+          s_np[w++] = (uint16_t)j;
       }
     }
     __syncthreads();
-    if (act && newcnt > 0) {
+    if (act && newcnt > 0 && newcnt <= 2) {  // from np2, descending
+      const uint32_t pa = np2 & 0x3ffu, pb = (np2 >> 10) & 0x3ffu;
+      const uint32_t hi = newcnt == 1 ? pa : max(pa, pb), lo = min(pa, pb);
+      const int w = nnew - excl - newcnt;
+      if (w < C) {
+        ocab[w] = (uint32_t)tid | (hi << 16);
+        ocimp[w] = make_float2(0.0f, 0.0f);
+      }
+      if (newcnt == 2 && w + 1 < C) {
+        ocab[w + 1] = (uint32_t)tid | (lo << 16);
+        ocimp[w + 1] = make_float2(0.0f, 0.0f);
+      }
+    } else if (act && newcnt > 2) {
       uint16_t* seg = s_np + excl;
       for (int a = 1; a < newcnt; ++a) {  // insertion sort, descending
         const uint16_t x = seg[a];

@@ -165,6 +165,26 @@ __device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __r
   }
 }
 
+// The pair tiles with the mask staged in LDS (stage: N (N - 1) bytes, the dead contact arrays) and
+// written out as whole 16-B pieces after the tiles: the tiles' 8-byte mask runs left most of the
+// env's mask lines partly written, so L2 wrote them back piece by piece (round 3 PMC: ~25 MB of HBM
+// writes per C4 step above the algorithmic bytes). The obs slots are the pair tiles'.
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_pairs_smask(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N,
+                                                    int lane, unsigned long long livem, const TdmParams& TP,
+                                                    const float2* sc, const float* sa, uint8_t* stage) {
+  tdm_obs_pairs<OT>(obs, mask ? stage : nullptr, N, lane, livem, TP, sc, sa);
+  if (!mask) return;
+  wave_lds_sync();  // the stage's bytes (written by other lanes) before the copy reads them
+  const int nb = N * (N - 1);
+  if ((nb & 15) == 0) {  // 16-B pieces (N = 32: 62 lanes, one store instruction)
+    for (int k = lane; 16 * k < nb; k += 64)
+      reinterpret_cast<uint4*>(mask)[k] = reinterpret_cast<const uint4*>(stage)[k];
+  } else {  // 64 consecutive bytes per store instruction
+    for (int k = lane; k < nb; k += 64) mask[k] = stage[k];
+  }
+}
+
 // The same slots in memory order: lane q of each pass writes slot q of the env's [N, N-1] block,
 // so one store instruction covers 64 consecutive slots (1 KB: whole 128-B lines; an env's block is
 // N (N-1) 16 B, a multiple of 128 B for N = 32) and the mask 64 consecutive bytes. Each slot
