@@ -28,6 +28,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--spin", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) first")
+    ap.add_argument("--bench-like", action="store_true",
+                    help="between the warm-up and the timed launch, the calls bench.py makes (counter reset, "
+                         "spill-count read, a second synchronize)")
     a = ap.parse_args()
     if a.spin:
         ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL).hipSetDeviceFlags(1)
@@ -45,6 +48,10 @@ def main():
         vec.reset()
         w.rollout_raw(base, W, sh)
         torch.cuda.synchronize(dev)
+        if a.bench_like:
+            w.reset_counters()
+            w.spilled()
+            torch.cuda.synchronize(dev)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
@@ -60,7 +67,8 @@ def main():
                              kernel=ev0.elapsed_time(ev1) * 1e-3))
     med = {k: float(np.median([x[k] for x in rows])) * 1e6 for k in rows[0]}
     med["gap"] = med["total"] - med["kernel"]
-    print(json.dumps({"us_median": {k: round(v, 2) for k, v in med.items()}, "spin": a.spin, "reps": a.reps}))
+    print(json.dumps({"us_median": {k: round(v, 2) for k, v in med.items()}, "spin": a.spin,
+                      "bench_like": a.bench_like, "reps": a.reps}))
 
 
 if __name__ == "__main__":
