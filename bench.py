@@ -288,10 +288,13 @@ def main():
         if args.env == "flock":
             world_h.reset_counters()
         spilled0 = world_h.spilled()
+        # the events are created (lazily, at their first record) before the timed region
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        ev1.record(stream)
         if launched:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
         if roll and args.policy == "bots":
