@@ -248,7 +248,29 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Inclusive prefix maximum over the 64 lanes of a wave in lane order, by DPP row shifts and row
 // broadcasts (no LDS crossbar round trips). Values must be > -2^30 (the identity used).
+// The whole wave must be active. Each step is one v_max_i32 with a DPP source: a lane whose source
+// is out of its row (no bound_ctrl) or outside the row mask is not written and keeps its own value,
+// which is the maximum's identity there. The compiler does not fold update_dpp into the max (it
+// emits a mov_dpp, an identity mov and the max per step: 24 instructions against 12).
+// -DMACM_NO_DPP_ASM: the builtin form.
 __device__ __forceinline__ int wave_prefix_max(int v) {
+#ifndef MACM_NO_DPP_ASM
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(v));
+  return v;
+#endif
   constexpr int kId = -0x40000000;
   v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));  // row_shr:1
   v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));  // row_shr:2

@@ -18,6 +18,7 @@
 // contacts exceed kernel A's LDS capacity is stepped whole by the spill step
 // (flock_spill.hpp) inside kernel A, and B and C skip it.
 #include <map>
+#include <type_traits>
 #include <mutex>
 
 #include "flock_common.hpp"
@@ -75,10 +76,6 @@ constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
 #define MACM_DFS_BATCH 4
 #endif
 constexpr int kDfsBatch = MACM_DFS_BATCH;
-#ifndef MACM_DFS_PREFETCH  // A/B knob: flock_dfs_wg reads the next stack entry ahead (1) or at its pop (0)
-#define MACM_DFS_PREFETCH 0
-#endif
-constexpr bool kDfsPrefetch = MACM_DFS_PREFETCH != 0;
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
 // block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
@@ -314,8 +311,16 @@ __global__ __launch_bounds__(1024) void flock_observe_wg(StepParams P, WorldBuff
 //                        write-back.
 // Every arithmetic operation and its order are those of the wave kernel and the spill step.
 
+// Up to this many agents kernel A keeps each CSR edge's other body next to it (s_oth, 4 B per
+// touching contact), so an island walk reads an edge and its other body in one LDS round trip
+// instead of two (edge, then the contact's pair). Above it (78 KB of LDS at N = 1024, two blocks
+// per CU) the walks read the pair.
+#ifndef MACM_OTH_MAX_AGENTS  // A/B knob
+#define MACM_OTH_MAX_AGENTS 512
+#endif
+constexpr int kOthMaxAgents = MACM_OTH_MAX_AGENTS;
 struct WgLayoutA {
-  int c, deg, csr_off, todo, ord, ib, ibod, stk, ic, scan, misc, tab, adj, total;
+  int c, deg, csr_off, todo, ord, ib, ibod, stk, ic, scan, misc, tab, adj, oth, total;
 };
 __host__ __device__ inline WgLayoutA wg_layout_a(int N, int tcap) {
   WgLayoutA L;
@@ -332,12 +337,13 @@ __host__ __device__ inline WgLayoutA wg_layout_a(int N, int tcap) {
   L.ord = take(2 * tcap);
   L.ib = take(2 * (N / 2 + 2));
   L.ibod = take(2 * N);
-  L.stk = take(2 * N);
+  L.stk = take(2 * (N + 16));  // the walks' stacks, then a dummy slot per wave
   L.ic = take(2 * (N / 2 + 2));
   L.scan = take(4 * 32);
   L.misc = take(4 * 8);
   L.tab = take(4 * tcap);
   L.adj = take(6 * tcap + 8);  // CSR edges (2 tcap u16), then level counts (tcap + 1 u32); levels (tcap u16) at 4 tcap + 8
+  L.oth = N <= kOthMaxAgents ? take(4 * tcap) : -1;  // [2 tcap] the other body of CSR edge q
   L.total = o;
   return L;
 }
@@ -545,6 +551,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   // contact, in island order, that touches body b (0 = none). s_deg is free from here on.
   uint16_t* s_last = s_deg;
   uint16_t* s_lvl = (uint16_t*)(lds + L.adj + 4 * tcap + 8);  // [tcap] level of island-ordered contact k
+  uint16_t* s_oth = L.oth >= 0 ? (uint16_t*)(lds + L.oth) : nullptr;
   if (act) s_last[tid] = 0;
   if (act && deg > 1) {
     const int o0 = s_off[tid];
@@ -558,6 +565,11 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       s_adj[y + 1] = key;
     }
   }
+  if (s_oth && act)
+    for (int q = s_off[tid], q1 = q + deg; q < q1; ++q) {
+      const uint32_t ab = s_tab[s_adj[q]];
+      s_oth[q] = (uint16_t)((int)(ab & 0xffffu) == tid ? ab >> 16 : ab & 0xffffu);
+    }
   __syncthreads();
   WSTAMP(19);
 
@@ -599,20 +611,40 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 #endif
     return;
   }
-  // One island walked by a whole wave from seed sd (its todo bit already cleared): a popped
-  // body's edges one per lane, levels by a prefix maximum (below). Appends to s_ord / s_lvl at
-  // nord and s_ibod at nb; the stack lives at s_stk[sbase...]. Every lane of the wave calls it.
-  auto par_walk = [&](int sd, int& nord, int& nb, int sbase, int& dmax) {
+  // Walk state per body in s_last: bits 0..13 = 1 + the level of the last walked contact touching
+  // it (levels <= tcap < 2^14), bit 15 = pushed, bit 14 = popped. One LDS read of an edge's other
+  // body gives everything the edge needs: the contact was walked iff the other body was popped (the
+  // first of its two bodies to be popped walks it), the body is pushed iff it was not pushed yet,
+  // and the level chain's input. A new contact's other body is pushed by then either way, so the
+  // walk writes its word as level | pushed; a pop ends with level | pushed | popped. An edge's other
+  // body comes from s_oth (N <= kOthMaxAgents; one read next to the edge's own) or from the
+  // contact's pair. No todo bits or visited flags are written.
+  constexpr int kPushed = 0x8000, kPopped = 0x4000, kLvl = 0x3fff;
+  auto edge_other = [&](auto HO, int q, int t, int bdy) -> int {
+    if constexpr (decltype(HO)::value) {
+      (void)t;
+      (void)bdy;
+      return s_oth[q];
+    } else {
+      (void)q;
+      const uint32_t ab = s_tab[t];
+      const int a = ab & 0xffffu;
+      return a == bdy ? (int)(ab >> 16) : a;
+    }
+  };
+  // One island walked by a whole wave from seed sd (never touched yet: level 0): a popped body's
+  // edges one per lane, levels by a prefix maximum (below). Appends to s_ord / s_lvl at nord and
+  // s_ibod at nb; the stack lives at s_stk[sbase...], the wave's dummy slot at s_stk[N + wave].
+  // Every lane of the wave calls it.
+  auto par_walk = [&](auto HO, int sd, int& nord, int& nb, int sbase, int& dmax) {
     const int lane = tid & (W - 1);
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint16_t* stk = s_stk + sbase;
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) stk[0] = (uint16_t)sd;
+    uint16_t* const dummy = s_stk + N + tid / W;
+    // the body to pop next with its CSR range and level: the seed, then the last push of the
+    // previous pop (in registers; its stack slot is dropped), else the stack's top
     int sp = 1;
-    // the top of the stack when the previous pop pushed (its last push), with its CSR range
-    // and level, read by the pushing lane alongside its other reads: the next pop then waits
-    // on no LDS read
-    int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;
+    int top_b = sd, top_e0 = s_off[sd], top_e1 = s_off[sd + 1], top_last = 0;
     __builtin_amdgcn_wave_barrier();
     while (sp > 0) {
       int bdy, e0, e1, xcur;
@@ -626,52 +658,37 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
         bdy = stk[sp];
         e0 = s_off[bdy];
         e1 = s_off[bdy + 1];
-        xcur = s_last[bdy];
+        xcur = s_last[bdy] & kLvl;
       }
       top_b = -1;
       if (lane == 0) s_ibod[nb] = (uint16_t)bdy;
       ++nb;
       // Levels of the new contacts c_1..c_m of bdy, in order (all touch bdy; their other bodies
-      // o_i are distinct): with X_0 = s_last[bdy] and y_i = s_last[o_i], the serial rule
+      // o_i are distinct): with X_0 = last[bdy] and y_i = last[o_i], the serial rule
       // X_i = max(X_{i-1}, y_i) + 1 gives X_i = i + max(X_0, max_{j<=i}(y_j - j + 1)),
-      // a prefix maximum over the lanes; level(c_i) = X_i - 1.
+      // a prefix maximum over the lanes; level(c_i) = X_i - 1. Branch-free up to the stores:
+      // lanes past the body's last edge read that edge and take no part.
       for (int q0 = e0; q0 < e1; q0 += W) {
-        const int q = q0 + lane;
-        bool newc = false, push = false;
-        int t = 0, o = 0;
-        uint32_t ab = 0u;
-        if (q < e1) {
-          t = s_adj[q];
-          ab = s_tab[t];
-          newc = !(ab & 0x80000000u);
-        }
-        const unsigned long long mc = __ballot(newc);
-        int rank = 0, z = -0x3fffffff, oe0 = 0, oe1 = 0, xi = 0;
+        const int q = min(q0 + lane, e1 - 1);
+        const int t = s_adj[q];
+        const int o = edge_other(HO, q, t, bdy);
+        const int so = s_last[o];
+        const int oe0 = s_off[o], oe1 = s_off[o + 1];
+        const bool newc = q0 + lane < e1 && !(so & kPopped);
+        const bool push = newc && !(so & kPushed);
+        const unsigned long long mc = __ballot(newc), mp = __ballot(push);
+        const int rank = __popcll(mc & lt) + 1;
+        const int z = wave_prefix_max(newc ? (so & kLvl) - rank + 1 : -0x3fffffff);
+        const int xi = rank + max(xcur, z);
         if (newc) {
-          s_tab[t] = ab | 0x80000000u;
-          rank = __popcll(mc & lt) + 1;
+          s_last[o] = (uint16_t)(xi | kPushed);
           s_ord[nord + rank - 1] = (uint16_t)t;
-          const int a = ab & 0xffffu, bb = ab >> 16;
-          o = (a == bdy) ? bb : a;
-          push = (s_todo[o >> 6] >> (o & 63)) & 1ull;
-          z = (int)s_last[o] - rank + 1;
-          oe0 = s_off[o];
-          oe1 = s_off[o + 1];
-        }
-        z = wave_prefix_max(z);
-        if (newc) {
-          xi = rank + max(xcur, z);
-          s_last[o] = (uint16_t)xi;
           s_lvl[nord + rank - 1] = (uint16_t)(xi - 1);
+          *(push ? stk + sp + __popcll(mp & lt) : dummy) = (uint16_t)o;
         }
         const int mnew = __popcll(mc);
         if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
         nord += mnew;
-        const unsigned long long mp = __ballot(push);
-        if (push) {
-          atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
-          stk[sp + __popcll(mp & lt)] = (uint16_t)o;
-        }
         sp += __popcll(mp);
         if (mp) {  // the new top: the highest pushing lane
           const int hl = 63 - __clzll(mp);
@@ -682,11 +699,57 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
         }
         __builtin_amdgcn_wave_barrier();
       }
-      if (lane == 0) s_last[bdy] = (uint16_t)xcur;
+      if (lane == 0) s_last[bdy] = (uint16_t)(xcur | kPushed | kPopped);
       dmax = max(dmax, xcur);
       __builtin_amdgcn_wave_barrier();
     }
   };
+  // One island walked by one thread from seed sd (never touched yet), Box2D's serial order: per
+  // new contact, level = max(last[body], last[other]); the popped body's last stays in a register.
+  // Appends to s_ord / s_lvl at nord and s_ibod at nb; the stack lives at s_stk[nb at entry...].
+  auto serial_walk = [&](auto HO, int sd, int& nord, int& nb, int& dmax) {
+    const int sb = nb;
+    int sp = sb + 1;  // the seed, popped from registers
+    int top_b = sd, top_e0 = s_off[sd], top_e1 = s_off[sd + 1], top_lb = 0;
+    while (sp > sb) {
+      --sp;
+      int b, e0, e1, lb;
+      if (top_b >= 0) {
+        b = top_b;
+        e0 = top_e0;
+        e1 = top_e1;
+        lb = top_lb;
+      } else {
+        b = s_stk[sp];
+        e0 = s_off[b];
+        e1 = s_off[b + 1];
+        lb = s_last[b] & kLvl;
+      }
+      top_b = -1;
+      s_ibod[nb++] = (uint16_t)b;
+      for (int q = e0; q < e1; ++q) {
+        const int t = s_adj[q];
+        const int o = edge_other(HO, q, t, b);
+        const int so = s_last[o];
+        const int oe0 = s_off[o], oe1 = s_off[o + 1];
+        if (so & kPopped) continue;
+        const int l = max(lb, so & kLvl);  // level: 1 + the level of the last earlier contact touching b or o
+        lb = l + 1;
+        s_last[o] = (uint16_t)(lb | kPushed);
+        s_lvl[nord] = (uint16_t)l;
+        s_ord[nord++] = (uint16_t)t;
+        if (so & kPushed) continue;
+        s_stk[sp++] = (uint16_t)o;
+        top_b = o;
+        top_e0 = oe0;
+        top_e1 = oe1;
+        top_lb = lb;
+      }
+      s_last[b] = (uint16_t)(lb | kPushed | kPopped);
+      dmax = max(dmax, lb);
+    }
+  };
+#define MACM_WALK(f, ...) (s_oth ? f(std::true_type{}, __VA_ARGS__) : f(std::false_type{}, __VA_ARGS__))
   // Sparse worlds: islands first, then one thread per island (see kIslandDfs).
   const bool isl_dfs = kIslandDfs && !par_dfs && 2 * tcap >= 4 * N;
   if (isl_dfs) {
@@ -782,59 +845,14 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     if (wid < nbw) {
       const int sd = (int)job.x;
       int nord = (int)(job.y & 0xffffu), nb = (int)(job.y >> 16), dmax = 0;
-      if ((tid & (W - 1)) == 0) atomicAnd(&s_todo[sd >> 6], ~(1ull << (sd & 63)));
-      par_walk(sd, nord, nb, nb, dmax);
+      MACM_WALK(par_walk, sd, nord, nb, nb, dmax);
       if ((tid & (W - 1)) == 0) atomicMax(&s_misc[1], dmax);
     } else if (slot < nisl) {
       // the serial walk of island `slot` from its seed; its bodies, contacts and stack live in its
-      // own ranges, its bodies' todo bits share words with other islands' (atomicAnd)
+      // own ranges
       const int seed = (int)job.x;
       int nord = (int)(job.y & 0xffffu), nb = (int)(job.y >> 16), dmax = 0;
-      const int sb = nb;
-      int sp = sb;
-      atomicAnd(&s_todo[seed >> 6], ~(1ull << (seed & 63)));
-      s_stk[sp++] = (uint16_t)seed;
-      int top_b = -1, top_e0 = 0, top_e1 = 0;
-      while (sp > sb) {
-        --sp;
-        int b, e0, e1;
-        if (top_b >= 0) {
-          b = top_b;
-          e0 = top_e0;
-          e1 = top_e1;
-        } else {
-          b = s_stk[sp];
-          e0 = s_off[b];
-          e1 = s_off[b + 1];
-        }
-        top_b = -1;
-        s_ibod[nb++] = (uint16_t)b;
-        for (int q = e0; q < e1; ++q) {
-          const int t = s_adj[q];
-          const uint32_t ab = s_tab[t];
-          if (ab & 0x80000000u) continue;
-          s_tab[t] = ab | 0x80000000u;
-          const int a = ab & 0xffffu, bb = ab >> 16;
-          {
-            const int l = max((int)s_last[a], (int)s_last[bb]);
-            s_last[a] = (uint16_t)(l + 1);
-            s_last[bb] = (uint16_t)(l + 1);
-            s_lvl[nord] = (uint16_t)l;
-            dmax = max(dmax, l + 1);
-          }
-          s_ord[nord++] = (uint16_t)t;
-          const int o = (a == b) ? bb : a;
-          const unsigned long long ob = 1ull << (o & 63);
-          const unsigned long long tw = s_todo[o >> 6];
-          const int oe0 = s_off[o], oe1 = s_off[o + 1];
-          if (!(tw & ob)) continue;
-          atomicAnd(&s_todo[o >> 6], ~ob);
-          s_stk[sp++] = (uint16_t)o;
-          top_b = o;
-          top_e0 = oe0;
-          top_e1 = oe1;
-        }
-      }
+      MACM_WALK(serial_walk, seed, nord, nb, dmax);
       atomicMax(&s_misc[1], dmax);
     }
     if (kIslPriority) __builtin_amdgcn_s_setprio(0);
@@ -843,61 +861,20 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   // and other blocks' waves share the SIMD: raise its issue priority for the walk (as the wave
   // kernel does for its chain).
   if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(3);
-  if (!par_dfs && !isl_dfs && tid == 0) {
+  if (!par_dfs && !isl_dfs && tid == 0) {  // -DMACM_NO_ISLAND_DFS: one thread walks every island
     int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
-      const unsigned long long m = s_todo[w];
+      const unsigned long long m = s_todo[w];  // bodies with edges not considered as seeds yet
       if (m == 0ull) {
         --w;
         continue;
       }
       const int s = w * 64 + 63 - __clzll(m);
       s_todo[w] = m & ~(1ull << (s & 63));
+      if (s_last[s] & kPopped) continue;  // walked with an earlier seed's island
       s_ic[nisl] = (uint16_t)nord;
       s_ib[nisl] = (uint16_t)nb;
-      int sp = 0;
-      s_stk[sp++] = (uint16_t)s;
-      int top_b = -1, top_e0 = 0, top_e1 = 0;  // the last push of the previous pop (see par DFS)
-      while (sp > 0) {
-        --sp;
-        int b, e0, e1;
-        if (top_b >= 0) {
-          b = top_b;
-          e0 = top_e0;
-          e1 = top_e1;
-        } else {
-          b = s_stk[sp];
-          e0 = s_off[b];
-          e1 = s_off[b + 1];
-        }
-        top_b = -1;
-        s_ibod[nb++] = (uint16_t)b;
-        for (int q = e0; q < e1; ++q) {
-          const int t = s_adj[q];
-          const uint32_t ab = s_tab[t];
-          if (ab & 0x80000000u) continue;
-          s_tab[t] = ab | 0x80000000u;
-          const int a = ab & 0xffffu, bb = ab >> 16;
-          {  // level: 1 + the level of the last earlier contact touching a or bb
-            const int l = max((int)s_last[a], (int)s_last[bb]);
-            s_last[a] = (uint16_t)(l + 1);
-            s_last[bb] = (uint16_t)(l + 1);
-            s_lvl[nord] = (uint16_t)l;
-            dmax = max(dmax, l + 1);
-          }
-          s_ord[nord++] = (uint16_t)t;
-          const int o = (a == b) ? bb : a;
-          const unsigned long long ob = 1ull << (o & 63);
-          const unsigned long long tw = s_todo[o >> 6];
-          const int oe0 = s_off[o], oe1 = s_off[o + 1];
-          if (!(tw & ob)) continue;
-          s_todo[o >> 6] = tw & ~ob;
-          s_stk[sp++] = (uint16_t)o;
-          top_b = o;
-          top_e0 = oe0;
-          top_e1 = oe1;
-        }
-      }
+      MACM_WALK(serial_walk, s, nord, nb, dmax);
       ++nisl;
     }
     s_ic[nisl] = (uint16_t)nord;
@@ -905,10 +882,10 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     s_misc[0] = nisl;
     s_misc[1] = dmax;
   }
-  if (par_dfs && tid < W) {
+  if (par_dfs && tid < W) {  // -DMACM_NO_DFS_KERNEL: dense envs walked here by wave 0
     int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
-      const unsigned long long m = s_todo[w];
+      const unsigned long long m = s_todo[w] & __ballot(!(s_last[min(w * 64 + tid, N - 1)] & kPopped));
       if (m == 0ull) {
         --w;
         continue;
@@ -916,21 +893,20 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       const int sd = w * 64 + 63 - __clzll(m);
       __builtin_amdgcn_wave_barrier();
       if (tid == 0) {
-        s_todo[w] = m & ~(1ull << (sd & 63));
         s_ic[nisl] = (uint16_t)nord;
         s_ib[nisl] = (uint16_t)nb;
       }
-      par_walk(sd, nord, nb, 0, dmax);
+      MACM_WALK(par_walk, sd, nord, nb, 0, dmax);
       ++nisl;
     }
-    const int lane = tid;
-    if (lane == 0) {
+    if (tid == 0) {
       s_ic[nisl] = (uint16_t)nord;
       s_ib[nisl] = (uint16_t)nb;
       s_misc[0] = nisl;
       s_misc[1] = dmax;
     }
   }
+#undef MACM_WALK
   if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   const int nisl = s_misc[0];
@@ -1019,11 +995,11 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
 }
 
 namespace wg {
-// flock_dfs_wg's LDS (one wave per env): CSR edges (touching index | other body << 16), offsets,
-// per-body level bookkeeping, the stack, the unvisited-body and visited-contact bitmasks, the
-// island contact starts. The level counts of the records' counting sort reuse the edges.
+// flock_dfs_wg's LDS (one wave per env): CSR edges (other body only), offsets, per-body level and
+// walk state, the stack (one dummy slot past the end), the bodies with touching edges, the island
+// contact starts. The level counts of the records' counting sort reuse the edges.
 struct WgLayoutD {
-  int adj, off, last, stk, todo, pop, ic, total;
+  int adj, off, last, stk, has, ic, total;
 };
 __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
   WgLayoutD L;
@@ -1035,14 +1011,13 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
   };
   // 2 tcap edges, the other body (10 bits, N <= 1024) three to a word; adj..stk are reused as the
   // level counts (u32 [T + 1], T <= tcap)
-  const int rest = align16(2 * (N + 1)) + align16(2 * N) + align16(2 * N);
+  const int rest = align16(2 * (N + 1)) + align16(2 * N) + align16(2 * (N + 1));
   const int packed = 4 * ((2 * tcap + 2) / 3);
   L.adj = take(packed > 4 * (tcap + 1) - rest ? packed : 4 * (tcap + 1) - rest);
   L.off = take(2 * (N + 1));
   L.last = take(2 * N);
-  L.stk = take(2 * N);
-  L.todo = take(8 * ((N + 63) / 64));
-  L.pop = take(8 * ((N + 63) / 64));
+  L.stk = take(2 * (N + 1));
+  L.has = take(8 * ((N + 63) / 64));
   L.ic = take(2 * (N / 2 + 2));
   L.total = o;
   return L;
@@ -1070,8 +1045,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   uint16_t* s_off = (uint16_t*)(lds + L.off);
   uint16_t* s_last = (uint16_t*)(lds + L.last);
   uint16_t* s_stk = (uint16_t*)(lds + L.stk);
-  unsigned long long* s_todo = (unsigned long long*)(lds + L.todo);
-  unsigned long long* s_pop = (unsigned long long*)(lds + L.pop);  // bodies popped
+  unsigned long long* s_has = (unsigned long long*)(lds + L.has);  // bodies with touching edges
   uint16_t* s_ic = (uint16_t*)(lds + L.ic);
   const int IS = wg_isl_stride(N);
   const uint16_t* xoff = B.x_off + (size_t)e * (N + 1);
@@ -1087,19 +1061,27 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
     s_adj[wq] = o0 | (o1 << 10) | (o2 << 20);
   }
   for (int b = lane; b < N; b += W) s_last[b] = 0;
-  for (int w = lane; w < (N + 63) / 64; w += W) s_pop[w] = 0ull;
   __syncthreads();
-  for (int w = 0; w < (N + 63) / 64; ++w) {  // bodies with touching edges: DFS seeds / unvisited
+  for (int w = 0; w < (N + 63) / 64; ++w) {
     const int b = w * 64 + lane;
     const unsigned long long m = __ballot(b < N && s_off[b + 1] > s_off[b]);
-    if (lane == 0) s_todo[w] = m;
+    if (lane == 0) s_has[w] = m;
   }
   __syncthreads();
   if (kDfsPriority) __builtin_amdgcn_s_setprio(3);
+  // s_last[b]: 1 + the level of the last walked contact touching b (bits 0..13; levels <= tcap <
+  // 2^14), b pushed (bit 15), b popped (bit 14). One LDS read of the other body's word gives the
+  // three things an edge needs: the contact was walked iff its other body was popped (the first of
+  // its two bodies to be popped walks it), the body is pushed iff it was not pushed yet, and the
+  // level chain's input. A new contact's other body is pushed after it either way, so the walk
+  // writes its word as level | pushed; a pop ends by writing level | pushed | popped. Seeds are the
+  // highest bodies with edges not yet popped (every pushed body of an island is popped in it).
+  constexpr int kPushed = 0x8000, kPopped = 0x4000, kLvl = 0x3fff;
   const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   int nord = 0, nisl = 0, nb = 0, dmax = 0;
   for (int w = (N + 63) / 64 - 1; w >= 0;) {
-    const unsigned long long m = s_todo[w];
+    const int bw = w * 64 + lane;
+    const unsigned long long m = s_has[w] & __ballot(bw < N && !(s_last[min(bw, N - 1)] & kPopped));
     if (m == 0ull) {
       --w;
       continue;
@@ -1107,96 +1089,57 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
     const int sd = w * 64 + 63 - __clzll(m);
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
-      s_todo[w] = m & ~(1ull << (sd & 63));
       s_ic[nisl] = (uint16_t)nord;
       xib[nisl] = (uint16_t)nb;
-      s_stk[0] = (uint16_t)sd;
     }
+    // the body to pop next with its CSR range and level: the seed (never touched yet: level 0), then
+    // the last push of the previous pop (in registers; its stack slot is dropped), else the stack's
+    // top (two dependent LDS round trips)
     int sp = 1;
-    int top_b = -1, top_e0 = 0, top_e1 = 0, top_last = 0;  // the last push of the previous pop
-    __builtin_amdgcn_wave_barrier();
-    // The stack entry below the top, with its CSR range and level, read while the popped body is
-    // processed: when that body pushes nothing (common in dense worlds), the next pop finds them
-    // in registers instead of two dependent LDS round trips. Its level is refreshed from the lane
-    // that gives it a new contact in between (the only writer of s_last[that body]).
-    int pf_b = -1, pf_e0 = 0, pf_e1 = 0, pf_last = 0;
-    while (sp > 0) {
-      int bdy, e0, e1, xcur;
+    int top_b = sd, top_e0 = s_off[sd], top_e1 = s_off[sd + 1], top_last = 0;
+    for (;;) {
+      if (top_b < 0 && sp == 0) break;
       --sp;
+      int bdy, e0, e1, xcur;
       if (top_b >= 0) {
         bdy = top_b;
         e0 = top_e0;
         e1 = top_e1;
         xcur = top_last;
-      } else if (pf_b >= 0) {
-        bdy = pf_b;
-        e0 = pf_e0;
-        e1 = pf_e1;
-        xcur = pf_last;
       } else {
         bdy = s_stk[sp];
         e0 = s_off[bdy];
         e1 = s_off[bdy + 1];
-        xcur = s_last[bdy];
+        xcur = s_last[bdy] & kLvl;
       }
       top_b = -1;
-      pf_b = -1;
-      if (kDfsPrefetch && sp > 0) {
-        pf_b = s_stk[sp - 1];
-        pf_e0 = s_off[pf_b];
-        pf_e1 = s_off[pf_b + 1];
-        pf_last = s_last[pf_b];
-      }
-      if (lane == 0) {
-        xibod[nb] = (uint16_t)bdy;
-        // read by later pops only (no contact joins bdy to itself): no wait for the old word
-        __hip_atomic_fetch_or(&s_pop[bdy >> 6], 1ull << (bdy & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      }
+      if (lane == 0) xibod[nb] = (uint16_t)bdy;
       ++nb;
       // levels of the new contacts c_1..c_m of bdy in order: X_i = i + max(X_0, max_{j<=i}(y_j - j + 1))
-      // (see par_walk in kernel A)
+      // (see par_walk in kernel A). Branch-free up to the stores: lanes past the body's last edge
+      // read its last edge and take no part.
       for (int q0 = e0; q0 < e1; q0 += W) {
-        const int q = q0 + lane;
-        int o = 0, lo = 0, oe0 = 0, oe1 = 0;
-        unsigned long long tw = 0ull, pw = ~0ull;
-        if (q < e1) {  // one round of LDS reads after the edge's
-          const uint32_t qw = (uint32_t)q / 3u;
-          o = (s_adj[qw] >> (10u * ((uint32_t)q - 3u * qw))) & 1023u;
-          pw = s_pop[o >> 6];
-          tw = s_todo[o >> 6];
-          lo = s_last[o];
-          oe0 = s_off[o];
-          oe1 = s_off[o + 1];
-        }
-        const bool newc = !((pw >> (o & 63)) & 1ull);  // the contact was walked iff o was popped
-        const unsigned long long mc = __ballot(newc);
-        int rank = 0, z = -0x3fffffff, xi = 0;
-        bool push = false;
+        const int q = min(q0 + lane, e1 - 1);
+        const uint32_t qw = (uint32_t)q / 3u;
+        const int o = (s_adj[qw] >> (10u * ((uint32_t)q - 3u * qw))) & 1023u;
+        const int so = s_last[o];
+        const int oe0 = s_off[o], oe1 = s_off[o + 1];
+        const bool newc = q0 + lane < e1 && !(so & kPopped);
+        const bool push = newc && !(so & kPushed);
+        const unsigned long long mc = __ballot(newc), mp = __ballot(push);
+        const int rank = __popcll(mc & lt) + 1;
+        int z = wave_prefix_max(newc ? (so & kLvl) - rank + 1 : -0x3fffffff);
+        const int xi = rank + max(xcur, z);
         if (newc) {
-          rank = __popcll(mc & lt) + 1;
-          push = (tw >> (o & 63)) & 1ull;
-          z = lo - rank + 1;
-        }
-        z = wave_prefix_max(z);
-        if (newc) {
-          xi = rank + max(xcur, z);
-          s_last[o] = (uint16_t)xi;
+          s_last[o] = (uint16_t)(xi | kPushed);
           xdfs[nord + rank - 1] = (uint32_t)q | ((uint32_t)(xi - 1) << 16);  // CSR slot: < 2 tcap <= 9216
+          s_stk[push ? sp + __popcll(mp & lt) : N] = (uint16_t)o;  // slot N: the dummy
         }
         const int mnew = __popcll(mc);
         if (mnew) xcur = mnew + max(xcur, __builtin_amdgcn_readlane(z, W - 1));
         nord += mnew;
-        if (kDfsPrefetch) {  // the prefetched entry just got a new contact: its level is xi
-          const unsigned long long mf = __ballot(newc && o == pf_b);
-          if (mf) pf_last = __builtin_amdgcn_readlane(xi, __ffsll((long long)mf) - 1);
-        }
-        const unsigned long long mp = __ballot(push);
-        if (push) {
-          atomicAnd(&s_todo[o >> 6], ~(1ull << (o & 63)));
-          s_stk[sp + __popcll(mp & lt)] = (uint16_t)o;
-        }
         sp += __popcll(mp);
-        if (mp) {  // the new top: the highest pushing lane
+        if (mp) {  // the new top: the highest pushing lane, popped next straight from registers
           const int hl = 63 - __clzll(mp);
           top_b = __builtin_amdgcn_readlane(o, hl);
           top_e0 = __builtin_amdgcn_readlane(oe0, hl);
@@ -1205,7 +1148,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
         }
         __builtin_amdgcn_wave_barrier();
       }
-      if (lane == 0) s_last[bdy] = (uint16_t)xcur;
+      if (lane == 0) s_last[bdy] = (uint16_t)(xcur | kPushed | kPopped);
       dmax = max(dmax, xcur);
       __builtin_amdgcn_wave_barrier();
     }

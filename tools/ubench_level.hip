@@ -98,7 +98,7 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
       bool on = mylv == 0;
       float2* pa = on ? pa0 : pd;
       float2* pb = on ? pb0 : pd;
-#pragma unroll(VAR == 9 ? 2 : 1)
+#pragma unroll VAR == 9 ? 2 : 1
       for (int lv = 0; lv < nlev; ++lv) {
         float2 va = *pa, vb = *pb;
         const bool onc = on;
@@ -218,6 +218,48 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
         lt = chain ? y : lt;
         if constexpr (VAR == 8) wave_lds_sync();
       }
+    } else if constexpr (VAR == 10 || VAR == 11) {
+      // uniform form (N <= 64): body b's velocity lives in lane b (vx, vy); the level's contact
+      // (VAR 11: two disjoint contacts) has wave-uniform bodies, read by readlane, solved on
+      // uniform values and written back by writelane; its normal and impulses live in lane
+      // (level & 63) of per-lane registers. No LDS in the level loop.
+      float vx = s_v[lane].x, vy = s_v[lane].y;
+      float cnx = nx + 0.001f * lane, cny = ny - 0.001f * lane;
+      auto rl = [](float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+      auto wl = [](float v, int l, float old) {  // as writelane_m0 in flock_step_w64.hip
+        int o = __float_as_int(old);
+        asm volatile("s_nop 1\n\tv_writelane_b32 %0, %1, m0"
+                     : "+v"(o)
+                     : "s"(__builtin_amdgcn_readfirstlane(__float_as_int(v))), "{m0}"(__builtin_amdgcn_readfirstlane(l)));
+        return __int_as_float(o);
+      };
+      for (int lv = 0; lv < nlev; ++lv) {
+        const int c = lv & 63;
+        const int a0 = (lv * 7) & 63, b0 = (lv * 7 + 3) & 63;
+        float2 va = make_float2(rl(vx, a0), rl(vy, a0)), vb = make_float2(rl(vx, b0), rl(vy, b0));
+        float x = rl(ln, c), y = rl(lt, c);
+        gsv(va, vb, rl(cnx, c), rl(cny, c), x, y, mA, mA, kmass, fr);
+        if constexpr (VAR == 11) {
+          const int c2 = (lv + 32) & 63;
+          const int a1 = (lv * 7 + 5) & 63, b1 = (lv * 7 + 9) & 63;
+          float2 va1 = make_float2(rl(vx, a1), rl(vy, a1)), vb1 = make_float2(rl(vx, b1), rl(vy, b1));
+          float x1 = rl(ln, c2), y1 = rl(lt, c2);
+          gsv(va1, vb1, rl(cnx, c2), rl(cny, c2), x1, y1, mA, mA, kmass, fr);
+          vx = wl(va1.x, a1, vx);
+          vy = wl(va1.y, a1, vy);
+          vx = wl(vb1.x, b1, vx);
+          vy = wl(vb1.y, b1, vy);
+          ln = wl(x1, c2, ln);
+          lt = wl(y1, c2, lt);
+        }
+        vx = wl(va.x, a0, vx);
+        vy = wl(va.y, a0, vy);
+        vx = wl(vb.x, b0, vx);
+        vy = wl(vb.y, b0, vy);
+        ln = wl(x, c, ln);
+        lt = wl(y, c, lt);
+      }
+      s_v[lane] = make_float2(vx, vy);
     } else if constexpr (VAR == 5) {  // packed VALU chain alone
       f2v va = *(f2v*)pa0, vb = *(f2v*)pb0;
       const f2v n = {nx, ny}, t = {ny, -nx};
@@ -276,6 +318,8 @@ int main() {
     run<9>("V9 = V0 unrolled x2", blocks, nlev, iters);
     run<7>("V7 chain lanes, prefetched b", blocks, nlev, iters);
     run<8>("V8 chain lanes, b read+wait", blocks, nlev, iters);
+    run<10>("V10 uniform, 1 contact/level", blocks, nlev, iters);
+    run<11>("V11 uniform, 2 contacts/level", blocks, nlev, iters);
     run<3>("V3 VALU chain only", blocks, nlev, iters);
     run<5>("V5 packed VALU chain only", blocks, nlev, iters);
     run<4>("V4 LDS round trip only", blocks, nlev, iters);
