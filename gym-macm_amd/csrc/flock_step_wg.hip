@@ -1773,19 +1773,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       }
     }
     // nearest neighbours the walked strips cannot certify (a body outside the core [c0, c1] may be
-    // nearer): the wave walks every entry for them (the ones already seen change nothing)
-    const bool need = act && !grid::certified(G, px, T.c0, T.c1, bst);
-    if (__ballot(need)) {
+    // nearer; e.g. a body that strayed from its converged flock): the wave widens the core by 1, 2,
+    // 4, ... strips each way and walks the added strips for those lanes until each is certified
+    // (strips seen before change nothing); the whole range is covered after log2(H) rounds
+    bool need = act && !grid::certified(G, px, T.c0, T.c1, bst);
 #ifdef MACM_STAMPS
-      if (need) atomicAdd(&s_misc[3], 1);
+    if (need) atomicAdd(&s_misc[3], 1);
 #endif
-      const int qn = (int)G.start[G.H];
-      for (int q = 0; q < qn; ++q) {
+    for (int c0 = T.c0, c1 = T.c1, k = 1; __ballot(need); k <<= 1) {
+      const int n0 = max(0, c0 - k), n1 = min(G.H - 1, c1 + k);
+      const int qa = (int)G.start[n0], qb = (int)G.start[c0], qc = (int)G.start[c1 + 1], qd = (int)G.start[n1 + 1];
+      for (int q = qa; q < qb; ++q) {
         const float4 Eq = G.ent[q];
         const int j = __float_as_int(Eq.z);
         const float dx = Eq.x - px, dy = Eq.y - py;
         if (need && j != i) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
       }
+      for (int q = qc; q < qd; ++q) {
+        const float4 Eq = G.ent[q];
+        const int j = __float_as_int(Eq.z);
+        const float dx = Eq.x - px, dy = Eq.y - py;
+        if (need && j != i) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
+      }
+      c0 = n0;
+      c1 = n1;
+      need = need && !grid::certified(G, px, c0, c1, bst);
     }
 #ifdef MACM_STAMPS
     if (act) atomicAdd(&s_misc[2], ncand);
