@@ -281,6 +281,37 @@ __device__ __forceinline__ int wave_prefix_max(int v) {
   return v;
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave in lane order (integers), the DPP form of
+// wave_prefix_max: a lane whose DPP source is outside its row or the row mask is not written and
+// keeps its own partial sum. The whole wave must be active. -DMACM_NO_DPP_ASM: __shfl_up steps
+// (six LDS-crossbar round trips).
+__device__ __forceinline__ int wave_prefix_sum(int v) {
+#ifndef MACM_NO_DPP_ASM
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(v));
+  return v;
+#else
+  const int lane = threadIdx.x & 63;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+#endif
+}
+
 // Stores of the Flock step's per-agent outputs (obs, reward, neighbour id, collided): nontemporal
 // (the policy reads them, the step does not): driver window 34.0 -> 33.5 us, steady 21.6 -> 21.4 us
 // (profiles/r02/nt_stores). Not for TDM's [E, N, N-1, 4] obs: its 16-byte pair-tile stores then

@@ -122,11 +122,7 @@ __device__ __forceinline__ bool build(const Lds& G, bool act, float2 c, float4 f
     const int b0 = tid * per, b1 = min(G.H, b0 + per);
     uint32_t s = 0;
     for (int b = b0; b < b1; ++b) s += G.start[b];
-    uint32_t incl = s;  // block scan: wave shuffles + per-wave totals (red is free again)
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
-    }
+    const uint32_t incl = (uint32_t)wave_prefix_sum((int)s);  // block scan: wave DPP scan + per-wave totals (red is free again)
     if (lane == 63) ((uint32_t*)G.red)[wid] = incl;
     __syncthreads();
     uint32_t base = 0, total = 0;

@@ -103,11 +103,7 @@ __device__ __forceinline__ void normalize(float& x, float& y) {  // b2Vec2::Norm
 // Exclusive scan over the block in thread order; returns the block total.
 __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
   const int tid = threadIdx.x, lane = tid & (W - 1), wid = tid / W, nw = blockDim.x / W;
-  int incl = v;
-  for (int d = 1; d < W; d <<= 1) {
-    const int o = __shfl_up(incl, d, W);
-    if (lane >= d) incl += o;
-  }
+  const int incl = wave_prefix_sum(v);
   if (lane == W - 1) s_scan[wid] = incl;
   __syncthreads();
   int base = 0, total = 0;

@@ -662,13 +662,9 @@ __device__ __forceinline__ void sweep2_step(const PairRec* s_pj, SweepRec* win, 
 __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newmask, uint32_t* ocab,
                                                float2* ocimp, int C) {
   const int cnt = __popcll(newmask);
-  int incl = cnt;  // sum over lanes >= lane
-  for (int d = 1; d < W; d <<= 1) {
-    const int o = __shfl_down(incl, d, W);
-    if (lane + d < W) incl += o;
-  }
-  const int total = __shfl(incl, 0, W);
-  int w = incl - cnt;
+  const int pre = wave_prefix_sum(cnt);  // sum over lanes <= lane
+  const int total = __builtin_amdgcn_readlane(pre, W - 1);
+  int w = total - pre;  // the lanes above this one: they write first (descending a)
   unsigned long long m = newmask;
   while (m) {
     const int j = 63 - __clzll(m);

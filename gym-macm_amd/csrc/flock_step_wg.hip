@@ -72,8 +72,13 @@ constexpr bool kSolvePriority = false;
 constexpr bool kSolvePriority = true;
 #endif
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
+#ifndef MACM_SWEEP_PIPE  // A/B knob: kernel C's strip-cell candidate loop: entries read ahead (1), entries
+                         // and AABBs read ahead (2), in order (0)
+#define MACM_SWEEP_PIPE 1
+#endif
+constexpr bool kSweepPipe = MACM_SWEEP_PIPE != 0, kSweepPipe2 = MACM_SWEEP_PIPE == 2;
 #ifndef MACM_DFS_BATCH  // A/B knob: contacts per lane whose loads flock_dfs_wg's record pass issues together
-#define MACM_DFS_BATCH 4
+#define MACM_DFS_BATCH 8
 #endif
 constexpr int kDfsBatch = MACM_DFS_BATCH;
 
@@ -140,11 +145,7 @@ struct __align__(16) Rec {  // per-agent record for the pair sweep (48 B with fl
 // Exclusive scan over the block in thread order; returns the block total.
 __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
   const int tid = threadIdx.x, lane = tid & (W - 1), wid = tid / W, nw = blockDim.x / W;
-  int incl = v;
-  for (int d = 1; d < W; d <<= 1) {
-    const int o = __shfl_up(incl, d, W);
-    if (lane >= d) incl += o;
-  }
+  const int incl = wave_prefix_sum(v);
   if (lane == W - 1) s_scan[wid] = incl;
   __syncthreads();
   int base = 0, total = 0;
@@ -1187,11 +1188,7 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
     const int l0 = lane * per, l1 = min(dmax, l0 + per);
     int sum = 0;
     for (int l = l0; l < l1; ++l) sum += (int)s_cnt[l];
-    int incl = sum;
-    for (int d = 1; d < W; d <<= 1) {
-      const int y = __shfl_up(incl, d, W);
-      if (lane >= d) incl += y;
-    }
+    const int incl = wave_prefix_sum(sum);
     int run = incl - sum;
     for (int l = l0; l < l1; ++l) {
       const int c = (int)s_cnt[l];
@@ -1758,17 +1755,64 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 #ifdef MACM_STAMPS
         ncand += q1 - q0;
 #endif
-        for (int q = q0; q < q1; ++q) {
-          const float4 Eq = G.ent[q];
+        // One candidate: its entry (position, body) and its new fat AABB. Branch-free but for the
+        // rare overlap with a higher body (the old AABB's test for a new pair).
+        auto cand = [&](const float4 Eq, const float4 Fj) {
           const int j = __float_as_int(Eq.z);
-          const bool ovn = !(sep_max(fni, s_fn[j]) > 0.0f);
+          const bool ovn = !(sep_max(fni, Fj) > 0.0f);
           const float dx = Eq.x - px, dy = Eq.y - py;
           const bool other = j != i;
-          if (other) grid::nn_take(j, dx * dx + dy * dy, bst, bjj);
-          col |= other && ovn;
+          const float d2 = dx * dx + dy * dy;
+          // grid::nn_take with bitwise operators: no short-circuit branches
+          const bool take = other & ((d2 < bst) | ((d2 == bst) & (j < bjj)));
+          bst = take ? d2 : bst;
+          bjj = take ? j : bjj;
+          col |= other & ovn;
           const bool nw = j > i && ovn && sep_max(foi, s_fo[j]) > 0.0f;
           np2 = nw ? (np2 << 10) | (uint32_t)j : np2;
           nc += nw ? 1 : 0;
+        };
+        if (kSweepPipe2) {
+          // entries two candidates ahead and AABBs one ahead: every read has a whole candidate's
+          // test to arrive in (the loop-carried copies at the back edge find their loads done)
+          if (q0 < q1) {
+            const int ql = q1 - 1;
+            float4 Ea = G.ent[q0], Eb = G.ent[min(q0 + 1, ql)];
+            float4 Fa = s_fn[__float_as_int(Ea.z)];
+            for (int q = q0;; q += 2) {
+              const float4 Fb = s_fn[__float_as_int(Eb.z)];
+              const float4 Ec = G.ent[min(q + 2, ql)];
+              cand(Ea, Fa);
+              if (q + 1 >= q1) break;
+              const float4 Fc = s_fn[__float_as_int(Ec.z)];
+              const float4 Ed = G.ent[min(q + 3, ql)];
+              cand(Eb, Fb);
+              if (q + 2 >= q1) break;
+              Ea = Ec;
+              Fa = Fc;
+              Eb = Ed;
+            }
+          }
+        } else if (kSweepPipe) {
+          // two candidates per iteration, each entry read one candidate ahead (into the register
+          // pair the other candidate is not using, so the loop carries no copies that would wait
+          // for the loads): an entry's read hides under the previous candidate's test
+          if (q0 < q1) {
+            float4 Ea = G.ent[q0];
+            for (int q = q0;; q += 2) {
+              const float4 Eb = G.ent[min(q + 1, q1 - 1)];
+              cand(Ea, s_fn[__float_as_int(Ea.z)]);
+              if (q + 1 >= q1) break;
+              Ea = G.ent[min(q + 2, q1 - 1)];
+              cand(Eb, s_fn[__float_as_int(Eb.z)]);
+              if (q + 2 >= q1) break;
+            }
+          }
+        } else {
+          for (int q = q0; q < q1; ++q) {
+            const float4 Eq = G.ent[q];
+            cand(Eq, s_fn[__float_as_int(Eq.z)]);
+          }
         }
       }
     }
@@ -1945,9 +1989,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const float dx = pb.x - pa.x, dy = pb.y - pa.y;
       touch = !(dx * dx + dy * dy > rr);
     }
-    int tpos, kpos;
-    const int tn = block_scan_excl(touch ? 1 : 0, tpos, s_scan);
-    const int kn = block_scan_excl(keep ? 1 : 0, kpos, s_scan);
+    // one block scan for both ranks (touching in the low half, kept in the high; counts <= BS)
+    int packed;
+    const int pn = block_scan_excl((touch ? 1 : 0) | (keep ? 0x10000 : 0), packed, s_scan);
+    const int tpos = packed & 0xffff, kpos = packed >> 16, tn = pn & 0xffff, kn = pn >> 16;
     if (keep) {
       const int w = nnew + kept + kpos;
       const int trank = Tr + tpos;
@@ -1986,9 +2031,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
     }
   }
-  int dummy;
-  const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);
-  const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);
+  int dummy;  // both counts in one scan (collided in the low half, rewarded in the high)
+  const int cp = block_scan_excl((act && coll ? 1 : 0) | (act && rew > 0.0f ? 0x10000 : 0), dummy, s_scan);
+  const int ncoll = cp & 0xffff, npos = cp >> 16;
   if (status) atomicOr(&s_misc[1], status);
   __syncthreads();
   WSTAMP(8);
