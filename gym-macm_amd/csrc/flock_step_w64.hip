@@ -111,10 +111,13 @@ constexpr bool kLevels = true;
 // TDM obs through the staged writer (tdm_obs.hpp): whole-line stores, 709 B per agent-step of HBM
 // traffic instead of 864, but C4 34.1 us per step instead of 28.2 (profiles/r03/abtests/tdm_obs/):
 // off, the pair tiles stay (A/B knob)
-#ifdef MACM_NO_TDM_MASK_STAGED  // A/B knob: the pair tiles write the mask bytes straight to HBM
-constexpr bool kTdmMaskStaged = false;
-#else
+// The mask staged in LDS and written as 16-B pieces (round 4): HBM writes -4%, but the kernel's
+// extra VGPRs spill 28 B more scratch (reads +27%): 868 -> 870 B per agent-step, time unchanged
+// (profiles/r04/tdm_mask/). Off: the pair tiles write the mask bytes (A/B knob -DMACM_TDM_MASK_STAGED).
+#ifdef MACM_TDM_MASK_STAGED
 constexpr bool kTdmMaskStaged = true;
+#else
+constexpr bool kTdmMaskStaged = false;
 #endif
 #ifdef MACM_TDM_OBS_STAGED
 constexpr bool kTdmObsStaged = true;
