@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 box session: the wave kernel's wide Gauss-Seidel levels in level order (parity + A/B).
+set -u
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"
+OUT=gpurun_out/${1:-r04m}
+mkdir -p "$OUT"
+st() { echo "$1 rc=$2" | tee -a "$OUT/status.txt"; [ "$2" -eq 0 ] || exit "$2"; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_wide_levels.py tests/test_gpu_bots.py tests/test_gpu_tdm.py tests/test_gpu_headline.py \
+  tests/test_gpu_parity.py tests/test_gpu_rollout.py tests/test_gpu_dense.py > "$OUT/pytest.log" 2>&1; st pytest $?
+bash tools/ab_r04.sh "$(basename $OUT)/ab" "mbots:islord,lvord c4bots:islord,lvord mtr:islord,lvord c4:islord,lvord" > "$OUT/ab.log" 2>&1; st ab $?
+echo ALLDONE | tee -a "$OUT/status.txt"

@@ -218,6 +218,37 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
         lt = chain ? y : lt;
         if constexpr (VAR == 8) wave_lds_sync();
       }
+    } else if constexpr (VAR == 12 || VAR == 13) {
+      // V0 with ONE dummy slot shared by the lanes outside the level: their reads are an LDS
+      // broadcast (no bank conflicts with the level's lanes). V12: only the level's lanes store
+      // (exec-masked stores); V13: every lane stores (the dummy lanes all to the shared slot).
+      float2* const ps = s_v + 1024;
+      bool on = mylv == 0;
+      float2* pa = on ? pa0 : ps;
+      float2* pb = on ? pb0 : ps;
+      for (int lv = 0; lv < nlev; ++lv) {
+        float2 va = *pa, vb = *pb;
+        const bool onc = on;
+        on = mylv == lv + 1;
+        float2* const na = on ? pa0 : ps;
+        float2* const nb = on ? pb0 : ps;
+        float x = ln, y = lt;
+        gsv(va, vb, nx, ny, x, y, mA, mA, kmass, fr);
+        if constexpr (VAR == 12) {
+          if (onc) {
+            *pa = va;
+            *pb = vb;
+          }
+        } else {
+          *pa = va;
+          *pb = vb;
+        }
+        ln = onc ? x : ln;
+        lt = onc ? y : lt;
+        pa = na;
+        pb = nb;
+        wave_lds_sync();
+      }
     } else if constexpr (VAR == 10 || VAR == 11) {
       // uniform form (N <= 64): body b's velocity lives in lane b (vx, vy); the level's contact
       // (VAR 11: two disjoint contacts) has wave-uniform bodies, read by readlane, solved on
@@ -318,6 +349,8 @@ int main() {
     run<9>("V9 = V0 unrolled x2", blocks, nlev, iters);
     run<7>("V7 chain lanes, prefetched b", blocks, nlev, iters);
     run<8>("V8 chain lanes, b read+wait", blocks, nlev, iters);
+    run<12>("V12 shared dummy, masked st", blocks, nlev, iters);
+    run<13>("V13 shared dummy, all store", blocks, nlev, iters);
     run<10>("V10 uniform, 1 contact/level", blocks, nlev, iters);
     run<11>("V11 uniform, 2 contacts/level", blocks, nlev, iters);
     run<3>("V3 VALU chain only", blocks, nlev, iters);
