@@ -345,6 +345,11 @@ constexpr bool kWideLevels = false;
 constexpr bool kWideLevels = true;
 #endif
 constexpr int kNoLevel = 0xffff;  // a slot without a contact (or whose island has left the passes)
+#ifdef MACM_WIDE_ISLAND_ORDER  // A/B knob: slots in island order (round 3)
+constexpr bool kWideLevelOrder = false;
+#else
+constexpr bool kWideLevelOrder = true;
+#endif
 
 // S slots per lane; REG: each slot's normal and impulses in registers (S = 2, T <= 128), else read
 // from / written to the touching-contact arrays in LDS at every level step (S = 4: registers for
@@ -363,9 +368,9 @@ struct WideLevels {
   __device__ __forceinline__ static int isl(uint32_t x) { return x >> 16; }
 
   template <int S, bool REG>
-  __device__ __forceinline__ void init(int lane, int Tw, int nisl, const uint8_t* s_ord, const uint32_t* s_tab,
+  __device__ __forceinline__ void init(int lane, int Tw, int nisl, uint8_t* s_ord, const uint32_t* s_tab,
                                        const float* s_tnx, const float* s_tny, const float* s_tln,
-                                       const float* s_tlt, const uint16_t* s_ic) {
+                                       const float* s_tlt, const uint16_t* s_ic, uint32_t* s_tmp) {
     uint32_t abq[S];
 #pragma unroll
     for (int q = 0; q < S; ++q) {
@@ -412,6 +417,73 @@ struct WideLevels {
     }
 #pragma unroll
     for (int q = 0; q < S; ++q) lvis[q] |= (uint32_t)is[q] << 16;
+    if (kWideLevelOrder) reorder<S, REG>(lane, Tw, s_ord, s_tab, s_tnx, s_tny, s_tln, s_tlt, s_tmp);
+  }
+
+  // Level order (round 4): contact k of the level-sorted order moves to slot k / 64 of lane k % 64,
+  // so a level's contacts fill one slot (a level straddles two slots at most once) and a level step
+  // runs one slot's update. In island order every island restarts at level 0, so with two or more
+  // islands most level steps ran an update per slot. Contacts of one level share no body: their
+  // order within the level changes nothing. s_tmp (>= 512 B, the DFS masks, dead here): the level
+  // histogram as 16-bit counters, then each contact's level | island << 8 at its new place.
+  template <int S, bool REG>
+  __device__ __forceinline__ void reorder(int lane, int Tw, uint8_t* s_ord, const uint32_t* s_tab,
+                                          const float* s_tnx, const float* s_tny, const float* s_tln,
+                                          const float* s_tlt, uint32_t* s_tmp) {
+    for (int w = lane; w < 128; w += 64) s_tmp[w] = 0u;  // 256 levels (dmax <= Tw <= 256)
+    wave_lds_sync();
+    int rk[S], tq[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const int l = lvl(lvis[q]);
+      tq[q] = it(pw[q]);
+      rk[q] = 0;
+      if (l != kNoLevel) {
+        const uint32_t sh = 16u * (uint32_t)(l & 1);
+        rk[q] = (int)((atomicAdd(&s_tmp[l >> 1], 1u << sh) >> sh) & 0xffffu);
+      }
+    }
+    wave_lds_sync();
+    {  // exclusive scan of the counts: lane L owns levels 4L .. 4L + 3 (two words)
+      const uint32_t w0 = s_tmp[2 * lane], w1 = s_tmp[2 * lane + 1];
+      const int c0 = (int)(w0 & 0xffffu), c1 = (int)(w0 >> 16), c2 = (int)(w1 & 0xffffu), c3 = (int)(w1 >> 16);
+      const int sum = c0 + c1 + c2 + c3;
+      const int ex = wave_prefix_sum(sum) - sum;
+      wave_lds_sync();
+      s_tmp[2 * lane] = (uint32_t)ex | ((uint32_t)(ex + c0) << 16);
+      s_tmp[2 * lane + 1] = (uint32_t)(ex + c0 + c1) | ((uint32_t)(ex + c0 + c1 + c2) << 16);
+    }
+    wave_lds_sync();
+    int pos[S];
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const int l = lvl(lvis[q]);
+      pos[q] = l != kNoLevel ? (int)((s_tmp[l >> 1] >> (16u * (uint32_t)(l & 1))) & 0xffffu) + rk[q] : -1;
+    }
+    wave_lds_sync();
+    uint16_t* const s_lv = reinterpret_cast<uint16_t*>(s_tmp);
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+      if (pos[q] >= 0) {
+        s_ord[pos[q]] = (uint8_t)tq[q];
+        s_lv[pos[q]] = (uint16_t)(lvl(lvis[q]) | (isl(lvis[q]) << 8));
+      }
+    wave_lds_sync();
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const int k = 64 * q + lane;
+      const int t = k < Tw ? (int)s_ord[k] : 0;
+      const uint32_t ab = k < Tw ? s_tab[t] : 0u;
+      const uint32_t lv = k < Tw ? (uint32_t)s_lv[k] : 0u;
+      pw[q] = (ab & 0xffu) | ((ab >> 8) & 0xff00u) | ((uint32_t)t << 16);
+      lvis[q] = k < Tw ? ((lv & 0xffu) | ((lv >> 8) << 16)) : (uint32_t)kNoLevel;
+      if constexpr (REG) {
+        nx[q] = s_tnx[t];
+        ny[q] = s_tny[t];
+        ln[q] = s_tln[t];
+        lt[q] = s_tlt[t];
+      }
+    }
   }
 
   // warm start (pass -1) + vel_iters velocity passes, level by level; then (REG) the impulses to
@@ -1302,7 +1374,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       constexpr int S = decltype(sc)::value;
       constexpr bool REG = decltype(rc)::value;
       WideLevels wl;
-      wl.template init<S, REG>(lane, Tw, nisl, s_ord, s_tab, s_tnx, s_tny, s_tln, s_tlt, s_ic);
+      wl.template init<S, REG>(lane, Tw, nisl, s_ord, s_tab, s_tnx, s_tny, s_tln, s_tlt, s_ic, s_tm);
       wl.template velocity<S, REG>(P, s_v, s_tnx, s_tny, s_tln, s_tlt, mA, mB, kmass, friction);
       __syncthreads();
       STAMP(5);
