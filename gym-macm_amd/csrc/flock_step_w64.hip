@@ -345,6 +345,27 @@ constexpr bool kWideLevels = false;
 constexpr bool kWideLevels = true;
 #endif
 constexpr int kNoLevel = 0xffff;  // a slot without a contact (or whose island has left the passes)
+// One-slot level steps: the lanes outside the level on a dummy slot each (round 3). One shared slot
+// (an LDS broadcast; microbenchmark V13 278 -> 275 cycles per level step, kernel B C5 -1%) measured
+// M bots +2%, the window unchanged (profiles/r04/abtests/shared_dummy/): A/B knob
+// -DMACM_WAVE_SHARED_DUMMY. The position minima of dummy lanes stay per lane either way.
+#ifdef MACM_WAVE_SHARED_DUMMY
+constexpr bool kSharedDummy = true;
+#else
+constexpr bool kSharedDummy = false;
+#endif
+// Level order: skip a slot by its level range (a scalar test) before the exec-masked update. Measured
+// M bots 161 -> 197 us (profiles/r04/abtests/serial_prefetch/), off: A/B knob -DMACM_WIDE_RANGE_SKIP.
+#ifdef MACM_WIDE_RANGE_SKIP
+constexpr bool kWideRangeSkip = kWideLevelOrder;
+#else
+constexpr bool kWideRangeSkip = false;
+#endif
+#ifdef MACM_WIDE_PRIORITY  // A/B knob: only the wide-level waves keep priority 3 through the chain
+constexpr bool kWidePriority = true;
+#else
+constexpr bool kWidePriority = false;
+#endif
 #ifdef MACM_WIDE_ISLAND_ORDER  // A/B knob: slots in island order (round 3)
 constexpr bool kWideLevelOrder = false;
 #else
@@ -486,6 +507,23 @@ struct WideLevels {
     }
   }
 
+  // level order: the lowest and highest level of each slot (lane 0 and the slot's last contact;
+  // an empty slot gets an empty range)
+  template <int S>
+  __device__ __forceinline__ void slot_ranges(int* lo, int* hi) const {
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const unsigned long long m = __ballot(lvl(lvis[q]) != kNoLevel);
+      if (m == 0ull) {
+        lo[q] = 1;
+        hi[q] = 0;
+      } else {
+        lo[q] = lvl((uint32_t)__builtin_amdgcn_readfirstlane((int)lvis[q]));
+        hi[q] = lvl((uint32_t)__builtin_amdgcn_readlane((int)lvis[q], 63 - __clzll(m)));
+      }
+    }
+  }
+
   // warm start (pass -1) + vel_iters velocity passes, level by level; then (REG) the impulses to
   // s_tln / s_tlt
   template <int S, bool REG>
@@ -498,10 +536,17 @@ struct WideLevels {
     // than one after the other), and levels grow along the island order, so in most level steps
     // one slot is busy. The warm-start pass and the velocity passes are separate loops, so that a
     // level step has no branch before its stores.
+    // Level order (kWideLevelOrder): slot q holds levels lo[q] .. hi[q] (wave-uniform), so a level
+    // step visits only the slots whose range holds it (a scalar test). The update stays
+    // exec-masked: run branch-free (every lane on the slot, the idle ones on a dummy) it was 14%
+    // slower in the M closed loop, where 4-5 waves per SIMD share the CU's LDS.
+    int lo[S], hi[S];
+    slot_ranges<S>(lo, hi);
     auto pass = [&](auto warm) {
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {
+          if (kWideRangeSkip && (l < lo[q] || l > hi[q])) continue;  // uniform: no lane of slot q at level l
           if (lvl(lvis[q]) == l) {  // exec-masked; a slot with no contact of this level is skipped
             if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));  // LDS addresses not hoisted (VGPRs)
             float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
@@ -553,6 +598,8 @@ struct WideLevels {
                                            uint8_t* s_isolved, float mA, float mB) {
     const unsigned long long islm = nisl >= 64 ? ~0ull : ((1ull << nisl) - 1ull);
     unsigned long long done = 0ull;
+    int lo[S], hi[S];  // level order: each slot's level range, taken before islands leave (a superset after)
+    slot_ranges<S>(lo, hi);
     for (int itr = 0; itr < P.pos_iters && done != islm; ++itr) {
       if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
       // an island that has left the passes never returns: its contacts lose their level
@@ -562,6 +609,7 @@ struct WideLevels {
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {  // one slot at a time, busy slots only, as in the velocity passes
+          if (kWideRangeSkip && (l < lo[q] || l > hi[q])) continue;  // uniform (slot ranges, below)
           if (lvl(lvis[q]) == l) {
             if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));
             float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
@@ -1349,6 +1397,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   // would walk such an island serially, ~470 cycles per contact update
   const bool lvl_wide = kWideLevels && T > 64 && big_isl;
   const bool skip_isl = lvl_path || lvl_wide;  // no per-island lanes: the level paths solve every island
+  // The widest chains (T > 64 solved by levels, converged flocks) set a closed loop's step time: the
+  // other waves with contacts step down to priority 2 for the rest of the chain (A/B knob).
+  if (kWidePriority && kChainPriority && hasdeg && !lvl_wide) __builtin_amdgcn_s_setprio(2);
   // ---- integrate positions --------------------------------------------------
   float cx = p.x, cy = p.y;
   auto integrate_positions = [&]() {
@@ -1441,9 +1492,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       // every lane runs every level step, the lanes outside the level on their own dummy slot in
       // s_tm (the DFS masks: dead until the next step's Collide), so a level step has no exec-mask
       // branch; only the level's lanes keep their impulses
-      float2* const pda = lhas ? s_v + la : reinterpret_cast<float2*>(s_tm) + lane;
-      float2* const pdb = lhas ? s_v + lb : reinterpret_cast<float2*>(s_tm) + lane;
-      float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
+      float2* const pdd = reinterpret_cast<float2*>(s_tm) + (kSharedDummy ? 0 : lane);
+      float2* const pda = lhas ? s_v + la : pdd;
+      float2* const pdb = lhas ? s_v + lb : pdd;
       const int mylvl = lhas ? lvl : -1;
       auto lpass = [&](auto warm) {
 #if MACM_WAVE_LEVEL_ADDR_AHEAD
@@ -1653,10 +1704,11 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           // an island that has left) correct their own dummy slot in s_tm and take their minimum
           // into its first word
           const int mylvl = (lhas && !((done >> lisl) & 1ull)) ? lvl : -1;
-          float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
+          float2* const pdd = reinterpret_cast<float2*>(s_tm) + (kSharedDummy ? 0 : lane);
           float2* const pda = lhas ? s_c + la : pdd;
           float2* const pdb = lhas ? s_c + lb : pdd;
-          int* const pmd = reinterpret_cast<int*>(pdd);
+          // a dummy lane's minimum: its own word (past the shared slot), atomics on one address serialise
+          int* const pmd = kSharedDummy ? reinterpret_cast<int*>(s_tm) + 2 + lane : reinterpret_cast<int*>(pdd);
           int* const pmi = lhas ? s_pmin + lisl : pmd;
 #if MACM_WAVE_LEVEL_ADDR_AHEAD
           float2* pa = mylvl == 0 ? pda : pdd;

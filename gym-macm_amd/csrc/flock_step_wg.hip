@@ -72,6 +72,17 @@ constexpr bool kSolvePriority = false;
 constexpr bool kSolvePriority = true;
 #endif
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
+#ifndef MACM_SERIAL_PREFETCH  // A/B knob: kernel A's one-thread island walks read the next edge ahead
+#define MACM_SERIAL_PREFETCH 1
+#endif
+constexpr bool kSerialPrefetch = MACM_SERIAL_PREFETCH != 0;
+// Kernel B's level steps: the idle lanes share one dummy slot (an LDS broadcast; A/B knob
+// -DMACM_LANE_DUMMY: a slot per lane, round 3); their position minima keep a word each.
+#ifdef MACM_LANE_DUMMY
+constexpr bool kSharedDummy = false;
+#else
+constexpr bool kSharedDummy = true;
+#endif
 #ifndef MACM_SWEEP_PIPE  // A/B knob: kernel C's strip-cell candidate loop: entries read ahead (1), entries
                          // and AABBs read ahead (2), in order (0)
 #define MACM_SWEEP_PIPE 1
@@ -728,9 +739,25 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       }
       top_b = -1;
       s_ibod[nb++] = (uint16_t)b;
+      // the next edge and its other body are read one edge ahead (the edges are not written
+      // during the walk): an edge then costs one dependent LDS round trip (its other body's word)
+      int tn = 0, on = 0;
+      if (kSerialPrefetch && e0 < e1) {
+        tn = s_adj[e0];
+        on = edge_other(HO, e0, tn, b);
+      }
       for (int q = e0; q < e1; ++q) {
-        const int t = s_adj[q];
-        const int o = edge_other(HO, q, t, b);
+        int t, o;
+        if (kSerialPrefetch) {
+          t = tn;
+          o = on;
+          const int qn = min(q + 1, e1 - 1);
+          tn = s_adj[qn];
+          on = edge_other(HO, qn, tn, b);
+        } else {
+          t = s_adj[q];
+          o = edge_other(HO, q, t, b);
+        }
         const int so = s_last[o];
         const int oe0 = s_off[o], oe1 = s_off[o + 1];
         if (so & kPopped) continue;
@@ -1445,7 +1472,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       // exec-mask branch per level); only the level's lanes keep their impulses
       float2* const pa0 = s_v + a;
       float2* const pb0 = s_v + b;
-      float2* const pd = s_dum + lane;
+      float2* const pd = s_dum + (kSharedDummy ? 0 : lane);  // shared: an LDS broadcast for the idle lanes
       float2* pa = mylv == lv0 ? pa0 : pd;
       float2* pb = mylv == lv0 ? pb0 : pd;
       level_loop(lv0, lv1, mylv, [&](int, bool onc, bool onn) {
@@ -1519,19 +1546,21 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
         const bool live = !s_done[I];
         // branch-free level steps as in the velocity passes; the dummy slots are in s_v (dead after
         // the position integration), a dummy lane's minimum goes to its slot's first word
-        float2* const pdd = s_v + lane;
+        float2* const pdd = s_v + (kSharedDummy ? 0 : lane);
+        // a dummy lane's minimum stays in a word of its own (atomics on one address serialise)
+        float* const pmd = reinterpret_cast<float*>(s_v + (kSharedDummy ? 1 + lane : lane));
         const int mylvp = live ? mylv : -1;
         float2* const pca = s_c + a;
         float2* const pcb = s_c + b;
         float* const pmi = s_mins + I;
         float2* pa = mylvp == lv0 ? pca : pdd;
         float2* pb = mylvp == lv0 ? pcb : pdd;
-        float* pm = mylvp == lv0 ? pmi : reinterpret_cast<float*>(pdd);
+        float* pm = mylvp == lv0 ? pmi : pmd;
         level_loop(lv0, lv1, mylvp, [&](int, bool, bool onn) {
           float2 ca = *pa, cb = *pb;
           float2* const na = onn ? pca : pdd;
           float2* const nb = onn ? pcb : pdd;
-          float* const nm = onn ? pmi : reinterpret_cast<float*>(pdd);
+          float* const nm = onn ? pmi : pmd;
           const float sep = gs_position<kpos>(ca, cb, P.radius, mA, mB);
           *pa = ca;
           *pb = cb;
