@@ -114,6 +114,13 @@ constexpr bool kLevels = true;
 // The mask staged in LDS and written as 16-B pieces (round 4): HBM writes -4%, but the kernel's
 // extra VGPRs spill 28 B more scratch (reads +27%): 868 -> 870 B per agent-step, time unchanged
 // (profiles/r04/tdm_mask/). Off: the pair tiles write the mask bytes (A/B knob -DMACM_TDM_MASK_STAGED).
+// TDM obs in row-block order with the transposed half staged (tdm_obs.hpp, round 4; float32 obs,
+// N <= 32: the 6 KB stage). A/B knob -DMACM_NO_TDM_ROWBLOCKS: the pair tiles as in round 3.
+#ifdef MACM_NO_TDM_ROWBLOCKS
+constexpr bool kTdmObsRowBlocks = false;
+#else
+constexpr bool kTdmObsRowBlocks = true;
+#endif
 #ifdef MACM_TDM_MASK_STAGED
 constexpr bool kTdmMaskStaged = true;
 #else
@@ -2066,6 +2073,12 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       if (staged)
         tdm_obs_staged<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<unsigned char*>(&s_pool));
     }
+    if constexpr (sizeof(OT) == 4 && kTdmObsRowBlocks) {
+      if (!staged && tdm_obs_rb_stage_bytes(N) <= (int)sizeof(Pool)) {  // the contact arrays are dead here
+        tdm_obs_rowblocks<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<float4*>(&s_pool));
+        staged = true;
+      }
+    }
     if (!staged) {
       if (kTdmMaskStaged && N * (N - 1) <= (int)sizeof(Pool))  // the contact arrays are dead here
         tdm_obs_pairs_smask<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<uint8_t*>(&s_pool));
@@ -2156,6 +2169,10 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
 // (flock_rollout_w64.hip, -mllvm -disable-machine-licm): with the step inside a loop, machine
 // LICM hoists the f64 polynomial constants of the trig and atan2 code out of it and the
 // register allocator spills them (327 VGPRs of spills; none without the hoisting).
+#ifndef MACM_ROLL_OPAQUE_LANE  // A/B knob: 0 none, 1 TDM rollouts, 2 TDM and Flock rollouts
+#define MACM_ROLL_OPAQUE_LANE 1
+#endif
+constexpr bool kRollOpaqueLaneTdm = MACM_ROLL_OPAQUE_LANE >= 1, kRollOpaqueLaneFlock = MACM_ROLL_OPAQUE_LANE >= 2;
 template <typename OT>
 struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   StepParams P;
@@ -2210,10 +2227,16 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     const size_t abytes = MODE == kTdm ? 4 : 3;  // closed loop: uint8 actions per agent
     uint8_t* const pol_in = A.policy_act ? A.policy_act + kr * EN * abytes : nullptr;
     __builtin_amdgcn_s_setprio(0);  // as at a launch: the chain raises it again
+    // The lane index, opaque to the compiler inside the loop: else every lane-derived address and
+    // mask of the step is hoisted out of it and held across all K steps. The TDM step then ran out
+    // of its 128 VGPRs and kept 7 of them in scratch, re-read every step (rollout: 28 B per lane).
+    int sl = (int)threadIdx.x;
+    if (MODE == kTdm ? kRollOpaqueLaneTdm : kRollOpaqueLaneFlock) asm volatile("" : "+v"(sl));
     step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, TB, A.cur ^ (k & 1),
                                         pol_in ? pol_in : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
                                         obs, traj_row(A.nbr_out, kr, EN), traj_row(A.rew_out, kr, EN),
-                                        traj_row(A.coll_out, kr, EN), traj_row(A.done_out, kr, (size_t)A.P.n_envs));
+                                        traj_row(A.coll_out, kr, EN), traj_row(A.done_out, kr, (size_t)A.P.n_envs),
+                                        blockIdx.x, sl);
     // the next step reads only what this wave wrote: workgroup scope (this CU's L1 and its XCD's L2)
     // suffices; agent scope would write back and invalidate the L2 every step (5x slower, measured)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

@@ -300,6 +300,83 @@ __device__ __forceinline__ void tdm_obs_staged(OT* __restrict__ obs, uint8_t* __
   }
 }
 
+// Row-block order (round 4): the pair tiles of tdm_obs_pairs (each unordered pair once, both
+// directions from one atan2 core), but taken row block by row block so that every 128-B line of
+// the env's [N, N-1, 4] block is written within one short stretch. Row block R (rows 8R .. 8R+7,
+// 8 x 496 B = 31 whole lines at N = 32) gets its tiles (R, J > R) in the pair's own direction
+// (row i, slot j - 1), its diagonal tile, and its slots i < 8R, which the tiles (I < R, R)
+// computed in earlier blocks and left in an LDS stage as the finished float32 slot (the same bits
+// the pair form stores). The pair tiles wrote that direction into rows of later blocks as 8-slot
+// runs spread over the whole obs phase, whose lines left L2 partly written (PMC: ~150 B per
+// agent-step of HBM writes above the algorithmic bytes). float32 obs; stage:
+// 512 nb (nb - 1) bytes, nb = N / 8 rounded up (6 KB at N = 32: the wave kernel's dead contact
+// arrays).
+__host__ __device__ constexpr int tdm_obs_rb_stage_bytes(int N) { return 512 * ((N + 7) >> 3) * (((N + 7) >> 3) - 1); }
+
+template <typename OT>
+__device__ __forceinline__ void tdm_obs_rowblocks(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
+                                                  unsigned long long livem, const TdmParams& TP, const float2* sc,
+                                                  const float* sa, float4* stage) {
+  static_assert(sizeof(OT) == 4, "the stage keeps the finished float32 slots");
+  const int S = N - 1, nb = (N + 7) >> 3;
+  const int a = lane >> 3, b = lane & 7;
+  int dr = 0, rem = lane & 31;  // diagonal pair `lane & 31` (< 28) of a block: row-major over dr < dc
+  while (dr < 7 && rem >= 7 - dr) {
+    rem -= 7 - dr;
+    ++dr;
+  }
+  const int dc = dr + 1 + rem;
+  auto soff = [](int J) { return 32 * J * (J - 1); };  // stage entries of the blocks before J: 8J' slots x 8 rows
+  for (int R = 0; R < nb; ++R) {
+    const int i = 8 * R + a;
+    for (int J = R + 1; J < nb; ++J) {
+      const int j = 8 * J + b;
+      if (i < N && j < N) {
+        const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
+        double r = 0.0, t1 = 0.0, t2 = 0.0, p1 = 0.0, ty = 0.0;
+        if (m) {  // tdm_obs_pair_m's arithmetic
+          const float2 ci = sc[i], cj = sc[j];
+          const float xi = ci.x, yi = ci.y, xj = cj.x, yj = cj.y, ai = sa[i], aj = sa[j];
+          const float rx = xj - xi, ry = yj - yi;
+          const float qx = xi - xj, qy = yi - yj;
+          const float d2 = rx * rx + ry * ry;
+          r = obs_sqrt<OT>(d2);
+          const double core = obs_atan2_core(fabs((double)rx), fabs((double)ry));
+          t1 = wrap_pi(obs_atan2_finish(core, (double)ry, (double)rx) - (double)ai);
+          t2 = wrap_pi(obs_atan2_finish(core, (double)qy, (double)qx) - (double)aj);
+          p1 = wrap_pi((double)aj - (double)ai);
+          ty = tdm_team_nb(TP, j) == tdm_team_nb(TP, i) ? 1.0 : 0.0;
+        }
+        const size_t s1 = (size_t)i * S + (j - 1);
+        if (obs) store4<OT>(obs + s1 * 4, r, t1, p1, ty);
+        if (mask) mask[s1] = m ? 1 : 0;
+        // row j = 8J + b, slot i, as store4 would write it (p2 = -p1 exactly); lanes contiguous
+        stage[soff(J) + 8 * i + b] = make_float4((float)r, (float)t2, (float)(-p1), (float)ty);
+      }
+    }
+    // the diagonal tiles two at a time (lanes 0-27 block R, lanes 32-59 block R + 1, as the pair
+    // tiles do): block R + 1's own pairs are written one block early
+    if ((R & 1) == 0) {
+      const int D = R + (lane >> 5), k = lane & 31;
+      if (k < 28 && D < nb && 8 * D + dc < N) tdm_obs_pair<OT>(obs, mask, S, 8 * D + dr, 8 * D + dc, livem, TP, sc, sa);
+    }
+    if (R > 0) {
+      wave_lds_sync();  // the stage entries of block R (other lanes, earlier blocks)
+      // rows 8R .. 8R + 7, slots o < 8R: 64 R entries, one per lane, entry e = 8 o + rb (each store
+      // instruction: 8 rows x 8 consecutive slots); masked slots were staged as zeros
+      for (int e = lane; e < 64 * R; e += 64) {
+        const int o = e >> 3, rb = e & 7;
+        const int j = 8 * R + rb;
+        if (j < N) {
+          const size_t s2 = (size_t)j * S + o;
+          if (obs) *reinterpret_cast<float4*>(obs + s2 * 4) = stage[soff(R) + e];
+          if (mask) mask[s2] = ((livem >> o) & (livem >> j) & 1ull) ? 1 : 0;
+        }
+      }
+    }
+  }
+}
+
 #ifdef MACM_TDM_OBS_LINEAR
 #define MACM_TDM_OBS tdm_obs_linear
 #else
