@@ -1187,6 +1187,18 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     // TDM: the same hand-over, after this step's actions, casts and deaths; the spill step does the
     // physics of the living bodies and TDM's env layer (its records in HBM: the pool is smaller)
     if (touch_over || (!fast_dfs && __builtin_amdgcn_ballot_w64(deg > DEG) != 0ull) || P.force_spill) {
+      // The spill working-set slot is taken before anything of this step is committed: a pool that
+      // stays full (~1 s) leaves the env wholly unstepped and reported, never half-stepped (ADVICE
+      // r03, as the workgroup TDM step does)
+      __shared__ int s_slot;
+      const int slot = spill::acquire_slot(B, e, &s_slot);
+      if (slot < 0) {
+        if (lane == 0) {
+          B.status[e] |= MACM_ST_SPILL_WAIT;
+          report_status(B, MACM_ST_SPILL_WAIT);
+        }
+        return;
+      }
       // the combat state of this step is committed first (the spill step reads it back: nothing
       // of it stays live in registers across the spill step)
       if (lane < N) {
@@ -1208,7 +1220,8 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         B.env_counters[(size_t)e * 4 + 2] = ctr[2] + (unsigned long long)__popcll(alive0_m & ~livem);
       }
       spill::step_env<OT, false, kTdm>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out,
-                                        reinterpret_cast<unsigned char*>(&s_pool), &TP, &TB, make_float2(Fx, Fy));
+                                        reinterpret_cast<unsigned char*>(&s_pool), &TP, &TB, make_float2(Fx, Fy),
+                                        slot);
       return;
     }
 #endif
