@@ -101,6 +101,9 @@ struct WorldBuffers {
   int32_t sp_pool;               // pool size S (0: one slot per env, slot = env)
   uint32_t* spill_count;         // [E]       steps taken by the spill step (macm_world_spilled)
   uint32_t* host_status;         // mapped pinned host word: nonzero once any env set a status bit
+  // [E] wave-kernel rollouts: the env order of the launch, heaviest first (flock_step_w64.hip,
+  // rollout_sched); NULL: wave b steps env b
+  uint32_t* sched;
 };
 
 // A status bit was set in some env: tell the host without a synchronisation (macm_world_step

@@ -1311,6 +1311,11 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       ++nisl;
     }
     };
+#ifdef MACM_AB_DFS_TWICE  // timing-only A/B knob: the walk's cost (run once more, discarded)
+    if (TMW == 2 && T > 64) dfs(BoolC<true>{});
+    else dfs(BoolC<false>{});
+    nord = nisl = nb = 0;
+#endif
     if (TMW == 2 && T > 64) dfs(BoolC<true>{});
     else dfs(BoolC<false>{});
     icv = writelane_m0(nord, nisl, icv);
@@ -1462,6 +1467,17 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     if (lvl_path) {
       const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
       uint32_t lastv = 0u;
+#ifdef MACM_AB_LVL_TWICE  // timing-only A/B knob: the level walk's cost (run once more, discarded)
+      for (int k = 0; k < T; ++k) {
+        const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
+        const int a = ab & 0xffffu, bb = ab >> 16;
+        const int l = max(__builtin_amdgcn_readlane(lastv, a), __builtin_amdgcn_readlane(lastv, bb));
+        lastv = writelane_m0(l + 1, a, lastv);
+        lastv = writelane_m0(l + 1, bb, lastv);
+        lvlv = writelane_m0(l, k, lvlv);
+      }
+      lastv = 0u;
+#endif
       for (int k = 0; k < T; ++k) {
         const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
         const int a = ab & 0xffffu, bb = ab >> 16;
@@ -2215,9 +2231,59 @@ __device__ __forceinline__ T* traj_row(T* p, size_t k, size_t per_step) {
   return p ? p + k * per_step : p;
 }
 
+// Load balancing of a rollout launch (round 4). A rollout keeps each env on one wave for all K
+// steps, so the launch ends with the wave of the heaviest env (a dense or converged flock whose
+// Gauss-Seidel chain is several times the mean), and two or three such envs that land on one SIMD
+// slow each other's latency-bound chains. Before the rollout, rollout_sched orders the envs by
+// their contact-list size (the work of the step's chain grows with it), heaviest first, and wave b
+// of the rollout steps env order[b]: the dispatcher places one wave per SIMD before the second, so
+// the heaviest envs start one per SIMD. An env's results do not depend on its wave. Measured
+// (profiles/r04/abtests/roll_balance): M closed loop 160 -> 148 us per step; the scheduling kernel
+// costs ~6 us per launch (+0.3 us per step of a 20-step rollout, no gain there), so rollouts shorter
+// than kRollBalanceMinSteps keep wave b on env b. Claiming envs by SIMD id at the wave's start
+// (3 device-scope atomics per wave on two counters) balanced as well but cost ~50 us per launch.
+// A/B knob -DMACM_NO_ROLL_BALANCE: wave b steps env b.
+#ifdef MACM_NO_ROLL_BALANCE
+constexpr bool kRollBalance = false;
+#else
+constexpr bool kRollBalance = true;
+#endif
+#ifndef MACM_ROLL_BALANCE_MIN_STEPS
+#define MACM_ROLL_BALANCE_MIN_STEPS 32
+#endif
+constexpr int kRollBalanceMinSteps = MACM_ROLL_BALANCE_MIN_STEPS;
+
+// order[0..E): the envs by descending contact-list size (ccount, clamped to C); one workgroup
+__global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict__ ccount, uint32_t* __restrict__ order,
+                                                     int E, int C) {
+  extern __shared__ uint32_t s_h[];  // [C + 1] envs per list size, then the order's starts
+  __shared__ int s_scan[32];
+  const int tid = threadIdx.x, BS = blockDim.x;
+  for (int i = tid; i <= C; i += BS) s_h[i] = 0u;
+  __syncthreads();
+  for (int e = tid; e < E; e += BS) atomicAdd(&s_h[min((int)ccount[e], C)], 1u);
+  __syncthreads();
+  {  // starts in descending size: thread t owns sizes C - t per .. C - t per - per + 1
+    const int per = (C + 1 + BS - 1) / BS, hi = C - tid * per, lo = max(-1, hi - per);
+    int sum = 0;
+    for (int c = hi; c > lo; --c) sum += (int)s_h[c];
+    int run;
+    spill::block_scan_excl(sum, run, s_scan);
+    for (int c = hi; c > lo; --c) {
+      const int n = (int)s_h[c];
+      s_h[c] = (uint32_t)run;
+      run += n;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += BS) order[atomicAdd(&s_h[min((int)ccount[e], C)], 1u)] = (uint32_t)e;
+}
+
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
 __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_rollout_w64(RolloutArgs<OT> A0) {
   const int nsteps = A0.nsteps;
+  const bool bal = kRollBalance && A0.B.sched && nsteps >= kRollBalanceMinSteps;  // as in launch_roll
+  const int env = bal ? (int)A0.B.sched[blockIdx.x] : (int)blockIdx.x;
   for (int k = 0; k < nsteps; ++k) {
     // each step reads its parameters from the kernel arguments afresh, through a pointer the
     // compiler cannot see through, so nothing derived from them stays live across the loop
@@ -2249,7 +2315,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
                                         pol_in ? pol_in : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
                                         obs, traj_row(A.nbr_out, kr, EN), traj_row(A.rew_out, kr, EN),
                                         traj_row(A.coll_out, kr, EN), traj_row(A.done_out, kr, (size_t)A.P.n_envs),
-                                        blockIdx.x, sl);
+                                        env, sl);
     // the next step reads only what this wave wrote: workgroup scope (this CU's L1 and its XCD's L2)
     // suffices; agent scope would write back and invalidate the L2 every step (5x slower, measured)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -2257,7 +2323,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     if (pol_in) {  // every agent row, as the bots kernel over all E x N rows
       uint8_t* const pol_out = A.traj ? pol_in + EN * abytes : pol_in;
       if (lane < N) {
-        const size_t row = (size_t)blockIdx.x * N + lane;
+        const size_t row = (size_t)env * N + lane;
         if constexpr (MODE == kTdm)
           bot_combat_row(obs + row * (N - 1) * 4, TB.mask_out + row * (N - 1), N, pol_out + row * 4);
         else
@@ -2275,6 +2341,9 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
                         void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
+  if (kRollBalance && B.sched && nsteps >= kRollBalanceMinSteps)
+    hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (P.max_contacts + 1), s,
+                       reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, P.max_contacts);
   hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s,
                      RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol,
                                      traj});

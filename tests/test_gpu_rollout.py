@@ -198,3 +198,29 @@ def test_tdm_closed_loop_rollout_equals_per_step():
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"state[{k}]")
     assert torch.equal(act_a, act_b)
     assert int(a.counters()[1]) > 0
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (600, 64, 40, {"start_spread": 6}),                 # mixed densities: a non-trivial env order
+    (300, 20, 33, {"obs_dtype": torch.float64}),        # the 32-lane instantiation, odd K
+])
+def test_balanced_rollout_equals_per_step(E, N, K, kw):
+    """Rollouts of >= 32 steps (kRollBalanceMinSteps) run env order[b] on wave b, the envs sorted by
+    contact-list size (rollout_sched): open loop, then a closed loop, both against per-step launches."""
+    from gym_macm.bots import flock_actions as bot_actions
+    a = FlockVec(E, n_agents=[N], seed=17, device="cuda:0", **kw)
+    b = FlockVec(E, n_agents=[N], seed=17, device="cuda:0", **kw)
+    acts = flock_actions(K, E, N, 23)
+    for k in range(K):
+        a.step(acts[k])
+    b.rollout(acts)
+    assert_same(a, b, "balanced open-loop rollout")
+    act_a = bot_actions(a.obs)
+    act_b = act_a.clone()
+    for _ in range(K):
+        a.step(act_a)
+        bot_actions(a.obs, out=act_a)
+    b.rollout_bots(act_b, K)
+    assert_same(a, b, "balanced closed-loop rollout")
+    assert torch.equal(act_a, act_b), "the bot's next actions"
+    assert b.status() == 0

@@ -17,4 +17,5 @@ timeout -k 10 400 bash tools/pmc.sh "$OUT/pmc_c4" --env tdm --steps 20 --warmup 
   python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > "$R/$OUT/m_rocprof_bench.json" 2> "$R/$OUT/m_rocprof.err"); st rocprof $?
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/m_driver.json" 2> "$OUT/m_driver.err"; st m_driver $?
 timeout -k 10 400 python bench.py > "$OUT/m_default.json" 2> "$OUT/m_default.err"; st m_default $?
+timeout -k 10 400 python bench.py --policy bots --steps 100 --warmup 300 --no-cpu-baseline > "$OUT/m_bots.json" 2> "$OUT/m_bots.err"; st m_bots $?
 echo ALLDONE | tee -a "$R/$OUT/status.txt"
