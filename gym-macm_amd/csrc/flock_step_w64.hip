@@ -2252,6 +2252,7 @@ constexpr bool kRollBalance = true;
 #define MACM_ROLL_BALANCE_MIN_STEPS 32
 #endif
 constexpr int kRollBalanceMinSteps = MACM_ROLL_BALANCE_MIN_STEPS;
+constexpr int kSchedMaxSize = 4095;
 
 // order[0..E): the envs by descending contact-list size (ccount, clamped to C); one workgroup
 __global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict__ ccount, uint32_t* __restrict__ order,
@@ -2341,9 +2342,14 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
                         void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
-  if (kRollBalance && B.sched && nsteps >= kRollBalanceMinSteps)
-    hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (P.max_contacts + 1), s,
-                       reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, P.max_contacts);
+  if (kRollBalance && B.sched && nsteps >= kRollBalanceMinSteps) {
+    // list sizes above kSchedMaxSize share the top bucket (any order among them is a valid order;
+    // the histogram stays within 16 KB of LDS whatever max_contacts a world was given)
+    const int CB = P.max_contacts < kSchedMaxSize ? P.max_contacts : kSchedMaxSize;
+    hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (CB + 1), s,
+                       reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, CB);
+    if (hipPeekAtLastError() != hipSuccess) return;  // no rollout on a stale order (the caller reports it)
+  }
   hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s,
                      RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol,
                                      traj});

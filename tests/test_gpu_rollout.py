@@ -203,6 +203,7 @@ def test_tdm_closed_loop_rollout_equals_per_step():
 @pytest.mark.parametrize("E,N,K,kw", [
     (600, 64, 40, {"start_spread": 6}),                 # mixed densities: a non-trivial env order
     (300, 20, 33, {"obs_dtype": torch.float64}),        # the 32-lane instantiation, odd K
+    (64, 64, 32, {"max_contacts": 50000}),              # beyond the order's 4096 buckets (200 KB of LDS unclamped)
 ])
 def test_balanced_rollout_equals_per_step(E, N, K, kw):
     """Rollouts of >= 32 steps (kRollBalanceMinSteps) run env order[b] on wave b, the envs sorted by
