@@ -9,6 +9,7 @@ mkdir -p "$OUT"
 args() {
   case $1 in
     mtr) echo "--steps 20 --warmup 5" ;;
+    mstep) echo "--launch step --steps 20 --warmup 5" ;;
     mss) echo "--steps 1000 --warmup 100" ;;
     mbots) echo "--policy bots --steps 100 --warmup 300" ;;
     c2) echo "--envs 1024 --steps 1000 --warmup 100" ;;
