@@ -45,6 +45,7 @@ def assert_traj(ref, traj, ctx):
     (2100, 64, 4, {}),                 # >= 2048 envs: the headline's scalar-sweep instantiation
     (6, 100, 5, {"start_spread": 12}),  # workgroup path: three launches per step
     (1031, 100, 4, {"start_spread": 12}),  # workgroup path in env slices on their own streams
+    (200, 64, 33, {}),                 # >= 32 steps: the envs in the balanced order (rollout_sched)
 ])
 def test_flock_trajectory_equals_per_step(E, N, K, kw):
     cont = kw.get("action_mode") == "continuous"
@@ -69,6 +70,7 @@ def test_flock_trajectory_equals_per_step(E, N, K, kw):
     (32, 20, 8, {"obs_dtype": torch.float64}),
     (4, 100, 4, {"start_spread": 12}),
     (1031, 100, 3, {"start_spread": 12}),
+    (128, 64, 32, {}),  # the balanced order
 ])
 def test_flock_closed_loop_trajectory(E, N, K, kw):
     a = FlockVec(E, n_agents=[N], seed=12, device="cuda:0", start_spread=kw.pop("start_spread", 6), **kw)
@@ -109,7 +111,7 @@ def assert_tdm_state(a, b):
     np.testing.assert_array_equal(a.counters(), b.counters())
 
 
-@pytest.mark.parametrize("teams,K,obs_f64", [([16, 16], 9, False), ([8, 8, 8], 10, True)])
+@pytest.mark.parametrize("teams,K,obs_f64", [([16, 16], 9, False), ([8, 8, 8], 10, True), ([16, 16], 32, False)])
 def test_tdm_trajectory_equals_per_step(teams, K, obs_f64):
     E, N = 48, sum(teams)
     a, b = tdm_pair(teams, E, obs_f64)
