@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-4 box session: the whole GPU suite and the smoke at HEAD (after the added trajectory cases).
+set -u
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"
+OUT=gpurun_out/${1:-r04fin2}
+mkdir -p "$OUT"
+st() { echo "$1 rc=$2" | tee -a "$OUT/status.txt"; [ "$2" -eq 0 ] || exit "$2"; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; st pytest_gpu $?
+timeout -k 10 180 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1; st smoke $?
+echo ALLDONE | tee -a "$OUT/status.txt"
