@@ -101,8 +101,8 @@ struct WorldBuffers {
   int32_t sp_pool;               // pool size S (0: one slot per env, slot = env)
   uint32_t* spill_count;         // [E]       steps taken by the spill step (macm_world_spilled)
   uint32_t* host_status;         // mapped pinned host word: nonzero once any env set a status bit
-  // [E] wave-kernel rollouts: the env order of the launch, heaviest first (flock_step_w64.hip,
-  // rollout_sched); NULL: wave b steps env b
+  // [E] the env order of a launch, heaviest first (flock_step_w64.hip, rollout_sched): wave-kernel
+  // rollouts, and the workgroup step's kernels (flock_step_wg.hip, kWgEnvOrder)
   uint32_t* sched;
 };
 

@@ -2356,6 +2356,13 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
 }
 
 // the same instantiation choice as launch_step_w64 / launch_tdm_step_w64
+// order[0..E): the envs by descending contact-list size (the workgroup step, kWgEnvOrder)
+hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int C, hipStream_t s) {
+  const int CB = C < kSchedMaxSize ? C : kSchedMaxSize;
+  hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (CB + 1), s, ccount, order, E, CB);
+  return hipGetLastError();
+}
+
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
                               int nsteps, unsigned long long astride, int traj) {

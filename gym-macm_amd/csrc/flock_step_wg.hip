@@ -26,6 +26,23 @@
 #include "flock_grid.hpp"
 
 namespace macm {
+hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int C, hipStream_t s);
+
+// The step's env order (round 4): before each step the envs are ordered by contact-list size,
+// heaviest first (launch_env_order, one workgroup), and workgroup b of kernels A, DFS, B and C
+// steps env order[b]. Kernels A and C take several dispatch rounds (more workgroups than fit the
+// chip at once), so the heaviest envs start in the first round instead of ending a late one, and
+// kernel B's heaviest waves start one per SIMD. Any order gives the same results: every env is
+// stepped by exactly one workgroup of each kernel. A/B knob -DMACM_NO_WG_ENV_ORDER: b steps env b.
+#ifdef MACM_NO_WG_ENV_ORDER
+constexpr bool kWgEnvOrder = false;
+#else
+constexpr bool kWgEnvOrder = true;
+#endif
+__device__ __forceinline__ int wg_env(const WorldBuffers& B) {
+  return (kWgEnvOrder && B.sched) ? (int)B.sched[blockIdx.x] : (int)blockIdx.x;
+}
+
 namespace wg {
 
 constexpr int W = 64;
@@ -407,7 +424,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
                                                         uint8_t* __restrict__ done_out) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x;
+  const int e = wg_env(B);
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
   const int N = P.n_agents;
@@ -1063,7 +1080,7 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
 __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x, lane = threadIdx.x, N = P.n_agents;
+  const int e = wg_env(B), lane = threadIdx.x, N = P.n_agents;
   const int tid = lane;  // WSTAMP
   (void)tid;
   if (B.x_nisl[e] != kDfsPending) return;  // kernel A walked it, or the spill step stepped it
@@ -1360,7 +1377,7 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
 __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x, lane = threadIdx.x, N = P.n_agents;
+  const int e = wg_env(B), lane = threadIdx.x, N = P.n_agents;
   const int IS = wg_isl_stride(N);
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
@@ -1602,7 +1619,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                                         uint8_t* __restrict__ done_out) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x;
+  const int e = wg_env(B);
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
   const int N = P.n_agents;
@@ -2149,6 +2166,11 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
                           hipStream_t s) {
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
+  if (kWgEnvOrder && B.sched) {
+    const hipError_t oe =
+        launch_env_order(reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, P.max_contacts, s);
+    if (oe != hipSuccess) return oe;
+  }
   const int N = P.n_agents, la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
   const int ld = wg::wg_layout_d(N, tcap).total;
   if (obs_f64) {

@@ -426,7 +426,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       (!w->wave && (rc = dalloc(w, (float4**)&B.sp_rec, (size_t)SL * N * 3))) ||  // 48-B records
       (SL < n_envs && (rc = dalloc(w, &B.sp_lock, (size_t)SL))) ||
       (rc = dalloc(w, &B.spill_count, (size_t)n_envs)) || (rc = dalloc(w, &w->bad, 1)) ||
-      (w->wave && (rc = dalloc(w, &B.sched, (size_t)n_envs))) ||
+      (rc = dalloc(w, &B.sched, (size_t)n_envs)) ||
       (rc = dalloc(w, &w->mt, (size_t)n_envs * kMtStride)) || (rc = dalloc(w, &w->rmask, (size_t)n_envs))
   ) {
     free_world(w);
@@ -620,7 +620,7 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
   off(S.x_vmid, EN), off(S.x_cout, EN), off(S.x_vout, EN), off(S.x_deg, EN), off(S.x_isolv, IS);
   off(S.x_tab, e0 * tcap), off(S.x_adj, e0 * 2 * tcap), off(S.x_off, e0 * (N + 1)), off(S.x_dfs, e0 * tcap);
   off(S.spill_count, e0);
-  S.sched = nullptr;  // a slice steps env blockIdx.x (rollout scheduling is per world)
+  off(S.sched, e0);  // a slice's order holds slice-local env ids (launch_env_order on the slice)
   if (B.sp_pool == 0) {  // one working-set slot per env: the slice's rows; a pool is shared as it is
     off(S.sp_tab, e0 * C), off(S.sp_adj, e0 * 2 * C), off(S.sp_ord, e0 * C), off(S.sp_cst, e0 * C);
     off(S.sp_cim, e0 * C), off(S.sp_lam, e0 * C);

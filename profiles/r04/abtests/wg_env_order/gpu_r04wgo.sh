@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 box session: the workgroup step's env order (heaviest first): the whole GPU suite on the
+# new library, then the A/B against the same library without it (nowgo) and HEAD.
+set -u
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"
+OUT=gpurun_out/${1:-r04wgo}
+mkdir -p "$OUT"
+st() { echo "$1 rc=$2" | tee -a "$OUT/status.txt"; [ "$2" -eq 0 ] || exit "$2"; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest.log" 2>&1; st pytest $?
+bash tools/ab_r04.sh "$(basename $OUT)/ab" "c3:nowgo,wgo c3bots:nowgo,wgo c5r:nowgo,wgo mtr:head,wgo" > "$OUT/ab.log" 2>&1; st ab $?
+echo ALLDONE | tee -a "$OUT/status.txt"
