@@ -39,6 +39,25 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def _loaded_hip_runtime():
+    """The HIP runtime torch already loaded into this process, opened with RTLD_NOLOAD so that no
+    second copy is ever loaded (a hard-coded soname could load one, and device flags
+    set on it would not reach torch's). Found in /proc/self/maps; refuses if none is loaded."""
+    import ctypes
+    paths = []
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and os.path.basename(parts[-1]).startswith("libamdhip64.so"):
+                paths.append(parts[-1])
+    for p in dict.fromkeys(paths):
+        try:
+            return ctypes.CDLL(p, mode=os.RTLD_NOLOAD | ctypes.RTLD_GLOBAL)
+        except OSError:
+            continue
+    raise SystemExit("--host-wait spin: no HIP runtime (libamdhip64) is loaded in this process")
+
+
 def _cpu_window(step_fn, acts, warmup, steps, budget_s):
     """Run `warmup` untimed steps, then time up to `steps` steps (the GPU leg's window),
     fewer if they would exceed the budget. Returns (timed steps, seconds, warmup run)."""
@@ -163,9 +182,13 @@ def main():
                          "BASELINE config 4: 4096 over 8, config 5: 16384 over 8) instead of --envs per GPU; "
                          "actions are drawn for the whole job, so every env's results are those of a "
                          "single-process run")
-    ap.add_argument("--trajectory", action="store_true",
-                    help="random policy, rollout launch: keep every step's outputs ([K, E, N, ...] buffers, "
-                         "macm_world_rollout_traj), as the reference returns (obs, rewards) from every env.step")
+    ap.add_argument("--outputs", choices=("trajectory", "overwrite"), default="trajectory",
+                    help="random policy, rollout launch: trajectory (default) keeps every step's outputs in "
+                         "[K, E, N, ...] buffers (macm_world_rollout_traj / macm_tdm_rollout_traj), as the reference "
+                         "returns (obs, rewards) from every env.step (mvmnt.py:140); overwrite: every step "
+                         "overwrites one output set, the caller receives only the last step's "
+                         "(macm_world_rollout / macm_tdm_rollout)")
+    ap.add_argument("--trajectory", action="store_true", help="= --outputs trajectory (kept for old scripts)")
     ap.add_argument("--host-wait", choices=("default", "spin"), default="default",
                     help="spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is initialised, so "
                          "the host polls for completion instead of waiting for an interrupt (A/B of the host "
@@ -178,8 +201,7 @@ def main():
                                          else "pmc_tdm_step.json")
 
     if args.host_wait == "spin":
-        import ctypes
-        hip = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)  # torch's HIP runtime (already loaded)
+        hip = _loaded_hip_runtime()
         rc = hip.hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
         if rc != 0:
             raise SystemExit(f"hipSetDeviceFlags(hipDeviceScheduleSpin) failed: {rc}")
@@ -214,8 +236,12 @@ def main():
     else:  # weak: --envs per GPU
         E = args.envs
         e_off = gdist.env_offset(rank, E)
-    if args.trajectory and (args.policy != "random" or args.launch != "rollout" or args.env != "flock"):
-        raise SystemExit("--trajectory times the Flock random-action rollout launch")
+    if args.trajectory:
+        args.outputs = "trajectory"
+    # every step's outputs are what env.step returns; the forms that get them without a trajectory
+    # buffer are the closed loop (the bot consumes each step's obs inside the launch) and one launch
+    # per step (the caller reads each step's outputs between launches)
+    use_traj = args.outputs == "trajectory" and args.policy == "random" and args.launch == "rollout"
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 1 + (0 if strong else rank))
 
@@ -267,8 +293,8 @@ def main():
             world_h.step_raw(loop_ptr, sh_)
             policy()
     rollout = args.launch == "rollout"
-    traj = world_h.trajectory_buffers(K) if args.trajectory else None
-    rname = "macm_world_rollout_traj" if traj is not None else "macm_world_rollout"
+    traj = world_h.trajectory_buffers(K) if use_traj else None
+    rname = ("macm_world_rollout" if args.env == "flock" else "macm_tdm_rollout") + ("_traj" if traj is not None else "")
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}, "
         f"{'one rollout launch' if rollout else 'one launch per step'}")
 
@@ -286,7 +312,7 @@ def main():
                 step(base + w * stride, sh)
         torch.cuda.synchronize(dev)
         if args.env == "flock":
-            world_h.reset_counters()
+            world_h.reset_counters()  # and the reward sums
         spilled0 = world_h.spilled()
         # the events are created (lazily, at their first record) before the timed region
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -319,6 +345,9 @@ def main():
     status = int(gdist.reduce_counters([world_h.status()], device=red_dev, op="max")[0])
     cnt = gdist.reduce_counters(world_h.counters(), device=red_dev)
     spilled = int(gdist.reduce_counters([spilled], device=red_dev)[0])
+    # Σreward (float64): every rank's per-env sums gathered and added in global env
+    # order, so the total is bit-identical to a single-process run of the job at any rank count
+    reward_sum = gdist.reduce_reward_sums(world_h.reward_sums()[0], device=red_dev) if args.env == "flock" else None
     elapsed = gdist.reduce_max(elapsed, device=red_dev)
     total_agent_steps = (args.total_envs if strong else world * E) * N * K
     if args.env == "flock":
@@ -354,8 +383,10 @@ def main():
             kname = kname.replace("float", "double").replace("double, true>", "double, false>")
         spl = K if (rollout and N <= 64) else 1  # env steps per launch of the priced kernel
         traffic_src = None
+        oform = "trajectory" if traj is not None else "overwrite"
         if (tj and tj.get("envs") == E and tj.get("agents") == N and tj.get("kernel") == kname
-                and tj.get("policy", "random") == args.policy and tj.get("steps_per_launch", 1) == spl):
+                and tj.get("policy", "random") == args.policy and tj.get("steps_per_launch", 1) == spl
+                and (spl == 1 or args.policy != "random" or tj.get("outputs", "overwrite") == oform)):
             if tj.get("lib_sha256") and tj["lib_sha256"] == lib_sha256():
                 # per step (a rollout launch's bytes over its steps), like achieved
                 traffic = tj.get("hbm_bytes_per_launch") / tj.get("steps_per_launch", 1)
@@ -419,8 +450,10 @@ def main():
                 # (mvmnt.py:140); the plain rollout launch overwrites its outputs every step
                 "outputs": ("every step's ([K, E, N, ...] trajectory buffers)" if traj is not None
                             else "every step's (one launch per step)" if not rollout
-                            else "the last step's (each step overwrites them; counters cover all K steps); "
-                                 "--trajectory keeps every step's"),
+                            else "every step's obs consumed by the device bot inside the launch; the caller "
+                                 "receives the last step's" if args.policy == "bots"
+                            else "overwrite: the last step's (each step overwrites them; counters cover all K "
+                                 "steps)"),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -439,7 +472,8 @@ def main():
         }
         if args.env == "flock":
             out["counters"] = {"agent_steps": int(cnt[0]), "collided_agent_steps": int(cnt[1]),
-                               "positive_reward_agent_steps": int(cnt[2]), "done_env_steps": int(cnt[3])}
+                               "positive_reward_agent_steps": int(cnt[2]), "done_env_steps": int(cnt[3]),
+                               "reward_sum": reward_sum}
         else:
             out["counters"] = {"alive_agent_steps": int(cnt[0]), "melee_attacks": int(cnt[1]),
                                "deaths": int(cnt[2]), "done_env_steps": int(cnt[3])}

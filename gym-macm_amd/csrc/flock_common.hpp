@@ -65,6 +65,7 @@ struct WorldBuffers {
   uint8_t* done;       // [E]
   int32_t* status;     // [E]      MACM_ST_* bits
   unsigned long long* env_counters;  // [E, 4] per-env accumulators (see macm_world_counters)
+  double* env_rsum;              // [E]      per-env reward sum, float64 (macm_world_reward_sums)
   unsigned long long* stamps;    // [E, 16] diagnostic build only (MACM_STAMPS), else NULL
   float2* scratch;               // [E, tcap] list-order impulses (workgroup kernel only)
   // Workgroup path, split step (flock_step_wg_a -> flock_solve_wg -> flock_step_wg_c), per env:
@@ -354,6 +355,64 @@ constexpr int kOut = 0, kState = 1;
 
 __device__ __forceinline__ int wave_max(int v) {  // over all 64 lanes, wave-uniform
   return __builtin_amdgcn_readlane(wave_prefix_max(v), 63);
+}
+
+// ---- the reward sum (macm_world_reward_sums) -----------------------------------
+// One env-step's rewards are summed as float64 values of the float32 rewards the step writes, in a
+// fixed order, so the per-env total is bit-stable and the host restates it exactly
+// (gym_macm.dist.pairwise_reward_sum): pairwise over the agent slots 0 .. P - 1 with +0.0 in the
+// slots of lanes >= N, P = 64 * 2^ceil(log2(waves of the block)). That is an xor butterfly within a
+// wave — lane 0 holds ((r0 + r1) + (r2 + r3)) + ... — and the waves' sums pairwise in the same way.
+// Each level here pairs partial sums whose pairing equals the xor butterfly's (every lane of a group
+// holds its group's sum once the level before has run; IEEE addition is commutative), by DPP
+// within rows and lane reads across them, with no LDS round trip.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// Pairwise sum of the wave's 64 values (the whole wave active); wave-uniform result.
+__device__ __forceinline__ double wave_pairwise_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1, 0, 3, 2]: r0 + r1
+  v += dpp_f64<0x4E>(v);   // quad_perm [2, 3, 0, 1]: (r0 + r1) + (r2 + r3)
+  v += dpp_f64<0x141>(v);  // row_half_mirror: lane i <- 7 - i, the other quad's sum
+  v += dpp_f64<0x140>(v);  // row_mirror: lane i <- 15 - i, the other half-row's sum
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+// The same over a block of blockDim.x / 64 <= 16 waves (every thread calls it; s_tmp: 16 doubles of
+// LDS, free on entry and on return); the result is valid in thread 0.
+__device__ __forceinline__ double block_pairwise_sum(double v, double* s_tmp) {
+  v = wave_pairwise_sum(v);
+  const int nw = blockDim.x >> 6, wid = threadIdx.x >> 6;
+  if (nw == 1) return v;
+  if ((threadIdx.x & 63) == 0) s_tmp[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n2 = 1;
+    while (n2 < nw) n2 <<= 1;
+    for (int q = nw; q < n2; ++q) s_tmp[q] = 0.0;
+    for (int h = 1; h < n2; h <<= 1)
+      for (int q = 0; q + h < n2; q += 2 * h) s_tmp[q] = s_tmp[q] + s_tmp[q + h];
+    v = s_tmp[0];
+  }
+  __syncthreads();
+  return v;
+}
+
+// env e's total += one step's sum, as a float64 atomic add without return: the wave does not wait
+// for it (a load-add-store held 2 VGPRs across the step's observation and spilled in the rollout
+// kernel) and the adds of one wave to one address take effect in program order (per-location
+// coherence), so the total is the steps' sums added in step order. No denormal arises (the sums are
+// of float32 rewards in [-1, 1]). Every writer of env_rsum uses it.
+__device__ __forceinline__ void add_reward_sum(const WorldBuffers& B, int e, double v) {
+  unsafeAtomicAdd(B.env_rsum + e, v);
 }
 
 // Per-env CPython MT19937 streams in HBM for device-side resets (csrc/env_reset.hip).

@@ -127,6 +127,7 @@ __device__ __forceinline__ int block_scan_excl(int v, int& excl, int* s_scan) {
 constexpr unsigned kSlotSpins = 1u << 17;  // x s_sleep 127 (~8k cycles): ~0.5-1 s
 __device__ __forceinline__ int acquire_slot(const WorldBuffers& B, int e, int* s_slot) {
   if (B.sp_pool == 0) return e;
+  if (B.sp_pool < 0) return -1;  // MACM_DEBUG_SPILL_FAIL: the pool is never free (test hook)
   if (threadIdx.x == 0) {
     const int S = B.sp_pool;
     int got = -1;
@@ -147,8 +148,23 @@ __device__ __forceinline__ int acquire_slot(const WorldBuffers& B, int e, int* s
   return *s_slot;
 }
 
+// An env that found no free slot is not stepped (MACM_ST_SPILL_WAIT): its bodies keep their
+// start-of-step state, and so must its contact list, which the next step (or step k + 1 of a
+// rollout) reads from the other buffer. Copies list `cur` of env e into `cur ^ 1`; every thread of
+// the block calls it (without it the env resumed from a list two steps old).
+__device__ __forceinline__ void keep_lists(const StepParams& P, const WorldBuffers& B, int e, int cur) {
+  const int C = P.max_contacts, nxt = cur ^ 1;
+  const int M = B.ccount[cur][e];
+  const size_t row = (size_t)e * C;
+  for (int k = threadIdx.x; k < M; k += blockDim.x) {
+    B.cab[nxt][row + k] = B.cab[cur][row + k];
+    B.cimp[nxt][row + k] = B.cimp[cur][row + k];
+  }
+  if (threadIdx.x == 0) B.ccount[nxt][e] = M;
+}
+
 __device__ __forceinline__ void release_slot(const WorldBuffers& B, int slot) {
-  if (B.sp_pool == 0) return;
+  if (B.sp_pool <= 0) return;
   __builtin_amdgcn_s_waitcnt(0);  // this thread's stores are done (vmcnt / lgkmcnt 0)
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -233,7 +249,8 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   // the HBM working set of this env's slot, capacity C (touching contacts are a subset of the list);
   // held_slot >= 0: the caller took it before committing anything (the workgroup TDM step)
   const int slot = held_slot >= 0 ? held_slot : acquire_slot(B, e, s_misc + 7);
-  if (slot < 0) {  // the pool stayed full for ~1 s: not stepped, reported
+  if (slot < 0) {  // the pool stayed full for ~1 s: not stepped (lists included), reported
+    keep_lists(P, B, e, cur);
     if (tid == 0) {
       B.status[e] |= MACM_ST_SPILL_WAIT;
       report_status(B, MACM_ST_SPILL_WAIT);
@@ -773,6 +790,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     int dummy;
     const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
     const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
+    const double rsum = block_pairwise_sum((double)rew, reinterpret_cast<double*>(s_scan));  // thread 0
     if (act) {
       B.pos[ag] = make_float2(cx, cy);
       B.vel[ag] = make_float2(vx, vy);
@@ -797,6 +815,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       ec[1] += (unsigned long long)ncoll;
       ec[2] += (unsigned long long)npos;
       ec[3] += (unsigned long long)dn;
+      add_reward_sum(B, e, rsum);
       if (B.spill_count) B.spill_count[e] += 1u;
     }
     release_slot(B, slot);  // the observation above reads recs (HBM when !RECS_LDS)

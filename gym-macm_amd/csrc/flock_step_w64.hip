@@ -1193,6 +1193,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       __shared__ int s_slot;
       const int slot = spill::acquire_slot(B, e, &s_slot);
       if (slot < 0) {
+        spill::keep_lists(P, B, e, cur);
         if (lane == 0) {
           B.status[e] |= MACM_ST_SPILL_WAIT;
           report_status(B, MACM_ST_SPILL_WAIT);
@@ -2121,9 +2122,11 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   const unsigned long long mst1 = __ballot(status & 1), mst2 = __ballot(status & 2), mst4 = __ballot(status & 4);
   unsigned long long c1 = 0ull, c2 = 0ull;
   int alive_teams = 0, last_team = -1;
+  double rsum = 0.0;
   if constexpr (!kT) {
     c1 = __popcll(__ballot(act && coll));        // collided agent-steps
     c2 = __popcll(__ballot(act && rew > 0.0f));  // positive-reward agent-steps
+    rsum = wave_pairwise_sum((double)rew);  // lanes >= N: rew = +0.0
   } else {
     c1 = __popcll(att_m);               // melee attacks
     c2 = __popcll(alive0_m & ~livem);   // deaths
@@ -2164,6 +2167,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     ulonglong2* ec = reinterpret_cast<ulonglong2*>(B.env_counters + (size_t)e * 4);
     ec[0] = make_ulonglong2(ctr[0] + c0, ctr[1] + c1);
     ec[1] = make_ulonglong2(ctr[2] + c2, ctr[3] + (unsigned long long)dn);
+    if constexpr (!kT) add_reward_sum(B, e, rsum);
   }
   STAMP(13);
 #ifdef MACM_TIMELINE
@@ -2262,7 +2266,7 @@ __global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict
   const int tid = threadIdx.x, BS = blockDim.x;
   for (int i = tid; i <= C; i += BS) s_h[i] = 0u;
   __syncthreads();
-  for (int e = tid; e < E; e += BS) atomicAdd(&s_h[min((int)ccount[e], C)], 1u);
+  for (int e = tid; e < E; e += BS) atomicAdd(&s_h[max(0, min((int)ccount[e], C))], 1u);
   __syncthreads();
   {  // starts in descending size: thread t owns sizes C - t per .. C - t per - per + 1
     const int per = (C + 1 + BS - 1) / BS, hi = C - tid * per, lo = max(-1, hi - per);
@@ -2277,7 +2281,7 @@ __global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict
     }
   }
   __syncthreads();
-  for (int e = tid; e < E; e += BS) order[atomicAdd(&s_h[min((int)ccount[e], C)], 1u)] = (uint32_t)e;
+  for (int e = tid; e < E; e += BS) order[atomicAdd(&s_h[max(0, min((int)ccount[e], C))], 1u)] = (uint32_t)e;
 }
 
 template <int MODE, int NCAP, typename OT, bool SCAL = false>

@@ -400,7 +400,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
       (rc = dalloc(w, &B.cimp[0], (size_t)n_envs * C)) || (rc = dalloc(w, &B.cimp[1], (size_t)n_envs * C)) ||
       (rc = dalloc(w, &B.step_count, (size_t)n_envs)) || (rc = dalloc(w, &B.time_passed, (size_t)n_envs)) ||
       (rc = dalloc(w, &B.done, (size_t)n_envs)) || (rc = dalloc(w, &B.status, (size_t)n_envs)) ||
-      (rc = dalloc(w, &B.env_counters, (size_t)n_envs * 4))
+      (rc = dalloc(w, &B.env_counters, (size_t)n_envs * 4)) || (rc = dalloc(w, &B.env_rsum, (size_t)n_envs))
 #ifdef MACM_STAMPS
       || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 32))
 #endif
@@ -440,6 +440,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   }
   hipError_t e = hipMemcpy(B.tidx, tidx.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemset(B.env_counters, 0, (size_t)n_envs * 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(B.env_rsum, 0, (size_t)n_envs * sizeof(double));
   if (e == hipSuccess) e = hipMemset(B.ccount[0], 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.status, 0, sizeof(int32_t) * n_envs);
   if (e == hipSuccess) e = hipMemset(B.spill_count, 0, sizeof(uint32_t) * n_envs);
@@ -614,7 +615,7 @@ static WorldBuffers slice_buffers(const WorldBuffers& B, size_t e0, size_t N, si
   off(S.targets, e0 * T);
   for (int c = 0; c < 2; ++c) off(S.ccount[c], e0), off(S.cab[c], e0 * C), off(S.cimp[c], e0 * C);
   off(S.step_count, e0), off(S.time_passed, e0), off(S.done, e0), off(S.status, e0);
-  off(S.env_counters, e0 * 4), off(S.stamps, e0 * 32);
+  off(S.env_counters, e0 * 4), off(S.env_rsum, e0), off(S.stamps, e0 * 32);
   off(S.scratch, e0 * tcap), off(S.x_cst, e0 * tcap), off(S.x_cimp, e0 * tcap), off(S.x_ord, e0 * tcap);
   off(S.x_ic, IS), off(S.x_nlvl, e0), off(S.x_ib, IS), off(S.x_ibod, EN), off(S.x_nisl, e0);
   off(S.x_vmid, EN), off(S.x_cout, EN), off(S.x_vout, EN), off(S.x_deg, EN), off(S.x_isolv, IS);
@@ -933,6 +934,26 @@ int macm_world_reset_counters(macm_world* w, void* stream) {
   DeviceGuard g(w->device);
   HIP_TRY(hipMemsetAsync(w->B.env_counters, 0, (size_t)w->P.n_envs * 4 * sizeof(unsigned long long),
                          (hipStream_t)stream));
+  HIP_TRY(hipMemsetAsync(w->B.env_rsum, 0, (size_t)w->P.n_envs * sizeof(double), (hipStream_t)stream));
+  return MACM_OK;
+}
+
+// Per-env reward sums (flock_common.hpp: each step's float32 rewards as float64, pairwise over the
+// agent slots, added to the env's total in step order) and their sum over envs in env order, starting
+// from +0.0: a fixed order throughout, so the total is bit-stable for any launch form or env slicing.
+int macm_world_reward_sums(macm_world* w, double* per_env, double* total, void* stream) {
+  if (!w || (!per_env && !total)) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  std::vector<double> h((size_t)w->P.n_envs);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(h.data(), w->B.env_rsum, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (per_env) memcpy(per_env, h.data(), h.size() * sizeof(double));
+  if (total) {
+    double acc = 0.0;
+    for (double v : h) acc += v;
+    *total = acc;
+  }
   return MACM_OK;
 }
 
@@ -949,15 +970,18 @@ int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream) {
   return MACM_OK;
 }
 
-// MACM_DEBUG_SPILL_POOL (a test hook): share `pool` of the slots allocated at creation; a call
-// without the flag brings back the world's own pool (or one slot per env). The locks are cleared
+// MACM_DEBUG_SPILL_POOL (a test hook): share `pool` of the slots allocated at creation;
+// MACM_DEBUG_SPILL_FAIL: no slot is ever free (every spilling env ends SPILL_WAIT); a call
+// without either flag brings back the world's own pool (or one slot per env). The locks are cleared
 // only after the device has finished every step that could hold one.
 extern "C++" template <typename Wt>
 static int set_spill_pool(Wt* w, int32_t flags, int pool) {
   const bool want = (flags & MACM_DEBUG_SPILL_POOL) != 0;
+  const bool never = (flags & MACM_DEBUG_SPILL_FAIL) != 0;
+  if (want && never) return fail(MACM_E_INVALID, "SPILL_POOL and SPILL_FAIL exclude each other");
   if (want && (pool < 1 || pool > w->slots_alloc))
     return fail(MACM_E_INVALID, "SPILL_POOL: 1 <= slots <= the " + std::to_string(w->slots_alloc) + " allocated");
-  const int target = want ? pool : w->pool0;
+  const int target = never ? -1 : want ? pool : w->pool0;  // -1: acquire_slot always fails
   if (target == w->B.sp_pool) return MACM_OK;
   DeviceGuard g(w->device);
   HIP_TRY(hipDeviceSynchronize());
@@ -973,7 +997,7 @@ int macm_world_set_debug(macm_world* w, int32_t flags) {
   if (!w) return fail(MACM_E_INVALID, "world is NULL");
   const int pool = (flags & MACM_DEBUG_SPILL_POOL) ? (flags >> 8) : 0;
   flags &= 0xff;
-  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SWEEP_CELLS | MACM_DEBUG_SWEEP_ALL_PAIRS | MACM_DEBUG_SPILL_POOL))
+  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SWEEP_CELLS | MACM_DEBUG_SWEEP_ALL_PAIRS | MACM_DEBUG_SPILL_POOL | MACM_DEBUG_SPILL_FAIL))
     return fail(MACM_E_INVALID, "unknown debug flag");
   if ((flags & MACM_DEBUG_SWEEP_CELLS) && (flags & MACM_DEBUG_SWEEP_ALL_PAIRS))
     return fail(MACM_E_INVALID, "SWEEP_CELLS and SWEEP_ALL_PAIRS exclude each other");
@@ -1065,10 +1089,11 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   w->cur = 0;
   w->wave = N <= 64;
   const int C = N * (N - 1) / 2;  // every pair: the list never overflows
-  // spill working-set slots. The wave kernel (N <= 64) hands a crowded env to the spill step after
-  // it has committed the step's combat state, so it gets one slot per env (<= 100 KB each: a pool
-  // wait must never leave an env half-stepped); the workgroup step takes its slot before committing
-  const int64_t SL = N <= 64 ? (int64_t)n_envs : default_capacity(N, n_envs, C, free_bytes).slots;
+  // spill working-set slots from the device budget, as Flock's: one per env when they fit, else a
+  // pool. Both TDM callers take their slot before committing anything of the step (the wave
+  // kernel's hand-over and the workgroup step), so a pool wait leaves an env wholly unstepped,
+  // never half-stepped (N <= 64 used to take one slot per env regardless of memory)
+  const int64_t SL = default_capacity(N, n_envs, C, free_bytes).slots;
   StepParams& P = w->P;
   memset(&P, 0, sizeof(P));
   P.n_envs = n_envs;
@@ -1476,8 +1501,8 @@ int macm_tdm_set_debug(macm_tdm* w, int32_t flags) {
   if (!w) return fail(MACM_E_INVALID, "world is NULL");
   const int pool = (flags & MACM_DEBUG_SPILL_POOL) ? (flags >> 8) : 0;
   flags &= 0xff;
-  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SPILL_POOL))
-    return fail(MACM_E_INVALID, "unknown debug flag (TDM: FORCE_SPILL, SPILL_POOL)");
+  if (flags & ~(MACM_DEBUG_FORCE_SPILL | MACM_DEBUG_SPILL_POOL | MACM_DEBUG_SPILL_FAIL))
+    return fail(MACM_E_INVALID, "unknown debug flag (TDM: FORCE_SPILL, SPILL_POOL, SPILL_FAIL)");
   if (int rc = set_spill_pool(w, flags, pool)) return rc;
   w->P.force_spill = (flags & MACM_DEBUG_FORCE_SPILL) ? 1 : 0;
   return MACM_OK;

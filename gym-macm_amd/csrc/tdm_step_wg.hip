@@ -104,6 +104,7 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
   __shared__ int s_slot;
   const int slot = spill::acquire_slot(B, e, &s_slot);
   if (slot < 0) {
+    spill::keep_lists(P, B, e, cur);
     if (tid == 0) {
       B.status[e] |= MACM_ST_SPILL_WAIT;
       report_status(B, MACM_ST_SPILL_WAIT);

@@ -19,6 +19,7 @@ DEBUG_FORCE_SPILL = 1
 DEBUG_SWEEP_CELLS = 2
 DEBUG_SWEEP_ALL_PAIRS = 4
 DEBUG_SPILL_POOL = 8  # | slots << 8
+DEBUG_SPILL_FAIL = 16  # no spill slot is ever free (SPILL_WAIT test hook)
 E_INVALID, E_OVERFLOW = -1, -5
 
 _ERRORS = {
@@ -201,6 +202,7 @@ SIGNATURES = {
     "macm_world_status": (c_int, [c_void_p, POINTER(c_int32), c_void_p]),
     "macm_world_counters": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_world_reset_counters": (c_int, [c_void_p, c_void_p]),
+    "macm_world_reward_sums": (c_int, [c_void_p, c_void_p, POINTER(c_double), c_void_p]),
     "macm_world_spilled": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_world_set_debug": (c_int, [c_void_p, c_int32]),
     "macm_tdm_config_default": (c_int, [POINTER(MacmTdmConfig)]),

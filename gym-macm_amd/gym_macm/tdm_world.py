@@ -198,6 +198,13 @@ class TdmWorld:
                              "world's device")
         return self._traj_call(self.L.macm_tdm_rollout_bots_traj, "macm_tdm_rollout_bots_traj", actions, K, traj)
 
+    def rollout_traj_raw(self, actions_ptr: int, n_steps: int, traj: dict, stream_handle: int) -> None:
+        """Minimal-overhead trajectory rollout for timed loops (no validation); ``traj`` from
+        trajectory_buffers(n_steps)."""
+        out = _abi.MacmTdmOutputs(*[_ptr(traj.get(k)) for k in self._TRAJ_KEYS])
+        self.L.macm_tdm_rollout_traj(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(out),
+                                     ctypes.c_void_p(stream_handle))
+
     def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
         """Minimal-overhead rollout for timed loops (no validation)."""
         self.L.macm_tdm_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),
@@ -296,7 +303,8 @@ class TdmWorld:
 
     def set_debug(self, flags: int) -> None:
         """Test hooks (macm_tdm_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the spill
-        step; DEBUG_SPILL_POOL | slots << 8 shares that many working-set slots."""
+        step; DEBUG_SPILL_POOL | slots << 8 shares that many working-set slots; DEBUG_SPILL_FAIL makes
+        every slot request fail (the env is left unstepped with ST_SPILL_WAIT)."""
         _abi.check(self.L.macm_tdm_set_debug(self.h, int(flags)), "macm_tdm_set_debug")
 
     def counters(self) -> np.ndarray:

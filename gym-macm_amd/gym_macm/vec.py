@@ -118,3 +118,7 @@ class FlockVec(object):
 
     def counters(self):
         return self.world.counters()
+
+    def reward_sums(self):
+        """(per-env reward totals [E] float64, their sum in env order); World.reward_sums."""
+        return self.world.reward_sums()

@@ -336,6 +336,16 @@ class World:
         _abi.check(self.L.macm_world_counters(self.h, out, self._stream()), "macm_world_counters")
         return np.array(list(out), np.int64)
 
+    def reward_sums(self):
+        """(per-env reward totals [E] float64, their sum in env order) accumulated since creation or
+        reset_counters, in the device's fixed order (macm_world_reward_sums; restated on the host by
+        gym_macm.dist.pairwise_reward_sum). Synchronises the stream."""
+        per_env = np.zeros((self.E,), np.float64)
+        tot = ctypes.c_double()
+        _abi.check(self.L.macm_world_reward_sums(self.h, ctypes.c_void_p(per_env.ctypes.data), ctypes.byref(tot),
+                                                 self._stream()), "macm_world_reward_sums")
+        return per_env, float(tot.value)
+
     def reset_counters(self) -> None:
         _abi.check(self.L.macm_world_reset_counters(self.h, self._stream()), "macm_world_reset_counters")
 
@@ -348,7 +358,9 @@ class World:
     def set_debug(self, flags: int) -> None:
         """Test hooks (macm_world_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the
         spill step; DEBUG_SWEEP_CELLS / DEBUG_SWEEP_ALL_PAIRS pick the workgroup path's pair sweep
-        regardless of N (default: strip cells at N >= 512)."""
+        regardless of N (default: strip cells from N = 256); DEBUG_SPILL_POOL | slots << 8 shares
+        that many working-set slots; DEBUG_SPILL_FAIL makes every slot request fail (the env is left
+        unstepped with ST_SPILL_WAIT)."""
         _abi.check(self.L.macm_world_set_debug(self.h, int(flags)), "macm_world_set_debug")
 
     def check_status(self) -> None:

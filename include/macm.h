@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 7
+#define MACM_ABI_VERSION 8
 
 enum {
   MACM_OK = 0,
@@ -75,13 +75,15 @@ enum {
 };
 
 /* macm_world_set_debug / macm_tdm_set_debug flags (test hooks; 0 = product behaviour; TDM takes
- * FORCE_SPILL and SPILL_POOL). */
+ * FORCE_SPILL, SPILL_POOL and SPILL_FAIL). */
 enum {
   MACM_DEBUG_FORCE_SPILL = 1,     /* every env takes the spill step (parity tests of that path)  */
   MACM_DEBUG_SWEEP_CELLS = 2,     /* N > 64: pair sweep over strip cells at any N (else N >= 512) */
   MACM_DEBUG_SWEEP_ALL_PAIRS = 4, /* N > 64: all-pairs pair sweep at any N                        */
-  MACM_DEBUG_SPILL_POOL = 8       /* the spill working set as a pool of (flags >> 8) slots, at most
+  MACM_DEBUG_SPILL_POOL = 8,      /* the spill working set as a pool of (flags >> 8) slots, at most
                                      the slots allocated (pooled-slot tests at small E)            */
+  MACM_DEBUG_SPILL_FAIL = 16      /* no spill slot is ever free: every env that needs the spill step
+                                     is left unstepped with MACM_ST_SPILL_WAIT (ABI 8 test hook)   */
 };
 
 /*
@@ -397,7 +399,19 @@ int macm_world_status(macm_world* w, int32_t* status_or, void* stream);
  *   in multi-GPU runs. reset_counters zeroes them.
  */
 int macm_world_counters(macm_world* w, int64_t out[4], void* stream);
-int macm_world_reset_counters(macm_world* w, void* stream);
+int macm_world_reset_counters(macm_world* w, void* stream);  /* also zeroes the reward sums */
+
+/*
+ * The rewards' sum (Σ of get_rewards' values, mvmnt.py:160-179), in float64 and
+ * in a fixed order so that it is bit-stable (ABI 8): each step's float32 rewards are summed as
+ * float64 pairwise over the agent slots 0 .. P-1 (P = 64 * 2^ceil(log2(ceil(N / 64))), +0.0 past N:
+ * ((r0 + r1) + (r2 + r3)) + ...), that sum is added to the env's total in step order, and `total`
+ * is the envs' totals summed in env order from +0.0. per_env: host double [E] or NULL; total: host
+ * double or NULL (not both NULL). Accumulated by every step since creation or reset_counters;
+ * synchronises `stream`. Multi-GPU: gather the per-env totals and sum them in global env order
+ * (gym_macm.dist.reduce_reward_sums), which gives the single-process total at any rank count.
+ */
+int macm_world_reward_sums(macm_world* w, double* per_env, double* total, void* stream);
 
 /* Env-steps taken by the spill step since creation (dense worlds; synchronises `stream`). */
 int macm_world_spilled(macm_world* w, int64_t* env_steps, void* stream);

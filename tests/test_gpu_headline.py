@@ -11,7 +11,9 @@ restatement of gym_macm/envs/mvmnt.py:81-140 over b2lite) steps all 4096 envs wi
     sleep clocks, the ordered contact list with its warm-start impulses, step count, time) bit-exact;
   * the last step's rewards, neighbour ids, collision flags (bit-exact) and observations (float32 of
     the oracle's float64, <= 1 ulp) of every agent;
-  * the world's counters over the K timed steps = the oracle's per-step outputs summed over them.
+  * the world's counters over the K timed steps = the oracle's per-step outputs summed over them,
+    and the reward sums (per env and in total, float64) = the oracle's rewards summed in the
+    device's fixed order (gym_macm.dist.pairwise_reward_sum), bit for bit.
 
 The closed loop (`--policy bots`, macm_world_rollout_bots with the device bots.flock) is pinned the
 same way, the oracle driven by the reference's bot (tests/parity.py flock_bot) on its own
@@ -25,6 +27,7 @@ from parity import assert_state_equal, f32_obs_mismatch, flock_bot, oracle_for
 pytestmark = pytest.mark.gpu
 
 from gym_macm.bots import flock_actions  # noqa: E402
+from gym_macm.dist import env_order_sum, pairwise_reward_sum  # noqa: E402
 from gym_macm.settings import flockSettings, to_config  # noqa: E402
 from gym_macm.vec import FlockVec  # noqa: E402
 
@@ -45,6 +48,12 @@ def check_last_outputs(vec, r):
     f32_obs_mismatch(vec.obs.cpu().numpy(), r["obs"])
 
 
+def check_reward_sums(vec, rs):
+    per_env, total = vec.reward_sums()
+    np.testing.assert_array_equal(per_env, rs, err_msg="per-env reward sums")
+    assert total == env_order_sum(rs)
+
+
 def test_headline_rollout_launch_all_envs_match_oracle():
     vec = FlockVec(E, n_agents=[N], seed=SEED, device="cuda:0")
     gen = torch.Generator(device="cuda:0")
@@ -58,14 +67,17 @@ def test_headline_rollout_launch_all_envs_match_oracle():
     a = acts.cpu().numpy()
     orc = oracle()
     tot = np.zeros(4, np.int64)
+    rs = np.zeros(E, np.float64)
     for k in range(W + K):
         r = orc.step(a[k], n_threads=THREADS)
         if k >= W:
             tot += [E * N, int(r["collided"].sum()), int((r["reward"] > 0).sum()), int(r["done"].sum())]
+            rs += pairwise_reward_sum(r["reward"])
     assert vec.status() == 0
     assert_state_equal(vec.get_state(), orc.get_state(vec.world.C), "after the timed launch")
     check_last_outputs(vec, r)
     np.testing.assert_array_equal(vec.counters(), tot)
+    check_reward_sums(vec, rs)
     assert tot[1] > 0
 
 
@@ -81,15 +93,18 @@ def test_headline_closed_loop_launch_all_envs_match_oracle():
     orc = oracle()
     obs, _ = orc.observe()
     tot = np.zeros(4, np.int64)
+    rs = np.zeros(E, np.float64)
     for k in range(W + K):
         act = flock_bot(obs.astype(np.float32).astype(np.float64))
         r = orc.step(act, n_threads=THREADS)
         obs = r["obs"]
         if k >= W:
             tot += [E * N, int(r["collided"].sum()), int((r["reward"] > 0).sum()), int(r["done"].sum())]
+            rs += pairwise_reward_sum(r["reward"])
     assert vec.status() == 0
     assert_state_equal(vec.get_state(), orc.get_state(vec.world.C), "after the closed-loop launch")
     check_last_outputs(vec, r)
     np.testing.assert_array_equal(vec.counters(), tot)
+    check_reward_sums(vec, rs)
     np.testing.assert_array_equal(loop.cpu().numpy(), flock_bot(obs.astype(np.float32).astype(np.float64)),
                                   err_msg="the bot's next actions")

@@ -1,7 +1,8 @@
 """HIP path vs the CPU oracle, through the C-ABI (libmacm_hip.so).
 
 Bar: bit-exact for positions, velocities, angles, fat AABBs, sleep clocks, the
-ordered contact list with warm-start impulses, neighbour ids, rewards and done;
+ordered contact list with warm-start impulses, neighbour ids, rewards and done, and the
+reward sums (per env and in total, in the device's fixed float64 order) of every rollout;
 observations (float32) equal the oracle's f64 values rounded to f32, with at most
 1 ulp allowed where double atan2/sin/cos of ocml and glibc round differently."""
 import numpy as np
@@ -13,6 +14,7 @@ from parity import assert_state_equal, f32_obs_mismatch, oracle_for
 
 pytestmark = pytest.mark.gpu
 
+from gym_macm.dist import env_order_sum, pairwise_reward_sum  # noqa: E402
 from gym_macm.settings import flockSettings, to_config  # noqa: E402
 from gym_macm.vec import FlockVec  # noqa: E402
 
@@ -50,10 +52,13 @@ def check_rollout(vec, orc, steps, rng, state_every=1, actions_fn=None, obs_f64=
     np.testing.assert_array_equal(vec.nbr_id.cpu().numpy(), n0)
     obs_check(vec.obs.cpu().numpy(), o0, obs_f64, "reset")
     ulp_total = 0
+    vec.world.reset_counters()
+    rs = np.zeros(E, np.float64)  # the reward sums in the device's order (macm_world_reward_sums)
     for t in range(steps):
         a = actions_fn(t) if actions_fn else rand_actions(rng, E, N)
         obs, nbr, rew, done = vec.step(torch.from_numpy(a).cuda())
         r = orc.step(a)
+        rs += pairwise_reward_sum(r["reward"])
         np.testing.assert_array_equal(rew.cpu().numpy(), r["reward"].astype(np.float32), err_msg=f"reward step {t}")
         np.testing.assert_array_equal(nbr.cpu().numpy(), r["nbr_id"], err_msg=f"nbr step {t}")
         np.testing.assert_array_equal(done.cpu().numpy(), r["done"], err_msg=f"done step {t}")
@@ -62,6 +67,9 @@ def check_rollout(vec, orc, steps, rng, state_every=1, actions_fn=None, obs_f64=
         if (t + 1) % state_every == 0 or t == steps - 1:
             assert_state_equal(vec.get_state(), orc.get_state(C), f"step {t}")
     assert vec.status() == 0
+    per_env, total = vec.reward_sums()
+    np.testing.assert_array_equal(per_env, rs, err_msg="per-env reward sums")
+    assert total == env_order_sum(rs), "reward total"
     return ulp_total
 
 

@@ -37,3 +37,23 @@ def test_bad_buffers_raise(key, t):
     b[key] = t
     with pytest.raises(ValueError):
         check_traj(b, SPEC, 3, DEV, KEYS)
+
+
+def test_pairwise_reward_sum_order():
+    """gym_macm.dist.pairwise_reward_sum: the device's order (flock_common.hpp block_pairwise_sum) —
+    float32 rewards as float64, pairwise over P = 64 * 2^ceil(log2(waves)) slots with +0.0 past N —
+    against a recursive restatement, at N that fill 1, 2, 3 -> 4 and 5 -> 8 waves."""
+    import numpy as np
+    from gym_macm.dist import env_order_sum, pairwise_reward_sum
+
+    def rec(x):
+        return x[0] if len(x) == 1 else rec(x[:len(x) // 2]) + rec(x[len(x) // 2:])
+
+    rng = np.random.default_rng(0)
+    for N, P in ((2, 64), (64, 64), (65, 128), (150, 256), (300, 512), (1024, 1024)):
+        r = (1.0 - rng.uniform(0, 60, size=(3, N)) / 35).astype(np.float32)
+        got = pairwise_reward_sum(r)
+        for e in range(3):
+            x = [float(v) for v in r[e]] + [0.0] * (P - N)
+            assert got[e] == rec(x), (N, e)
+    assert env_order_sum([0.1, 0.2, 0.3]) == (0.1 + 0.2) + 0.3

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--kernel", default="env_step_w64<0, 64, float, true>")
     ap.add_argument("--policy", default="random")
+    ap.add_argument("--outputs", default="trajectory", choices=("trajectory", "overwrite"),
+                    help="bench.py --outputs of the profiled run (a rollout launch's output form)")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--agents", type=int, default=64)
     ap.add_argument("--steps-per-launch", type=int, default=1,
@@ -62,7 +64,7 @@ def main():
     write_b = res["WRITE_SIZE"] * 1024.0
     agents = a.envs * a.agents
     out = {
-        "kernel": a.kernel, "envs": a.envs, "agents": a.agents, "policy": a.policy,
+        "kernel": a.kernel, "envs": a.envs, "agents": a.agents, "policy": a.policy, "outputs": a.outputs,
         "fetch_size_kib": res["FETCH_SIZE"], "write_size_kib": res["WRITE_SIZE"],
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "steps_per_launch": a.steps_per_launch,

@@ -1,8 +1,10 @@
-// Microbenchmark of one Gauss-Seidel level step (kernel B's velocity level loop) in isolation:
+// Microbenchmark of one Gauss-Seidel level step (kernel B's velocity level loop; V14 / V15 its
+// position level step, round 5) in isolation:
 // cycles per level step for several instruction forms, one wave per block, 1 block (a wave alone on
 // its SIMD) or 2048 blocks (2 waves per SIMD, the C5 shard's residency).
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -o tools/build/ubench_level tools/ubench_level.hip
 #include <hip/hip_runtime.h>
+#include "../gym-macm_amd/csrc/flock_common.hpp"  // sqrt_rn / rcp_rn / div_by_invariant of the product
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -42,6 +44,25 @@ __device__ __forceinline__ void gsv(float2& va, float2& vb, float nx, float ny, 
     va.x = va.x - mA * Px; va.y = va.y - mA * Py;
     vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
   }
+}
+
+// kernel B's position step (flock_step_wg.hip gs_position<true>): b2PositionSolverManifold (Normalize
+// with the product's sqrt_rn / rcp_rn), the clamped correction and -C / K; returns the separation
+__device__ __forceinline__ float gsp(float2& ca, float2& cb, float radius, float mA, float mB) {
+  float nx = cb.x - ca.x, ny = cb.y - ca.y;
+  const float len = macm::sqrt_rn(nx * nx + ny * ny);
+  if (len >= macm::kEps) {
+    const float inv = macm::rcp_rn(len);
+    nx *= inv;
+    ny *= inv;
+  }
+  const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
+  const float Cc = __builtin_amdgcn_fmed3f(macm::kBaumgarte * (sep + macm::kLinearSlop), -macm::kMaxLinearCorrection, 0.0f);
+  const float imp = macm::div_by_invariant(-Cc, mA + mB);
+  const float Px = imp * nx, Py = imp * ny;
+  ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
+  cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
+  return sep;
 }
 
 // packed form: the same IEEE ops on (x, y) pairs
@@ -291,6 +312,39 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
         lt = wl(y, c, lt);
       }
       s_v[lane] = make_float2(vx, vy);
+    } else if constexpr (VAR == 14) {  // the position step's VALU chain alone (bodies in registers)
+      float2 ca = *pa0, cb = make_float2(pa0->x + 0.9f, pa0->y + 0.1f);
+      float mn = 0.0f;
+      for (int lv = 0; lv < nlev; ++lv) {
+        const float sep = gsp(ca, cb, 0.5f, mA, mA);
+        mn = fminf(mn, sep);
+      }
+      *pa0 = ca;
+      *pb0 = cb;
+      ln += mn;
+    } else if constexpr (VAR == 15) {  // kernel B's position level step: branch-free, LDS, atomic min
+      float* const s_min = reinterpret_cast<float*>(s_v + 1024 + 32);  // per-lane words, never read here
+      float* const pmi = reinterpret_cast<float*>(s_v + 1024) + (lane & 1);
+      float* const pmd = s_min + lane;
+      bool on = mylv == 0;
+      float2* pa = on ? pa0 : pd;
+      float2* pb = on ? pb0 : pd;
+      float* pm = on ? pmi : pmd;
+      for (int lv = 0; lv < nlev; ++lv) {
+        float2 ca = *pa, cb = *pb;
+        on = mylv == lv + 1;
+        float2* const na = on ? pa0 : pd;
+        float2* const nb = on ? pb0 : pd;
+        float* const nm = on ? pmi : pmd;
+        const float sep = gsp(ca, cb, 0.5f, mA, mA);
+        *pa = ca;
+        *pb = cb;
+        __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        pa = na;
+        pb = nb;
+        pm = nm;
+        wave_lds_sync();
+      }
     } else if constexpr (VAR == 5) {  // packed VALU chain alone
       f2v va = *(f2v*)pa0, vb = *(f2v*)pb0;
       const f2v n = {nx, ny}, t = {ny, -nx};
@@ -354,6 +408,8 @@ int main() {
     run<10>("V10 uniform, 1 contact/level", blocks, nlev, iters);
     run<11>("V11 uniform, 2 contacts/level", blocks, nlev, iters);
     run<3>("V3 VALU chain only", blocks, nlev, iters);
+    run<14>("V14 position VALU chain only", blocks, nlev, iters);
+    run<15>("V15 position, kernel B form", blocks, nlev, iters);
     run<5>("V5 packed VALU chain only", blocks, nlev, iters);
     run<4>("V4 LDS round trip only", blocks, nlev, iters);
   }
