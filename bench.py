@@ -31,6 +31,10 @@ sys.path.insert(0, os.path.join(REPO, "gym-macm_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 B_ALG = 107  # bytes per agent-step: state r+w 2x40, action 3, obs 20, reward 4
+# The Gauss-Seidel chain floor (roofline.chain_floor_ms): cycles of one velocity / position level step's
+# dependent VALU chain, one wave alone on its SIMD (tools/ubench_level.hip V3 / V14 on the MI355X,
+# profiles/r05/ubench/), and the shader clock those cycles run at (V0: 278.1 cycles = 117.1 ns)
+C_VEL_LEVEL, C_POS_LEVEL, SHADER_GHZ = 208.0, 236.5, 2.375
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 SCALAR_SWEEP_MIN_ENVS = 2048  # = kScalarSweepMinEnvs in gym-macm_amd/csrc/flock_step_w64.hip
 
@@ -77,10 +81,15 @@ def _cpu_window(step_fn, acts, warmup, steps, budget_s):
     return n, time.perf_counter() - t0, w_run
 
 
-def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20, n_targets=1, tidx=None):
+def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20, n_targets=1, tidx=None,
+                 acts_host=None, levels_budget_s=0.0):
     """Time the CPU oracle on this host (OpenMP over envs) on the same workload as the GPU
     leg: the same E envs x N agents from reset, `warmup` untimed steps, then the GPU leg's
-    `steps` timed (fewer if they would exceed the budget)."""
+    `steps` timed (fewer if they would exceed the budget). acts_host: the GPU leg's own actions
+    [warmup + steps, E, N, 3] (else uniform draws of the same distribution).
+    levels_budget_s > 0: then an untimed replay of the same window records each timed step's
+    Gauss-Seidel level structure per env (OracleFlock.levels, for the chain floor); returns
+    (baseline dict, levels [steps', E] or None)."""
     from oracle import OracleFlock
     from gym_macm.settings import flockSettings, to_config
 
@@ -91,12 +100,47 @@ def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20,
     rng = np.random.default_rng(seed + 1)
     bufs = dict(obs=np.zeros((E, n_agents, 4), np.float64), nbr_id=np.zeros((E, n_agents), np.int32),
                 reward=np.zeros((E, n_agents), np.float64))
-    acts = [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(16)]
+    same = acts_host is not None
+    acts = (list(acts_host) if same else
+            [rng.integers(0, 3, size=(E, n_agents, 3)).astype(np.uint8) for _ in range(16)])
     n, dt, w_run = _cpu_window(lambda a: orc.step_raw(a, bufs, threads), acts, warmup, steps, budget_s)
-    return dict(value=E * n_agents * n / dt, unit="agent·steps/s", cores=threads, kind="port",
+    base = dict(value=E * n_agents * n / dt, unit="agent·steps/s", cores=threads, kind="port",
                 sample=f"oracle/ C restatement, {E} envs x {n_agents} agents, steps {w_run + 1}..{w_run + n} from "
-                       f"reset (the GPU leg times steps {warmup + 1}..{warmup + steps}), uniform random discrete "
-                       f"actions, OpenMP {threads} threads, {dt:.2f} s timed")
+                       f"reset (the GPU leg times steps {warmup + 1}..{warmup + steps}), "
+                       + ("the GPU leg's own actions" if same else "uniform random discrete actions")
+                       + f", OpenMP {threads} threads, {dt:.2f} s timed")
+    lv = None
+    if same and levels_budget_s > 0 and w_run == warmup and n >= steps:
+        # untimed replay of the GPU leg's window: the level structure each timed step solves
+        orc2 = OracleFlock(cfg, tidx, E, seed)
+        t0 = time.perf_counter()
+        rows = []
+        for k in range(warmup + steps):
+            if k >= warmup:
+                rows.append(orc2.levels()[:, 1].copy())
+                if time.perf_counter() - t0 > levels_budget_s:
+                    break
+            orc2.step_raw(acts[k], bufs, threads)
+        lv = np.stack(rows) if rows else None
+    return base, lv
+
+
+def chain_floor(levels, rollout, vel_iters=8, pos_iters=3):
+    """The Gauss-Seidel chain floor of the timed window, per step: every velocity and position pass
+    steps each level of an env's island order once ((1 + vel_iters) x C_VEL_LEVEL + pos_iters x
+    C_POS_LEVEL cycles per level, the dependent VALU floors of one wave alone on its SIMD), and a
+    launch ends with its deepest env: per step-launch sum_k max_e L[k, e]; one rollout launch of the
+    K steps, max_e sum_k L[k, e] (each env's wave runs its steps back to back). Returns (ms per step,
+    detail)."""
+    L = np.asarray(levels, np.int64)
+    K = L.shape[0]
+    per_launch, pipelined = int(L.max(axis=1).sum()), int(L.sum(axis=0).max())
+    lv = pipelined if rollout else per_launch
+    cyc = (1 + vel_iters) * C_VEL_LEVEL + pos_iters * C_POS_LEVEL
+    ms = lv * cyc / (SHADER_GHZ * 1e9) * 1e3 / K
+    return ms, {"levels_per_step_deepest": [int(x) for x in L.max(axis=1)], "levels_mean": float(L.mean()),
+                "sum_k_max_e": per_launch, "max_e_sum_k": pipelined, "steps_sampled": K,
+                "cycles_per_level": cyc, "c_vel": C_VEL_LEVEL, "c_pos": C_POS_LEVEL, "ghz": SHADER_GHZ}
 
 
 def b_alg_tdm(n_agents, obs_f64=False):
@@ -491,9 +535,17 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
             if args.env == "flock":
-                out["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_budget, E, W, K,
-                                                   n_targets=args.flocks if args.flocks > 1 else 1,
-                                                   tidx=None if targets is None else np.asarray(targets, np.int32))
+                # the GPU leg's own actions when the window is short (the driver's 25 steps)
+                ah = acts.cpu().numpy() if (args.policy == "random" and W + K <= 64) else None
+                out["cpu_baseline"], lv = cpu_baseline(
+                    N, args.seed, args.cpu_budget, E, W, K, n_targets=args.flocks if args.flocks > 1 else 1,
+                    tidx=None if targets is None else np.asarray(targets, np.int32), acts_host=ah,
+                    levels_budget_s=args.cpu_budget)
+                if lv is not None:
+                    fl_ms, fl = chain_floor(lv, rollout and N <= 64)
+                    out["roofline"]["chain_floor_ms"] = fl_ms
+                    out["roofline"]["chain_frac"] = fl_ms / kernel_ms
+                    out["roofline"]["chain_floor"] = fl
             else:
                 out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget, E, W, K)
         else:

@@ -107,6 +107,69 @@ struct WorldBuffers {
   uint32_t* sched;
 };
 
+// The solo split of a balanced wave-kernel rollout (flock_step_w64.hip env_rollout_w64<..., SOLO>):
+// the n heaviest envs in waves that own their SIMD, on `stream` (forked from and joined back into
+// the caller's stream with the two events). n = 0: one launch.
+struct SoloLaunch {
+  int n;
+  hipStream_t stream;
+  hipEvent_t fork, join;
+  // each solo wave adds 1 when it starts (monotonic); the caller's stream runs a watcher kernel
+  // (flock_step_wg.hip wait_count) until all n have, before the ordinary launch, so the solo waves
+  // are placed on empty SIMDs first (else the ordinary launch fills every SIMD and they wait for one
+  // to drain)
+  unsigned long long* started;
+  unsigned long long expected;
+};
+
+// The B -> C handoff of the workgroup step (flock_step_wg.hip, round 5). Kernel C of a step used to
+// start when kernel B's deepest env had finished, while most CUs idled through B's tail. With a
+// handoff, kernel C runs on a second stream, launched once every wave of B has started (behind a
+// watcher kernel that waits for b_started to reach the step's count, so B is wholly resident first
+// and no C block can take the resources a B wave still needs): each B wave publishes its env when it has finished
+// (its outputs for C stored write-through, st_wt, and drained first), and C's blocks take the envs
+// in that order. q == NULL: no handoff (C's block b steps env order[b]).
+struct Handoff {
+  unsigned long long* b_started;  // +1 per B wave at its start (monotonic; flock_step_wg.hip wait_count)
+  unsigned int* ctr;              // [2] envs B published, envs C took (zeroed by the step's order kernel)
+  unsigned long long* q;          // [E] B's finish order: tag << 32 | env
+  unsigned int tag;               // this step's tag (entries of earlier steps carry earlier tags)
+};
+
+// Write-through (sc1) stores and loads of the bytes kernel B hands to kernel C (the Handoff): agent-scope
+// relaxed atomics, which gfx950 issues as global_store / global_load ... sc1. Stored sc1 by every lane,
+// drained (vmcnt 0) before the flag, and loaded sc1 after the flag, they need no agent-scope
+// release / acquire (MI355X guide, inter-workgroup visibility: a release fence writes back the
+// XCD's whole L2, ~2-6 us, and one per B wave serialised in each XCD).
+__device__ __forceinline__ void st_wt(float2* p, float2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld_wt(const float2* p) {
+  const unsigned long long w =
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float2(__uint_as_float((unsigned int)w), __uint_as_float((unsigned int)(w >> 32)));
+}
+__device__ __forceinline__ void st_wt(uint8_t* p, uint8_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint8_t ld_wt(const uint8_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Host side of a world's handoff (macm_capi.hip): kernel C's stream, the join event, the device
+// words of Handoff, the last step's tag and the b_started count the next step waits for.
+struct HandoffStream {
+  hipStream_t stream;
+  hipEvent_t done;
+  unsigned long long* b_started;
+  unsigned int* ctr;
+  unsigned long long* q;
+  unsigned int tag;
+  unsigned long long expected;
+};
+
 // A status bit was set in some env: tell the host without a synchronisation (macm_world_step
 // reads the word before each launch). Rare path; a plain store, so bits of different envs may
 // overwrite each other (the per-env B.status keeps the exact OR for macm_world_status).

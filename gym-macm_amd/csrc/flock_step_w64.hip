@@ -2192,6 +2192,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
 }
 
 #ifdef MACM_ROLLOUT_TU
+hipError_t launch_wait_count(const unsigned long long* ctr, unsigned long long target, uint32_t* host_status,
+                             hipStream_t s);  // flock_step_wg.hip
+
 // nsteps consecutive steps of env blockIdx.x in one launch (macm_world_rollout): actions of step k
 // at actions + k * astride bytes ([K, E, N, A]), outputs overwritten each step (the last step's
 // remain) or, with traj, step k's outputs at row k of [K, ...] buffers (macm_world_rollout_traj),
@@ -2227,6 +2230,8 @@ struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   // trajectory form: every output (and, in the closed loop, the bot's actions: [K + 1, E, N, A],
   // step k reading row k and writing row k + 1) advances one row per step
   int traj;
+  int sched_off;  // a balanced launch steps envs order[sched_off + blockIdx.x] (solo split, below)
+  unsigned long long* solo_started;  // SOLO: the start counter (SoloLaunch::started)
 };
 
 // [K, ...] row k of an output (trajectory form); NULL stays NULL
@@ -2258,12 +2263,14 @@ constexpr bool kRollBalance = true;
 constexpr int kRollBalanceMinSteps = MACM_ROLL_BALANCE_MIN_STEPS;
 constexpr int kSchedMaxSize = 4095;
 
-// order[0..E): the envs by descending contact-list size (ccount, clamped to C); one workgroup
+// order[0..E): the envs by descending contact-list size (ccount, clamped to C); one workgroup.
+// reset2: the workgroup step's handoff counters (Handoff::ctr), zeroed for the step (or NULL)
 __global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict__ ccount, uint32_t* __restrict__ order,
-                                                     int E, int C) {
+                                                     int E, int C, unsigned int* reset2 = nullptr) {
   extern __shared__ uint32_t s_h[];  // [C + 1] envs per list size, then the order's starts
   __shared__ int s_scan[32];
   const int tid = threadIdx.x, BS = blockDim.x;
+  if (reset2 && tid < 2) reset2[tid] = 0u;
   for (int i = tid; i <= C; i += BS) s_h[i] = 0u;
   __syncthreads();
   for (int e = tid; e < E; e += BS) atomicAdd(&s_h[max(0, min((int)ccount[e], C))], 1u);
@@ -2284,11 +2291,26 @@ __global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict
   for (int e = tid; e < E; e += BS) order[atomicAdd(&s_h[max(0, min((int)ccount[e], C))], 1u)] = (uint32_t)e;
 }
 
-template <int MODE, int NCAP, typename OT, bool SCAL = false>
-__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_rollout_w64(RolloutArgs<OT> A0) {
+// Solo waves (round 5). Two heavy envs that share a SIMD slow each other's latency-bound chains, and
+// the balanced order alone still co-schedules the heaviest envs with three other waves (M closed
+// loop: ~500 cycles per level step shared, ~290 alone). A balanced rollout of at least
+// kRollBalanceMinSteps therefore launches its `solo` heaviest envs (order[0 .. solo)) in a kernel
+// instance whose waves own their SIMD — SOLO clobbers an accumulation register, so the register
+// file of a SIMD holds one such wave (512 of its registers allocated) — on a high-priority stream
+// forked from the caller's, and the other envs (order[solo ..)) in the ordinary instance. Which SIMD
+// a wave gets never changes an env's arithmetic; if the ordinary launch happened to be dispatched
+// first, the solo waves would only wait for free SIMDs (no wave waits on another).
+template <int MODE, int NCAP, typename OT, bool SCAL = false, bool SOLO = false>
+__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : 4))) void env_rollout_w64(
+    RolloutArgs<OT> A0) {
+  if constexpr (SOLO) {
+    asm volatile("" ::: "a255");  // one wave per SIMD (occupancy 1)
+    if (threadIdx.x == 0)  // this wave holds its SIMD: the ordinary launch may be dispatched
+      __hip_atomic_fetch_add(A0.solo_started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int nsteps = A0.nsteps;
   const bool bal = kRollBalance && A0.B.sched && nsteps >= kRollBalanceMinSteps;  // as in launch_roll
-  const int env = bal ? (int)A0.B.sched[blockIdx.x] : (int)blockIdx.x;
+  const int env = bal ? (int)A0.B.sched[A0.sched_off + blockIdx.x] : (int)blockIdx.x;
   for (int k = 0; k < nsteps; ++k) {
     // each step reads its parameters from the kernel arguments afresh, through a pointer the
     // compiler cannot see through, so nothing derived from them stays live across the loop
@@ -2343,33 +2365,59 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
 static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStream_t s, const StepParams& P,
                         const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
-                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
+                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
+                        SoloLaunch* solo = nullptr) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
-  if (kRollBalance && B.sched && nsteps >= kRollBalanceMinSteps) {
+  const bool bal = kRollBalance && B.sched && nsteps >= kRollBalanceMinSteps;
+  if (bal) {
     // list sizes above kSchedMaxSize share the top bucket (any order among them is a valid order;
     // the histogram stays within 16 KB of LDS whatever max_contacts a world was given)
     const int CB = P.max_contacts < kSchedMaxSize ? P.max_contacts : kSchedMaxSize;
     hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (CB + 1), s,
-                       reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, CB);
+                       reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, CB, nullptr);
     if (hipPeekAtLastError() != hipSuccess) return;  // no rollout on a stale order (the caller reports it)
   }
-  hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s,
-                     RolloutArgs<OT>{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol,
-                                     traj});
+  RolloutArgs<OT> A{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol, traj, 0,
+                    solo ? solo->started : nullptr};
+  int H = 0;
+  if constexpr (MODE == kFlock && NCAP == 64 && sizeof(OT) == 4) {
+    if (bal && solo && solo->stream && solo->started && solo->n > 0) H = solo->n < P.n_envs ? solo->n : 0;
+  }
+  if (H > 0) {
+    if constexpr (MODE == kFlock && NCAP == 64 && sizeof(OT) == 4) {
+      if (hipEventRecord(solo->fork, s) != hipSuccess || hipStreamWaitEvent(solo->stream, solo->fork, 0) != hipSuccess)
+        return;
+      hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL, true>), dim3(H), dim3(W), 0, solo->stream, A);
+      // the watcher (flock_step_wg.hip wait_count) is launched only behind a solo launch that was
+      // accepted: its H waves start (they wait for nothing) and end it
+      bool ok = hipPeekAtLastError() == hipSuccess;
+      if (ok) {
+        solo->expected += (unsigned long long)H;
+        ok = launch_wait_count(solo->started, solo->expected, B.host_status, s) == hipSuccess;
+      }
+      A.sched_off = H;
+      if (ok) hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs - H), dim3(W), 0, s, A);
+      // joined whatever happened above (no unjoined work on the solo stream)
+      (void)hipEventRecord(solo->join, solo->stream);
+      (void)hipStreamWaitEvent(s, solo->join, 0);
+    }
+    return;
+  }
+  hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s, A);
 }
 
 // the same instantiation choice as launch_step_w64 / launch_tdm_step_w64
 // order[0..E): the envs by descending contact-list size (the workgroup step, kWgEnvOrder)
-hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int C, hipStream_t s) {
+hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int C, hipStream_t s, unsigned int* reset2) {
   const int CB = C < kSchedMaxSize ? C : kSchedMaxSize;
-  hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (CB + 1), s, ccount, order, E, CB);
+  hipLaunchKernelGGL(rollout_sched, dim3(1), dim3(1024), sizeof(uint32_t) * (CB + 1), s, ccount, order, E, CB, reset2);
   return hipGetLastError();
 }
 
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
-                              int nsteps, unsigned long long astride, int traj) {
+                              int nsteps, unsigned long long astride, int traj, SoloLaunch* solo) {
   const TdmParams TP{};
   const TdmBuffers TB{};
   const bool small = P.n_agents <= 32;
@@ -2383,9 +2431,10 @@ hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cu
       launch_roll<kFlock, 32, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else if (P.n_envs >= kScalarSweepMinEnvs)
       launch_roll<kFlock, 64, float, true>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll,
-                                           done);
+                                           done, solo);
     else
-      launch_roll<kFlock, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
+      launch_roll<kFlock, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done,
+                                     solo);
   }
   return hipGetLastError();
 }

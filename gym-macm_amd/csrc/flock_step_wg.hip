@@ -26,7 +26,8 @@
 #include "flock_grid.hpp"
 
 namespace macm {
-hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int C, hipStream_t s);
+hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int C, hipStream_t s,
+                            unsigned int* reset2 = nullptr);
 
 // The step's env order (round 4): before each step the envs are ordered by contact-list size,
 // heaviest first (launch_env_order, one workgroup), and workgroup b of kernels A, DFS, B and C
@@ -41,6 +42,78 @@ constexpr bool kWgEnvOrder = true;
 #endif
 __device__ __forceinline__ int wg_env(const WorldBuffers& B) {
   return (kWgEnvOrder && B.sched) ? (int)B.sched[blockIdx.x] : (int)blockIdx.x;
+}
+
+// ---- the B -> C handoff (flock_common.hpp Handoff) -------------------------------------------------
+// Kernel B: every wave adds itself to b_started at its start (the second stream's wait), and
+// publishes its env when its body ends, whichever return it takes (the guard's destructor): its
+// stores of what C reads were write-through (st_wt: x_vout, x_cout, x_isolv, the list-order
+// impulses), all its stores complete (vmcnt 0), then the env at the next slot of the finish order
+// (an agent-scope atomic and an sc1 store; kernel C's block may run on another XCD).
+struct HandoffPublish {
+  const Handoff& H;
+  int e;
+  __device__ HandoffPublish(const Handoff& h, int env) : H(h), e(env) {
+    if (H.q && threadIdx.x == 0) __hip_atomic_fetch_add(H.b_started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ ~HandoffPublish() {
+    if (!H.q) return;
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0) {
+      const unsigned slot = __hip_atomic_fetch_add(&H.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&H.q[slot], ((unsigned long long)H.tag << 32) | (unsigned)e, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+};
+
+// Kernel C: the block's env, the next one kernel B finished (thread 0 polls with sc1 loads; the other
+// waves load after the barrier; every load of B's handed-off bytes is ld_wt). A wait of ~1 s (never
+// expected: every B wave is running when C is launched and waits for nothing) gives up:
+// MACM_ST_HANDOFF, the block steps nothing (returns -1).
+constexpr unsigned kHandoffSpins = 1u << 21;
+__device__ __forceinline__ int handoff_take(const WorldBuffers& B, const Handoff& H, int* s_env) {
+  if (threadIdx.x == 0) {
+    const unsigned idx = __hip_atomic_fetch_add(&H.ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int env = -1;
+    for (unsigned it = 0; it < kHandoffSpins; ++it) {
+      const unsigned long long v = __hip_atomic_load(&H.q[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(v >> 32) == H.tag) {
+        env = (int)(unsigned)v;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (env < 0) report_status(B, MACM_ST_HANDOFF);
+    *s_env = env;
+  }
+  __syncthreads();
+  const int env = *s_env;
+  __syncthreads();  // every thread has read it before the kernel reuses the word
+  return env;
+}
+
+// The dependency the handoff needs is "every wave of kernel B has started", which no stream or event
+// expresses (an event completes with a kernel). hipStreamWaitValue64 does (the first form), but each
+// wait cost ~1 ms of latency on the MI355X (C3, 1000 envs: 281 -> 1,360 us per step). This watcher,
+// one wave launched ahead of the consumer on its stream, polls the count (agent-scope loads) and
+// ends as soon as it reaches `target`; the consumer is launched after it. It takes one wave slot and
+// no LDS, so the producer's waves always fit beside it. A wait of ~1 s (never expected) reports
+// MACM_ST_HANDOFF and ends.
+constexpr unsigned kWatchSpins = 1u << 22;
+__global__ __launch_bounds__(64) void wait_count(const unsigned long long* __restrict__ ctr, unsigned long long target,
+                                                uint32_t* host_status) {
+  if (threadIdx.x != 0) return;
+  for (unsigned it = 0; it < kWatchSpins; ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (host_status) __hip_atomic_store(host_status, (uint32_t)MACM_ST_HANDOFF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t launch_wait_count(const unsigned long long* ctr, unsigned long long target, uint32_t* host_status,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(wait_count, dim3(1), dim3(64), 0, s, ctr, target, host_status);
+  return hipGetLastError();
 }
 
 namespace wg {
@@ -1374,10 +1447,11 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
 #ifndef MACM_LEVEL_UNROLL  // A/B knob: level steps per loop iteration (1 or 2)
 #define MACM_LEVEL_UNROLL 2
 #endif
-__global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap) {
+__global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap, Handoff H) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
   const int e = wg_env(B), lane = threadIdx.x, N = P.n_agents;
+  const HandoffPublish publish(H, e);  // to kernel C when this body ends (any return)
   const int IS = wg_isl_stride(N);
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
@@ -1509,7 +1583,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
       });
       const int k = c * W + lane;
       if (!warm && k < nc) {
-        if (last) g_lam[cur.o] = im;
+        if (last) st_wt(g_lam + cur.o, im);  // kernel C reads it (the handoff)
         else cimp[k] = im;
       }
       wait_vm();
@@ -1519,7 +1593,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   if (P.warm_starting) vel_pass(std::true_type{}, false);
   for (int it = 0; it < P.vel_iters; ++it) vel_pass(std::false_type{}, it + 1 == P.vel_iters);
   if (P.vel_iters == 0)  // StoreImpulses of the (warm-started) impulses as they are
-    for (int k = lane; k < nc; k += W) g_lam[xord[k]] = cimp[k];
+    for (int k = lane; k < nc; k += W) st_wt(g_lam + xord[k], cimp[k]);
 
   WSTAMP(14);
   // ---- integrate positions ---------------------------------------------------------------------
@@ -1534,7 +1608,7 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
     }
     const float2 c = s_c[i];
     s_c[i] = make_float2(c.x + P.dt * vx, c.y + P.dt * vy);
-    B.x_vout[en + i] = make_float2(vx, vy);
+    st_wt(B.x_vout + en + i, make_float2(vx, vy));
   }
   __syncthreads();
 
@@ -1604,22 +1678,24 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   if (mA + mB > 0.0f) pos_passes(std::true_type{});
   else pos_passes(std::false_type{});
   uint8_t* isolv = B.x_isolv + (size_t)e * IS;
-  for (int I = lane; I < nisl; I += W) isolv[I] = s_done[I];
+  for (int I = lane; I < nisl; I += W) st_wt(isolv + I, s_done[I]);
   WSTAMP(15);
 #ifdef MACM_STAMPS
   if (lane == 0) B.stamps[(size_t)e * 32 + 12] = (unsigned long long)B.x_nlvl[e] | ((unsigned long long)nc << 32);
 #endif
-  for (int i = lane; i < N; i += W) B.x_cout[en + i] = s_c[i];
+  for (int i = lane; i < N; i += W) st_wt(B.x_cout + en + i, s_c[i]);
 }
 
 template <typename OT>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void flock_step_wg_c(StepParams P, WorldBuffers B, int cur, int tcap,
                                                         OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
                                                         float* __restrict__ rew_out, uint8_t* __restrict__ coll_out,
-                                                        uint8_t* __restrict__ done_out) {
+                                                        uint8_t* __restrict__ done_out, Handoff H) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = wg_env(B);
+  // in kernel B's finish order (the block scan's scratch words carry the env to the block)
+  const int e = H.q ? handoff_take(B, H, reinterpret_cast<int*>(lds + wg_layout_c(P.n_agents).scan)) : wg_env(B);
+  if (e < 0) return;
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
   const int N = P.n_agents;
@@ -1655,7 +1731,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     p = B.pos[ag];
     fo = B.fat[ag];
     slp = B.sleep[ag];
-    const float2 c = B.x_cout[ag], vv = B.x_vout[ag];
+    const float2 c = ld_wt(B.x_cout + ag), vv = ld_wt(B.x_vout + ag);  // kernel B's (write-through)
     cx = c.x; cy = c.y; vx = vv.x; vy = vv.y;
     hasdeg = B.x_deg[ag] != 0;
   }
@@ -1709,7 +1785,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int mid = (lo + hi + 1) >> 1;
         if (s_ib[mid] <= k) lo = mid; else hi = mid - 1;
       }
-      s_flag[ibod[k]] = (__uint_as_float(s_mn[lo]) >= kTimeToSleep && isolv[lo]) ? 1 : 0;
+      s_flag[ibod[k]] = (__uint_as_float(s_mn[lo]) >= kTimeToSleep && ld_wt(isolv + lo)) ? 1 : 0;
     }
   }
   __syncthreads();
@@ -2044,7 +2120,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const int trank = Tr + tpos;
       if (w < C) {
         ocab[w] = ab;
-        ocimp[w] = (touch && trank < tcap) ? g_lam[trank] : make_float2(0.0f, 0.0f);
+        ocimp[w] = (touch && trank < tcap) ? ld_wt(g_lam + trank) : make_float2(0.0f, 0.0f);
       }
     }
     Tr += tn;
@@ -2164,33 +2240,64 @@ hipError_t wg_configure(int N, int tcap) {
   return e;
 }
 
+// One workgroup-path step: the env order, kernels A, DFS, B and C. With a handoff (HS non-NULL, and
+// stream waits supported), kernel C runs on HS->stream as B's consumer (see Handoff): that stream
+// waits for every B wave to have started, C's blocks take the envs in B's finish order, and the
+// caller's stream waits for C at the end, so the call's results are complete on `s` as before.
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
-                          hipStream_t s) {
+                          hipStream_t s, HandoffStream* HS) {
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
+  Handoff H{nullptr, nullptr, nullptr, 0u};
+  if (HS && kWgEnvOrder && B.sched) {
+    if (++HS->tag == 0u) HS->tag = 1u;  // 0 never tags a step (zeroed queue entries)
+    H = Handoff{HS->b_started, HS->ctr, HS->q, HS->tag};
+  }
   if (kWgEnvOrder && B.sched) {
-    const hipError_t oe =
-        launch_env_order(reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, P.max_contacts, s);
+    const hipError_t oe = launch_env_order(reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs,
+                                           P.max_contacts, s, H.q ? H.ctr : nullptr);
     if (oe != hipSuccess) return oe;
   }
   const int N = P.n_agents, la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
   const int ld = wg::wg_layout_d(N, tcap).total;
-  if (obs_f64) {
+  auto launch_c = [&](hipStream_t cs) {
+    if (obs_f64)
+      hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, cs, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
+                         done, H);
+    else
+      hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, cs, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
+                         done, H);
+  };
+  if (obs_f64)
     hipLaunchKernelGGL(flock_step_wg_a<double>, grid, block, la, s, P, B, cur, tcap, actions, (double*)obs, nbr, rew,
                        coll, done);
-    if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
-    hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
-    hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, s, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
-                       done);
-  } else {
+  else
     hipLaunchKernelGGL(flock_step_wg_a<float>, grid, block, la, s, P, B, cur, tcap, actions, (float*)obs, nbr, rew,
                        coll, done);
-    if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
-    hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap);
-    hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, s, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
-                       done);
+  if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
+  hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
+  if (!H.q) {
+    launch_c(s);
+    return hipGetLastError();
   }
-  return hipGetLastError();
+  // C on the second stream, behind a watcher that ends once all of B has started. The count it waits
+  // for follows the B launches that were accepted (every one of their waves adds itself); a watcher
+  // that cannot be launched runs C on the caller's stream after B instead (it takes B's envs from
+  // the complete queue).
+  hipError_t e = hipPeekAtLastError();
+  if (e != hipSuccess) return e;  // B not launched: nothing on the second stream, no count to wait for
+  HS->expected += (unsigned long long)P.n_envs;
+  if (launch_wait_count(HS->b_started, HS->expected, B.host_status, HS->stream) != hipSuccess) {
+    launch_c(s);
+    return hipGetLastError();
+  }
+  launch_c(HS->stream);
+  e = hipPeekAtLastError();
+  // joined whatever happened above
+  const hipError_t r = hipEventRecord(HS->done, HS->stream);
+  const hipError_t w = hipStreamWaitEvent(s, HS->done, 0);
+  if (e == hipSuccess) e = r != hipSuccess ? r : w;
+  return e != hipSuccess ? e : hipGetLastError();
 }
 
 hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr, const uint8_t* mask,

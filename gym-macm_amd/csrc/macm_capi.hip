@@ -20,14 +20,14 @@ hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, 
                            bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
-                              int nsteps, unsigned long long astride, int traj);
+                              int nsteps, unsigned long long astride, int traj, SoloLaunch* solo);
 hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
                            int32_t* nbr, const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
                               hipStream_t s);
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
-                          hipStream_t s);
+                          hipStream_t s, HandoffStream* HS);
 hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr,
                           const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_wg(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
@@ -86,6 +86,9 @@ struct macm_world {
   // workgroup-path rollouts: env slices on streams of their own (created on first use)
   std::vector<hipStream_t> slice_streams;
   std::vector<hipEvent_t> slice_events;  // [0] fork, [1 + s] join of slice s
+  SoloLaunch solo{0, nullptr, nullptr, nullptr, nullptr, 0ull};  // wave path: the balanced rollout's solo split
+  HandoffStream* ho = nullptr;  // workgroup path: kernel C as kernel B's consumer (handoff_for)
+  bool ho_tried = false;
   int slots_alloc = 0;  // spill working-set slots allocated (== E: one per env)
   int pool0 = 0;        // B.sp_pool as created (0: one slot per env), restored by set_debug
 };
@@ -179,7 +182,23 @@ void fill_body_params(StepParams& P, double hz, float radius, float density, flo
   P.diag_c = 1.0 / sqrt(two);  // 1 / np.sqrt(2)
 }
 
+static void free_handoff(HandoffStream*& h) {
+  if (!h) return;
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->done) (void)hipEventDestroy(h->done);
+  if (h->b_started) (void)hipFree(h->b_started);
+  if (h->ctr) (void)hipFree(h->ctr);
+  if (h->q) (void)hipFree(h->q);
+  delete h;
+  h = nullptr;
+}
+
 void free_world(macm_world* w) {
+  free_handoff(w->ho);
+  if (w->solo.stream) (void)hipStreamDestroy(w->solo.stream);
+  if (w->solo.fork) (void)hipEventDestroy(w->solo.fork);
+  if (w->solo.started) (void)hipFree(w->solo.started);
+  if (w->solo.join) (void)hipEventDestroy(w->solo.join);
   for (hipStream_t st : w->slice_streams) (void)hipStreamDestroy(st);
   for (hipEvent_t ev : w->slice_events) (void)hipEventDestroy(ev);
   w->slice_streams.clear();
@@ -231,6 +250,18 @@ struct Capacity {
   int64_t C;
   int64_t slots;  // == E: one slot per env
 };
+// The solo split of balanced wave-kernel rollouts (flock_step_w64.hip, env_rollout_w64<..., SOLO>):
+// how many of the heaviest envs run in waves that own their SIMD. MACM_SOLO_ENVS overrides it
+// (A/B sessions; 0 = one launch).
+#ifndef MACM_SOLO_ENVS_DEFAULT
+#define MACM_SOLO_ENVS_DEFAULT 0
+#endif
+static int solo_envs() {
+  const char* v = getenv("MACM_SOLO_ENVS");
+  const int n = v ? atoi(v) : MACM_SOLO_ENVS_DEFAULT;
+  return n > 0 ? n : 0;
+}
+
 Capacity default_capacity(int N, int E, int64_t max_contacts, size_t free_bytes) {
   const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
   const int64_t budget = std::max<int64_t>((int64_t)(free_bytes / 8), 256LL << 20);
@@ -365,6 +396,7 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   w->cur = 0;
   w->tidx = tidx;
   w->wave = N <= 64;
+  w->solo.n = w->wave ? solo_envs() : 0;
   {
     const int bs = N <= 64 ? 64 : wg_block(N);
     const int want = N <= 64 ? 256 : 5 * bs;  // register staging holds 5 records per thread
@@ -579,9 +611,41 @@ static int overflow_error(uint32_t st) {
   if (st & MACM_ST_TOUCH_OVERFLOW) what += " touching-contact capacity;";
   if (st & MACM_ST_DEGREE_OVERFLOW) what += " per-body contact capacity;";
   if (st & MACM_ST_SPILL_WAIT) what += " spill working-set pool (a dense env waited ~1 s for a slot);";
+  if (st & MACM_ST_HANDOFF) what += " B -> C handoff (a kernel-C block waited ~1 s for an env);";
   return fail(MACM_E_OVERFLOW, "an env outgrew its" + what +
                                    " the results since that step are not the reference's (status bits " +
                                    std::to_string(st) + "; reset, place or set_state clears them)");
+}
+
+// The workgroup step's B -> C handoff (flock_common.hpp Handoff), created at the first step that can
+// use it: the workgroup path, when kHandoffDefault or MACM_HANDOFF=1 (A/B; MACM_HANDOFF=0 off). Env
+// slices (rollout_wg_slices) run without it. NULL: kernel C launched after B on the same stream.
+#ifndef MACM_HANDOFF_DEFAULT
+#define MACM_HANDOFF_DEFAULT 0
+#endif
+static constexpr bool kHandoffDefault = MACM_HANDOFF_DEFAULT != 0;
+static HandoffStream* handoff_for(macm_world* w) {
+  if (w->wave || w->ho_tried) return w->ho;
+  w->ho_tried = true;
+  const char* v = getenv("MACM_HANDOFF");
+  if (!(v ? atoi(v) != 0 : kHandoffDefault)) return nullptr;
+  HandoffStream* h = new HandoffStream{};
+  bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&h->done, hipEventDisableTiming) == hipSuccess &&
+            hipMalloc(&h->b_started, sizeof(unsigned long long)) == hipSuccess &&
+            hipMalloc(&h->ctr, 2 * sizeof(unsigned int)) == hipSuccess &&
+            hipMalloc(&h->q, (size_t)w->P.n_envs * sizeof(unsigned long long)) == hipSuccess;
+  // tags start at 1, so a zeroed queue holds no entry of any step; the start count from 0
+  ok = ok && hipMemset(h->q, 0, (size_t)w->P.n_envs * sizeof(unsigned long long)) == hipSuccess &&
+       hipMemset(h->ctr, 0, 2 * sizeof(unsigned int)) == hipSuccess &&
+       hipMemset(h->b_started, 0, sizeof(unsigned long long)) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    free_handoff(h);
+    return nullptr;
+  }
+  w->ho = h;
+  return h;
 }
 
 int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out, void* stream) {
@@ -598,7 +662,7 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
                             out->collided, out->done, (hipStream_t)stream));
   else
     HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
-                           out->reward, out->collided, out->done, (hipStream_t)stream));
+                           out->reward, out->collided, out->done, (hipStream_t)stream, handoff_for(w)));
   w->cur ^= 1;
   return MACM_OK;
 }
@@ -704,7 +768,7 @@ static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions,
       const unsigned char* act_k = actions + k * kstride + e0 * abytes;
       hipError_t he = launch_step_wg(Ps[i], Bs[i], cur, w->tcap, act_k, obs_i, w->cfg.obs_f64 != 0,
                                      row(ok.nbr_id, N), row(ok.reward, N), row(ok.collided, N), row(ok.done, 1),
-                                     w->slice_streams[i]);
+                                     w->slice_streams[i], nullptr);
       if (he == hipSuccess && bots)
         he = launch_bots_flock(obs_i, w->cfg.obs_f64 != 0, obs_dim(w->cfg), (long long)Ps[i].n_envs * N,
                                const_cast<unsigned char*>(act_k) + (traj ? (size_t)E * abytes : 0), w->slice_streams[i]);
@@ -741,9 +805,19 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
   const unsigned long long astride =
       bots ? 0ull
            : (unsigned long long)w->P.n_envs * w->P.n_agents * (mode == 0 ? 3 * sizeof(uint8_t) : 2 * sizeof(float));
-  if (w->wave) {  // one launch; astride 0: the closed-loop form of the rollout kernel
+  if (w->wave) {  // one launch (two with the solo split); astride 0: the closed-loop form of the rollout kernel
+    if (w->solo.n > 0 && !w->solo.stream) {  // created at the first rollout that can use it
+      int lo = 0, hi = 0;
+      HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_TRY(hipStreamCreateWithPriority(&w->solo.stream, hipStreamNonBlocking, hi));
+      HIP_TRY(hipEventCreateWithFlags(&w->solo.fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&w->solo.join, hipEventDisableTiming));
+      HIP_TRY(hipMalloc(&w->solo.started, sizeof(unsigned long long)));
+      HIP_TRY(hipMemset(w->solo.started, 0, sizeof(unsigned long long)));
+    }
     HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
-                               out->collided, out->done, s, n_steps, astride, traj ? 1 : 0));
+                               out->collided, out->done, s, n_steps, astride, traj ? 1 : 0,
+                               w->solo.started ? &w->solo : nullptr));
     if (n_steps & 1) w->cur ^= 1;
     return MACM_OK;
   }
@@ -757,7 +831,7 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
     const macm_outputs ok = step_outputs(w, out, k, traj);
     const unsigned char* act_k = act + k * kstride;
     HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, act_k, ok.obs, w->cfg.obs_f64 != 0, ok.nbr_id, ok.reward,
-                           ok.collided, ok.done, s));
+                           ok.collided, ok.done, s, handoff_for(w)));
     w->cur ^= 1;
     if (bots)
       HIP_TRY(launch_bots_flock(ok.obs, w->cfg.obs_f64 != 0, obs_dim(w->cfg), rows,

@@ -15,6 +15,7 @@ REWARD_BINARY, REWARD_LINEAR = 0, 1
 COORD_POLAR, COORD_CARTESIAN = 0, 1
 
 ST_CONTACT_OVERFLOW, ST_TOUCH_OVERFLOW, ST_DEGREE_OVERFLOW, ST_INVALID_ACTION, ST_SPILL_WAIT = 1, 2, 4, 8, 16
+ST_HANDOFF = 32
 DEBUG_FORCE_SPILL = 1
 DEBUG_SWEEP_CELLS = 2
 DEBUG_SWEEP_ALL_PAIRS = 4

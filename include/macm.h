@@ -70,8 +70,11 @@ enum {
   MACM_ST_TOUCH_OVERFLOW = 2,   /* (before ABI 6) TDM touching contacts beyond capacity  */
   MACM_ST_DEGREE_OVERFLOW = 4,  /* (before ABI 6) TDM body degree beyond capacity        */
   MACM_ST_INVALID_ACTION = 8,   /* validate_actions: an action outside the action space  */
-  MACM_ST_SPILL_WAIT = 16       /* a dense env found no free spill working-set slot for ~1 s
+  MACM_ST_SPILL_WAIT = 16,      /* a dense env found no free spill working-set slot for ~1 s
                                    (a pooled world: fewer slots than envs) and was not stepped */
+  MACM_ST_HANDOFF = 32          /* workgroup path: a kernel-C block waited ~1 s for kernel B to hand
+                                   it an env (never expected: B's waves wait for nothing) and
+                                   skipped it; results since then are invalid (ABI 8)          */
 };
 
 /* macm_world_set_debug / macm_tdm_set_debug flags (test hooks; 0 = product behaviour; TDM takes

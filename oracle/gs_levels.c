@@ -1,12 +1,12 @@
-/* Gauss-Seidel level structure of a batch of envs (a measurement helper, not the product, not the
- * oracle): for each env, the touching contacts of its ordered contact list (b2CollideCircles:
+/* TEST / MEASUREMENT INFRASTRUCTURE ONLY (built into liboracle_flock.so; never the product).
+ * Gauss-Seidel level structure of a batch of envs, for the chain floor (bench.py's cpu_baseline
+ * leg, tools/chain_floor.py): for each env, the touching contacts of its ordered contact list (b2CollideCircles:
  * touching iff |pB - pA|^2 <= (2r)^2 in float32), Box2D's island order of them (seeds from the
  * highest body with edges, each body's edges in list order, as b2World::Solve's DFS over the
  * prepend-ordered edge lists) and the level of each contact in that order
  * (1 + the level of the last earlier contact sharing a body): what the step kernels' level-parallel
  * solvers step through once per velocity / position pass. Sleeping bodies are not modelled (an
- * early window from reset has none). Built by tools/chain_floor.py:
- *   gcc -O2 -fopenmp -shared -fPIC -o tools/build/libgs_levels.so tools/gs_levels.c
+ * early window from reset has none).
  */
 #include <stdint.h>
 #include <stdlib.h>

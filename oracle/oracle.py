@@ -94,6 +94,7 @@ def lib():
         "to_reset_envs": (None, [c_void_p, c_void_p]),
         "fo_reset_envs": (None, [c_void_p, c_void_p]),
         "to_get_state": (None, [c_void_p] + [c_void_p] * 13 + [c_int] + [c_void_p] * 4),
+        "gs_levels": (None, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float, c_void_p]),
         "to_set_state": (None, [c_void_p] + [c_void_p] * 13 + [c_int] + [c_void_p] * 4),
     }
     for name, (res, args) in sig.items():
@@ -186,6 +187,18 @@ class OracleFlock:
         if int(s["contact_count"].max(initial=0)) > C:
             raise OverflowError("oracle contact list exceeds max_contacts")
         return s
+
+    def levels(self) -> np.ndarray:
+        """[E, 4] int32 of the state the next step starts from (oracle/gs_levels.c): touching contacts,
+        Gauss-Seidel levels per pass in Box2D's island order (the deepest island), islands, contacts of
+        the largest island. A measurement for the chain floor, not part of the restatement."""
+        cap = max(1, max(self.L.fo_contacts(self.h, e, None, 0) for e in range(self.E)))
+        st = self.get_state(cap)
+        out = np.zeros((self.E, 4), np.int32)
+        rr = np.float32(2 * self.cfg.radius) ** 2
+        self.L.gs_levels(self.E, self.N, cap, st["pos"].ctypes.data, st["contact_count"].ctypes.data,
+                         st["contact_ab"].ctypes.data, float(rr), out.ctypes.data)
+        return out
 
     def set_state(self, s: dict) -> None:
         C = s["contact_ab"].shape[1]

@@ -225,3 +225,68 @@ def test_balanced_rollout_equals_per_step(E, N, K, kw):
     assert_same(a, b, "balanced closed-loop rollout")
     assert torch.equal(act_a, act_b), "the bot's next actions"
     assert b.status() == 0
+
+
+@pytest.mark.parametrize("solo,E,N,K,kw", [
+    (16, 600, 64, 40, {"start_spread": 6}),
+    (64, 2100, 64, 32, {"start_spread": 12}),                    # the scalar-sweep instantiation (>= 2048 envs)
+    (5, 70, 40, 33, {"reward_mode": "linear", "coord": "cartesian"}),
+    (8, 8, 64, 32, {}),                                          # solo >= envs: one launch
+])
+def test_solo_split_rollout_equals_per_step(monkeypatch, solo, E, N, K, kw):
+    """The solo split of a balanced rollout (env_rollout_w64<..., SOLO>: the `solo` heaviest envs in
+    waves that own their SIMD, on a second stream, the rest in the ordinary launch) equals per-step
+    launches, open and closed loop, with the reward sums."""
+    from gym_macm.bots import flock_actions as bot_actions
+    monkeypatch.setenv("MACM_SOLO_ENVS", str(solo))
+    b = FlockVec(E, n_agents=[N], seed=29, device="cuda:0", **kw)
+    monkeypatch.delenv("MACM_SOLO_ENVS")
+    a = FlockVec(E, n_agents=[N], seed=29, device="cuda:0", **kw)
+    acts = flock_actions(K, E, N, 31)
+    for k in range(K):
+        a.step(acts[k])
+    b.rollout(acts)
+    assert_same(a, b, "solo open-loop rollout")
+    act_a = bot_actions(a.obs)
+    act_b = act_a.clone()
+    for _ in range(K):
+        a.step(act_a)
+        bot_actions(a.obs, out=act_a)
+    b.rollout_bots(act_b, K)
+    assert_same(a, b, "solo closed-loop rollout")
+    assert torch.equal(act_a, act_b), "the bot's next actions"
+    pa, ta = a.reward_sums()
+    pb, tb = b.reward_sums()
+    np.testing.assert_array_equal(pa, pb)
+    assert ta == tb and b.status() == 0
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (40, 100, 12, {"start_spread": 12}),
+    (24, 300, 8, {"reward_mode": "linear"}),
+    (6, 1024, 6, {}),                                   # C5-shaped: dense DFS kernel, deep levels
+    (1000, 256, 5, {"start_spread": 30}),               # >= 1024 envs would take the slices; 1000 do not
+])
+def test_handoff_equals_plain_workgroup_step(monkeypatch, E, N, K, kw):
+    """The workgroup step's B -> C handoff (MACM_HANDOFF=1: kernel C on a second stream behind a watcher,
+    taking the envs in kernel B's finish order, B's outputs handed over write-through) gives the plain
+    launch order's results bit for bit: state, lists, outputs, counters and reward sums, per-step and
+    rollout launches."""
+    monkeypatch.setenv("MACM_HANDOFF", "1")
+    b = FlockVec(E, n_agents=[N], seed=E + N, device="cuda:0", **kw)
+    monkeypatch.setenv("MACM_HANDOFF", "0")
+    a = FlockVec(E, n_agents=[N], seed=E + N, device="cuda:0", **kw)
+    acts = flock_actions(2 * K, E, N, 7)
+    for k in range(K):
+        a.step(acts[k])
+        b.step(acts[k])
+    assert_same(a, b, "handoff per-step launches")
+    for k in range(K, 2 * K):
+        a.step(acts[k])
+    b.rollout(acts[K:])
+    assert_same(a, b, "handoff rollout")
+    np.testing.assert_array_equal(a.counters(), b.counters())
+    pa, ta = a.reward_sums()
+    pb, tb = b.reward_sums()
+    np.testing.assert_array_equal(pa, pb)
+    assert ta == tb and b.status() == 0

@@ -1,7 +1,8 @@
 """Gauss-Seidel chain floor and launch-boundary tail of a workgroup-path window (a measurement
 script). Runs the CPU oracle (oracle/) from reset over a bench window and, per env
-and step, takes the level structure of the step's touching contacts (tools/gs_levels.c: Box2D's
-island order, level = 1 + the last earlier level sharing a body): L[e, k] levels per pass.
+and step, takes the level structure of the step's touching contacts (Box2D's
+island order, level = 1 + the last earlier level sharing a body; oracle/gs_levels.c): L[e, k]
+levels per pass.
 
 Kernel B (flock_solve_wg, one wave per env) steps every level of every pass: warm start + vel_iters
 velocity passes and up to pos_iters position passes, so env e's chain in step k is
@@ -20,10 +21,8 @@ Printed, per window:
     python tools/chain_floor.py --agents 256 --envs 4096 --flocks 4 --warmup 5 --steps 20   # C3
 """
 import argparse
-import ctypes
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -33,39 +32,26 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "oracle"), os.path.join(REPO, "tests"), os.path.join(REPO, "gym-macm_amd")]
 
 
-def levels_lib():
-    so = os.path.join(REPO, "tools", "build", "libgs_levels.so")
-    src = os.path.join(REPO, "tools", "gs_levels.c")
-    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
-        os.makedirs(os.path.dirname(so), exist_ok=True)
-        subprocess.run(["gcc", "-O2", "-fopenmp", "-shared", "-fPIC", "-ffp-contract=off", "-o", so, src], check=True)
-    L = ctypes.CDLL(so)
-    L.gs_levels.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                            ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
-    return L
-
-
-def window_levels(agents, envs, flocks, warmup, steps, seed, spread, threads):
-    """[steps, envs, 4] (touching, levels, islands, largest island) of the timed steps."""
+def window_levels(agents, envs, flocks, warmup, steps, seed, spread, threads, policy="random"):
+    """[steps, envs, 4] (touching, levels, islands, largest island) of the timed steps; policy "bots":
+    the closed loop with the reference's bots.flock (tests/parity.py flock_bot) on the float32 obs."""
     from gym_macm.settings import flockSettings, to_config
     from oracle import OracleFlock
+    from parity import flock_bot
     N = agents
     tidx = None if flocks <= 1 else np.asarray([i * flocks // N for i in range(N)], np.int32)
     cfg = to_config(flockSettings(start_spread=spread), N, max(1, flocks), obs_f64=True)
     orc = OracleFlock(cfg, tidx, envs, seed)
     rng = np.random.default_rng(seed + 1)
-    L = levels_lib()
-    cap = 64 * N
     out = np.zeros((steps, envs, 4), np.int32)
-    rr = np.float32(2 * cfg.radius) ** 2
+    obs = orc.observe()[0] if policy == "bots" else None
     for k in range(warmup + steps):
         if k >= warmup:  # the structure the step is about to solve: the state at its start
-            st = orc.get_state(cap)
-            o = np.zeros((envs, 4), np.int32)
-            L.gs_levels(envs, N, cap, st["pos"].ctypes.data, st["contact_count"].ctypes.data,
-                        st["contact_ab"].ctypes.data, ctypes.c_float(rr), o.ctypes.data)
-            out[k - warmup] = o
-        orc.step(rng.integers(0, 3, size=(envs, N, 3)).astype(np.uint8), n_threads=threads)
+            out[k - warmup] = orc.levels()
+        if policy == "bots":
+            obs = orc.step(flock_bot(obs.astype(np.float32).astype(np.float64)), n_threads=threads)["obs"]
+        else:
+            orc.step(rng.integers(0, 3, size=(envs, N, 3)).astype(np.uint8), n_threads=threads)
     return out
 
 
@@ -77,6 +63,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--spread", type=float, default=20.0)
+    ap.add_argument("--policy", choices=("random", "bots"), default="random")
     ap.add_argument("--seed", type=int, default=0x6D61636D)
     ap.add_argument("--vel-iters", type=int, default=8)
     ap.add_argument("--pos-iters", type=int, default=3)
@@ -87,7 +74,7 @@ def main():
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     t0 = time.time()
-    lv = window_levels(a.agents, a.envs, a.flocks, a.warmup, a.steps, a.seed, a.spread, a.threads)
+    lv = window_levels(a.agents, a.envs, a.flocks, a.warmup, a.steps, a.seed, a.spread, a.threads, a.policy)
     L = lv[..., 1].astype(np.int64)  # [K, E]
     per_launch = int(L.max(axis=1).sum())
     pipelined = int(L.sum(axis=0).max())
@@ -97,7 +84,11 @@ def main():
     deepest = L.max(axis=1)
     res = {
         "config": dict(agents=a.agents, envs=a.envs, flocks=a.flocks, warmup=a.warmup, steps=a.steps, seed=a.seed,
-                       spread=a.spread),
+                       spread=a.spread, policy=a.policy),
+        "heaviest_envs": [dict(env=int(e), levels_total=int(L[:, e].sum()), touching_mean=float(lv[:, e, 0].mean()),
+                               islands_mean=float(lv[:, e, 2].mean()), largest_island_mean=float(lv[:, e, 3].mean()))
+                          for e in np.argsort(-L.sum(axis=0))[:8]],
+        "levels_total_percentiles": {str(q): float(np.percentile(L.sum(axis=0), q)) for q in (50, 90, 99, 100)},
         "levels_per_step_deepest": deepest.tolist(),
         "levels_per_step_mean": L.mean(axis=1).round(1).tolist(),
         "touching_mean": float(lv[..., 0].mean()), "touching_max": int(lv[..., 0].max()),
