@@ -69,43 +69,50 @@ __global__ __launch_bounds__(256) void draw_poses_kernel(const uint8_t* __restri
   for (int k = tid; k < kMtN; k += nt) s_mt[k] = g[k];
   int idx = (int)g[kMtN];
   __syncthreads();
-  const int need = 6 * N;  // three random() per agent, two words each
-  for (int got = 0; got < need;) {
-    if (idx >= kMtN) {
-      mt_twist(s_mt, tid, nt);
-      idx = 0;
+  // three random() per agent, two words each, in chunks of kMaxDrawWords / 6 agents (the stream's
+  // words stay in draw order: chunk after chunk, agent after agent)
+  constexpr int kChunk = kMaxDrawWords / 6;
+  for (int i0 = 0; i0 < N; i0 += kChunk) {
+    const int n = min(kChunk, N - i0);
+    const int need = 6 * n;
+    for (int got = 0; got < need;) {
+      if (idx >= kMtN) {
+        mt_twist(s_mt, tid, nt);
+        idx = 0;
+      }
+      const int take = min(kMtN - idx, need - got);
+      for (int w = tid; w < take; w += nt) s_w[got + w] = temper(s_mt[idx + w]);
+      got += take;
+      idx += take;
+      __syncthreads();
     }
-    const int take = min(kMtN - idx, need - got);
-    for (int w = tid; w < take; w += nt) s_w[got + w] = temper(s_mt[idx + w]);
-    got += take;
-    idx += take;
-    __syncthreads();
+    for (int q0 = tid; q0 < n; q0 += nt) {
+      const int i = i0 + q0;
+      double r[3];
+      for (int q = 0; q < 3; ++q) {  // random.random(): genrand_res53
+        const uint32_t a = s_w[6 * q0 + 2 * q] >> 5, b = s_w[6 * q0 + 2 * q + 1] >> 6;
+        r[q] = (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+      }
+      double x, y;
+      if (D.mode == kFlock) {  // mvmnt.py:62-63
+        x = D.spread * (r[0] - 0.5) + D.start_x;
+        y = D.spread * (r[1] - 0.5) + D.start_y;
+      } else {  // combat.py:83-84
+        x = r[0] * ((double)tdm_team_of(D.TP, i) + D.half_width);
+        y = r[1] * D.height;
+      }
+      const double a = (-1.0 + (1.0 - -1.0) * r[2]) * M_PI;  // random.uniform(-1, 1) * np.pi
+      pos[(size_t)e * N + i] = make_float2((float)x, (float)y);
+      angle[(size_t)e * N + i] = (float)a;
+    }
+    __syncthreads();  // the chunk's words are read before the next chunk overwrites them
   }
   for (int k = tid; k < kMtN; k += nt) g[k] = s_mt[k];
   if (tid == 0) g[kMtN] = (uint32_t)idx;
-  for (int i = tid; i < N; i += nt) {
-    double r[3];
-    for (int q = 0; q < 3; ++q) {  // random.random(): genrand_res53
-      const uint32_t a = s_w[6 * i + 2 * q] >> 5, b = s_w[6 * i + 2 * q + 1] >> 6;
-      r[q] = (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
-    }
-    double x, y;
-    if (D.mode == kFlock) {  // mvmnt.py:62-63
-      x = D.spread * (r[0] - 0.5) + D.start_x;
-      y = D.spread * (r[1] - 0.5) + D.start_y;
-    } else {  // combat.py:83-84
-      x = r[0] * ((double)tdm_team_of(D.TP, i) + D.half_width);
-      y = r[1] * D.height;
-    }
-    const double a = (-1.0 + (1.0 - -1.0) * r[2]) * M_PI;  // random.uniform(-1, 1) * np.pi
-    pos[(size_t)e * N + i] = make_float2((float)x, (float)y);
-    angle[(size_t)e * N + i] = (float)a;
-  }
 }
 
 hipError_t launch_draw_poses(const uint8_t* mask, uint32_t* mt, const PoseDraw& D, int n_envs, float2* pos,
                              float* angle, hipStream_t s) {
-  if (D.n_agents * 6 > kMaxDrawWords) return hipErrorInvalidValue;
   hipLaunchKernelGGL(draw_poses_kernel, dim3(n_envs), dim3(256), 0, s, mask, mt, D, pos, angle);
   return hipGetLastError();
 }

@@ -197,24 +197,35 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 // flags, listener, counters 0-2); each thread passes its force `F`. The physics skips the bodies
 // that are not alive (their contacts were destroyed with their proxies) and the env layer is TDM's:
 // the body state, the [N, N-1, 4] observation, done / winner, counter 3.
-template <typename OT, bool RECS_LDS, int MODE = kFlock>
+template <typename OT, bool RECS_LDS, int MODE = kFlock, int BPT = 1>
 __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers& B, int e, int cur,
                                          const void* __restrict__ actions, OT* __restrict__ obs,
                                          int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
                                          uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out,
                                          unsigned char* lds, const TdmParams* TP = nullptr,
-                                         const TdmBuffers* TB = nullptr, float2 F = make_float2(0.0f, 0.0f),
+                                         const TdmBuffers* TB = nullptr, const float2* F = nullptr,
                                          int held_slot = -1) {
+  // BPT bodies per thread (round 5, worlds above 1024 agents: blockDim.x = 1024, N <= BPT * 1024):
+  // thread t holds bodies t, t + BS, ..., t + (BPT - 1) BS; every per-body step below runs for each
+  // of them in that order, and every ordered reduction (block scans in body order, the pairwise
+  // reward sum) takes the chunks j = 0, 1, ... in turn, so the results are those of one thread per
+  // body. BPT = 1 is the form every other caller uses.
   constexpr bool kT = MODE == kTdm;
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
   const int N = P.n_agents;
   const int C = P.max_contacts;
-  const bool act = tid < N && (!kT || TB->alive[(size_t)e * N + tid] != 0);  // in the physics step
+  bool act[BPT];
+  size_t ag[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    act[j] = i < N && (!kT || TB->alive[(size_t)e * N + i] != 0);  // in the physics step
+    ag[j] = (size_t)e * N + i;
+  }
   // TDM: the living bodies, as the one wave's ballot (N <= 64, the wave kernel's hand-over) or as an
   // LDS bitmap (N > 64, the workgroup TDM step; filled below, read after the actions' barrier)
-  const unsigned long long livem = kT ? __ballot(act) : ~0ull;
-  const size_t ag = (size_t)e * N + tid;
+  const unsigned long long livem = kT ? __ballot(act[0]) : ~0ull;
   const int nxt = cur ^ 1;
   const Layout L = layout(N, RECS_LDS);
   float2* s_c = (float2*)(lds + L.c);
@@ -235,10 +246,14 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   uint32_t* s_alivew = (uint32_t*)(lds + L.alive);
   __syncthreads();  // the caller's last LDS accesses are done before the arrays are reused
   const bool wide = kT && N > W;
-  if (wide && (tid & (W - 1)) == 0) {  // wave w's ballot holds bodies 64w .. 64w + 63
-    const int q = 2 * (tid / W);
-    if (q < (N + 31) / 32) s_alivew[q] = (uint32_t)livem;
-    if (q + 1 < (N + 31) / 32) s_alivew[q + 1] = (uint32_t)(livem >> 32);
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {  // wave w's ballot of chunk j holds bodies j BS + 64w .. + 63
+    const unsigned long long m = j == 0 ? livem : __ballot(act[j]);
+    if (wide && (tid & (W - 1)) == 0) {
+      const int q = 2 * ((tid + j * BS) / W);
+      if (q < (N + 31) / 32) s_alivew[q] = (uint32_t)m;
+      if (q + 1 < (N + 31) / 32) s_alivew[q + 1] = (uint32_t)(m >> 32);
+    }
   }
   // both bodies of a pair take part in the physics (Flock: always)
   auto live2 = [&](int a, int b) -> bool {
@@ -272,63 +287,76 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const float2* cimp = B.cimp[cur] + (size_t)e * C;
   const int step_count = B.step_count[e];
   const int M = B.ccount[cur][e];
-  float2 p = make_float2(0.0f, 0.0f), v = make_float2(0.0f, 0.0f), tg = make_float2(0.0f, 0.0f);
-  float ang = 0.0f, slp = 0.0f;
-  float4 fo = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  int a0 = 1, a1 = 1, a2 = 1;
-  float ax = 0.0f, ay = 0.0f;
-  if (tid < N) {
-    p = B.pos[ag];
-    v = B.vel[ag];
-    ang = B.angle[ag];
-    fo = B.fat[ag];
-    slp = B.sleep[ag];
-    if constexpr (!kT) {
-      if (P.action_mode == MACM_ACTION_DISCRETE) {
-        const uint8_t* a = (const uint8_t*)actions + ag * 3;
-        a0 = a[0]; a1 = a[1]; a2 = a[2];
-      } else {
-        const float2 c = ((const float2*)actions)[ag];
-        ax = c.x; ay = c.y;
+  float2 p[BPT], v[BPT], tg[BPT];
+  float ang[BPT], slp[BPT];
+  float4 fo[BPT];
+  int a0[BPT], a1[BPT], a2[BPT];
+  float ax[BPT], ay[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    p[j] = v[j] = tg[j] = make_float2(0.0f, 0.0f);
+    ang[j] = slp[j] = 0.0f;
+    fo[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a0[j] = a1[j] = a2[j] = 1;
+    ax[j] = ay[j] = 0.0f;
+    if (i < N) {
+      p[j] = B.pos[ag[j]];
+      v[j] = B.vel[ag[j]];
+      ang[j] = B.angle[ag[j]];
+      fo[j] = B.fat[ag[j]];
+      slp[j] = B.sleep[ag[j]];
+      if constexpr (!kT) {
+        if (P.action_mode == MACM_ACTION_DISCRETE) {
+          const uint8_t* a = (const uint8_t*)actions + ag[j] * 3;
+          a0[j] = a[0]; a1[j] = a[1]; a2[j] = a[2];
+        } else {
+          const float2 c = ((const float2*)actions)[ag[j]];
+          ax[j] = c.x; ay[j] = c.y;
+        }
+        tg[j] = B.targets[(size_t)e * P.n_targets + B.tidx[i]];
       }
-      tg = B.targets[(size_t)e * P.n_targets + B.tidx[tid]];
+      s_c[i] = p[j];  // TDM: dead bodies' positions too (the observation)
     }
-    s_c[tid] = p;  // TDM: dead bodies' positions too (the observation)
   }
   for (int q = tid; q < (N + 31) / 32; q += BS) s_oldc[q] = 0u;
   for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0u;
   if (tid < 7) s_misc[tid] = 0;  // [7]: the slot (acquire_slot)
 
   // ---- actions -> angle, force (mvmnt.py:97-129) -------------------------------------------
-  float Fx = 0.0f, Fy = 0.0f;
-  if constexpr (kT) {
-    if (act) {
-      Fx = F.x;  // already m_force = 0 + F (the wave kernel's action loop)
-      Fy = F.y;
-    }
-  } else if (act) {
-    if (P.action_mode == MACM_ACTION_DISCRETE) {
-      float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
-      const double ad = (double)af;
-      if (fabs(ad) > M_PI) af = (float)(ad - sgn(ad) * (2.0 * M_PI));
-      ang = af;
-      const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
-      const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
-      double s0, c0, s1, c1;
-      act_trig(af, &s0, &c0, &s1, &c1);
-      Fx = (float)((c0 * k0 + c1 * k1) * cc * P.force);
-      Fy = (float)((s0 * k0 + s1 * k1) * cc * P.force);
-    } else {
-      float x = ax, y = ay;
-      if ((x * x + y * y) > 1.0f) {  // mvmnt.py:124-126 (the updated x, signs dropped)
-        x = sqrtf(x * x / (x * x + y * y));
-        y = sqrtf(y * y / (x * x + y * y));
+  float Fx[BPT], Fy[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    Fx[j] = Fy[j] = 0.0f;
+    if constexpr (kT) {
+      if (act[j]) {
+        Fx[j] = F[j].x;  // already m_force = 0 + F (the TDM step's action loop)
+        Fy[j] = F[j].y;
       }
-      Fx = x * P.force_f32;
-      Fy = y * P.force_f32;
+    } else if (act[j]) {
+      if (P.action_mode == MACM_ACTION_DISCRETE) {
+        float af = (float)((double)ang[j] + ((double)(a2[j] - 1) * P.rot_step) * P.inv_hz);
+        const double ad = (double)af;
+        if (fabs(ad) > M_PI) af = (float)(ad - sgn(ad) * (2.0 * M_PI));
+        ang[j] = af;
+        const double cc = ((a0[j] != 1) && (a1[j] != 1)) ? P.diag_c : 1.0;
+        const double k0 = (double)(a0[j] - 1), k1 = (double)(a1[j] - 1);
+        double s0, c0, s1, c1;
+        act_trig(af, &s0, &c0, &s1, &c1);
+        Fx[j] = (float)((c0 * k0 + c1 * k1) * cc * P.force);
+        Fy[j] = (float)((s0 * k0 + s1 * k1) * cc * P.force);
+      } else {
+        float x = ax[j], y = ay[j];
+        if ((x * x + y * y) > 1.0f) {  // mvmnt.py:124-126 (the updated x, signs dropped)
+          x = sqrtf(x * x / (x * x + y * y));
+          y = sqrtf(y * y / (x * x + y * y));
+        }
+        Fx[j] = x * P.force_f32;
+        Fy[j] = y * P.force_f32;
+      }
+      Fx[j] = 0.0f + Fx[j];  // m_force += force, from ClearForces' zero
+      Fy[j] = 0.0f + Fy[j];
     }
-    Fx = 0.0f + Fx;  // m_force += force, from ClearForces' zero
-    Fy = 0.0f + Fy;
   }
   __syncthreads();
 
@@ -371,17 +399,26 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     atomicAdd(&s_deg[ab >> 16], 1u);
   }
   __syncthreads();
-  const int deg = act ? (int)s_deg[tid] : 0;
+  int deg[BPT];
   {
-    int off;
-    block_scan_excl(deg, off, s_scan);
-    if (tid < N) s_off[tid] = (uint32_t)off;  // TDM: dead bodies too (s_off[b + 1] ends body b's edges)
+    int base = 0;  // the offsets of the chunks before (body order)
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int i = tid + j * BS;
+      deg[j] = act[j] ? (int)s_deg[i] : 0;
+      int off;
+      const int tot = block_scan_excl(deg[j], off, s_scan);
+      if (i < N) s_off[i] = (uint32_t)(base + off);  // TDM: dead bodies too (s_off[b + 1] ends body b's edges)
+      const unsigned long long m = __ballot(act[j] && deg[j] > 0);  // DFS seeds / unvisited bodies
+      if ((tid & (W - 1)) == 0 && i / W < (N + 63) / 64) s_todo[i / W] = m;
+      base += tot;
+    }
     if (tid == 0) s_off[N] = (uint32_t)(2 * T);
-    const unsigned long long m = __ballot(act && deg > 0);  // DFS seeds / unvisited bodies
-    if ((tid & (W - 1)) == 0 && tid / W < (N + 63) / 64) s_todo[tid / W] = m;
   }
   __syncthreads();
-  if (act) s_deg[tid] = s_off[tid];  // fill cursor
+#pragma unroll
+  for (int j = 0; j < BPT; ++j)
+    if (act[j]) s_deg[tid + j * BS] = s_off[tid + j * BS];  // fill cursor
   __syncthreads();
   for (int t = tid; t < T; t += BS) {
     const uint32_t ab = g_tab[t];
@@ -389,16 +426,19 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     g_adj[atomicAdd(&s_deg[ab >> 16], 1u)] = (uint32_t)t;
   }
   __syncthreads();
-  if (act && deg > 1) {  // insertion sort back into list order == Box2D edge order
-    const int o0 = (int)s_off[tid];
-    for (int x = o0 + 1; x < o0 + deg; ++x) {
-      const uint32_t key = g_adj[x];
-      int y = x - 1;
-      while (y >= o0 && g_adj[y] > key) {
-        g_adj[y + 1] = g_adj[y];
-        --y;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    if (act[j] && deg[j] > 1) {  // insertion sort back into list order == Box2D edge order
+      const int o0 = (int)s_off[tid + j * BS];
+      for (int x = o0 + 1; x < o0 + deg[j]; ++x) {
+        const uint32_t key = g_adj[x];
+        int y = x - 1;
+        while (y >= o0 && g_adj[y] > key) {
+          g_adj[y + 1] = g_adj[y];
+          --y;
+        }
+        g_adj[y + 1] = key;
       }
-      g_adj[y + 1] = key;
     }
   }
   __syncthreads();
@@ -451,10 +491,13 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
 
   // ---- integrate velocities + damping; island-ordered records with normals --------------------
-  if (act) {
-    const float vx = v.x + P.dt * (0.0f + P.inv_mass * Fx);  // gravityScale * gravity == 0
-    const float vy = v.y + P.dt * (0.0f + P.inv_mass * Fy);
-    s_v[tid] = make_float2(vx * P.damp, vy * P.damp);
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    if (act[j]) {
+      const float vx = v[j].x + P.dt * (0.0f + P.inv_mass * Fx[j]);  // gravityScale * gravity == 0
+      const float vy = v[j].y + P.dt * (0.0f + P.inv_mass * Fy[j]);
+      s_v[tid + j * BS] = make_float2(vx * P.damp, vy * P.damp);
+    }
   }
   for (int k = tid; k < nord; k += BS) {
     const int t = (int)g_ord[k];
@@ -538,20 +581,26 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   for (int k = tid; k < nord; k += BS) g_lam[g_ord[k]] = g_cim[k];  // StoreImpulses, list order
 
   // ---- integrate positions ----------------------------------------------------------------------
-  float cx = p.x, cy = p.y, vx = 0.0f, vy = 0.0f;
-  if (act) {
-    const float2 vv = s_v[tid];
-    vx = vv.x;
-    vy = vv.y;
-    const float tx = P.dt * vx, ty = P.dt * vy;
-    if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
-      const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
-      vx = vx * ratio;
-      vy = vy * ratio;
+  float cx[BPT], cy[BPT], vx[BPT], vy[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    cx[j] = p[j].x;
+    cy[j] = p[j].y;
+    vx[j] = vy[j] = 0.0f;
+    if (act[j]) {
+      const float2 vv = s_v[tid + j * BS];
+      vx[j] = vv.x;
+      vy[j] = vv.y;
+      const float tx = P.dt * vx[j], ty = P.dt * vy[j];
+      if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
+        const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
+        vx[j] = vx[j] * ratio;
+        vy[j] = vy[j] * ratio;
+      }
+      cx[j] = cx[j] + P.dt * vx[j];
+      cy[j] = cy[j] + P.dt * vy[j];
+      s_c[tid + j * BS] = make_float2(cx[j], cy[j]);
     }
-    cx = cx + P.dt * vx;
-    cy = cy + P.dt * vy;
-    s_c[tid] = make_float2(cx, cy);
   }
   __syncthreads();
 
@@ -587,12 +636,16 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
 
   // ---- sleep clock + island sleep decision (b2Island::Solve) --------------------------------------
-  float ns = 0.0f;
-  if (act) {
-    const bool moving = vx * vx + vy * vy > kLinearSleepTol * kLinearSleepTol;
-    ns = moving ? 0.0f : slp + P.dt;
-    s_slp[tid] = ns;
-    s_flag[tid] = (deg == 0 && ns >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
+  float ns[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    ns[j] = 0.0f;
+    if (act[j]) {
+      const bool moving = vx[j] * vx[j] + vy[j] * vy[j] > kLinearSleepTol * kLinearSleepTol;
+      ns[j] = moving ? 0.0f : slp[j] + P.dt;
+      s_slp[tid + j * BS] = ns[j];
+      s_flag[tid + j * BS] = (deg[j] == 0 && ns[j] >= kTimeToSleep && P.pos_iters > 0) ? 1 : 0;
+    }
   }
   __syncthreads();
   for (int I = tid; I < nisl; I += BS) {
@@ -605,76 +658,98 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   __syncthreads();
 
   // ---- SynchronizeFixtures: fat-AABB hysteresis ------------------------------------------------------
-  float4 fn = fo;
-  if (act) {
-    const float2 cc = s_c[tid];
-    cx = cc.x;
-    cy = cc.y;
-    const float r = P.radius;
-    const float c0x = p.x, c0y = p.y;
-    const float lox = bmin(c0x - r, cx - r), loy = bmin(c0y - r, cy - r);
-    const float hix = bmax(c0x + r, cx + r), hiy = bmax(c0y + r, cy + r);
-    const bool contains = fo.x <= lox && fo.y <= loy && hix <= fo.z && hiy <= fo.w;
-    if (!contains) {
-      fn = make_float4(lox - kAabbExtension, loy - kAabbExtension, hix + kAabbExtension, hiy + kAabbExtension);
-      const float dx = kAabbMultiplier * (cx - c0x), dy = kAabbMultiplier * (cy - c0y);
-      if (dx < 0.0f) fn.x += dx; else fn.z += dx;
-      if (dy < 0.0f) fn.y += dy; else fn.w += dy;
+  float4 fn[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    fn[j] = fo[j];
+    if (act[j]) {
+      const float2 cc = s_c[i];
+      cx[j] = cc.x;
+      cy[j] = cc.y;
+      const float r = P.radius;
+      const float c0x = p[j].x, c0y = p[j].y;
+      const float lox = bmin(c0x - r, cx[j] - r), loy = bmin(c0y - r, cy[j] - r);
+      const float hix = bmax(c0x + r, cx[j] + r), hiy = bmax(c0y + r, cy[j] + r);
+      const bool contains = fo[j].x <= lox && fo[j].y <= loy && hix <= fo[j].z && hiy <= fo[j].w;
+      if (!contains) {
+        fn[j] = make_float4(lox - kAabbExtension, loy - kAabbExtension, hix + kAabbExtension, hiy + kAabbExtension);
+        const float dx = kAabbMultiplier * (cx[j] - c0x), dy = kAabbMultiplier * (cy[j] - c0y);
+        if (dx < 0.0f) fn[j].x += dx; else fn[j].z += dx;
+        if (dy < 0.0f) fn[j].y += dy; else fn[j].w += dy;
+      }
+      if (s_flag[i]) {
+        vx[j] = 0.0f;
+        vy[j] = 0.0f;
+        ns[j] = 0.0f;
+      }
+      Rec r0;
+      r0.fn = fn[j];
+      r0.fo = fo[j];
+      r0.c = make_float2(cx[j], cy[j]);
+      recs[i] = r0;
+    } else if (kT && i < N) {  // a dead body: overlaps nothing, infinitely far
+      Rec r0;
+      r0.fn = r0.fo = make_float4(__builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff());
+      r0.c = make_float2(__builtin_inff(), __builtin_inff());
+      recs[i] = r0;
     }
-    if (s_flag[tid]) {
-      vx = 0.0f;
-      vy = 0.0f;
-      ns = 0.0f;
-    }
-    Rec r0;
-    r0.fn = fn;
-    r0.fo = fo;
-    r0.c = make_float2(cx, cy);
-    recs[tid] = r0;
-  } else if (kT && tid < N) {  // a dead body: overlaps nothing, infinitely far
-    Rec r0;
-    r0.fn = r0.fo = make_float4(__builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff());
-    r0.c = make_float2(__builtin_inff(), __builtin_inff());
-    recs[tid] = r0;
   }
   __syncthreads();
 
   // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour (mvmnt.py:185-196) ------------
   //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t); new contacts = Ov(F_t) \ Ov(F_{t-1})
-  bool coll = act && ((s_oldc[tid >> 5] >> (tid & 31)) & 1u);
-  int newcnt = 0;
-  float best = __builtin_inff();
-  int bj = tid == 0 ? 1 : 0;
-  if (act) {
-    for (int j = 0; j < N; ++j) {
-      const Rec r = recs[j];
-      const bool ovn = overlap(fn, r.fn);
-      const float dx = r.c.x - cx, dy = r.c.y - cy;
-      const float d2 = dx * dx + dy * dy;  // b2DistanceSquared(other, agent)
-      const bool other = j != tid;
-      coll |= other && ovn;
-      if (other && d2 < best) {  // strict '<': the lowest index wins ties (mvmnt.py:194)
-        best = d2;
-        bj = j;
+  bool coll[BPT];
+  int newcnt[BPT], bj[BPT];
+  float best[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    coll[j] = act[j] && ((s_oldc[i >> 5] >> (i & 31)) & 1u);
+    newcnt[j] = 0;
+    best[j] = __builtin_inff();
+    bj[j] = i == 0 ? 1 : 0;
+    if (act[j]) {
+      for (int q = 0; q < N; ++q) {
+        const Rec r = recs[q];
+        const bool ovn = overlap(fn[j], r.fn);
+        const float dx = r.c.x - cx[j], dy = r.c.y - cy[j];
+        const float d2 = dx * dx + dy * dy;  // b2DistanceSquared(other, agent)
+        const bool other = q != i;
+        coll[j] |= other && ovn;
+        if (other && d2 < best[j]) {  // strict '<': the lowest index wins ties (mvmnt.py:194)
+          best[j] = d2;
+          bj[j] = q;
+        }
+        if (q > i && ovn && !overlap(fo[j], r.fo)) ++newcnt[j];
       }
-      if (j > tid && ovn && !overlap(fo, r.fo)) ++newcnt;
     }
   }
   // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs -------------------------
   uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
   float2* ocimp = B.cimp[nxt] + (size_t)e * C;
-  int excl;
-  const int nnew = block_scan_excl(newcnt, excl, s_scan);
-  if (act && newcnt > 0) {
-    int w = nnew - excl - newcnt;  // agents > tid come first
-    for (int j = N - 1; j > tid; --j) {
-      const Rec r = recs[j];
-      if (overlap(fn, r.fn) && !overlap(fo, r.fo)) {
-        if (w < C) {
-          ocab[w] = (uint32_t)tid | ((uint32_t)j << 16);
-          ocimp[w] = make_float2(0.0f, 0.0f);
+  int excl[BPT];
+  int nnew = 0;  // the chunks' exclusive scans in body order, then the total
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int tot = block_scan_excl(newcnt[j], excl[j], s_scan);
+    excl[j] += nnew;
+    nnew += tot;
+  }
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    if (act[j] && newcnt[j] > 0) {
+      int w = nnew - excl[j] - newcnt[j];  // agents > i come first
+      for (int q = N - 1; q > i; --q) {
+        const Rec r = recs[q];
+        if (overlap(fn[j], r.fn) && !overlap(fo[j], r.fo)) {
+          if (w < C) {
+            ocab[w] = (uint32_t)i | ((uint32_t)q << 16);
+            ocimp[w] = make_float2(0.0f, 0.0f);
+          }
+          ++w;
         }
-        ++w;
       }
     }
   }
@@ -714,14 +789,18 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
 
   // ---- TDM: state write-back, TDM.get_obs (combat.py:166-167, 206-227), done / winner (:171-182) --------
   if constexpr (kT) {
-    if (tid < N) {
-      if (act) {
-        B.pos[ag] = make_float2(cx, cy);
-        B.vel[ag] = make_float2(vx, vy);
-        B.fat[ag] = fn;
-        B.sleep[ag] = ns;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int i = tid + j * BS;
+      if (i < N) {
+        if (act[j]) {
+          B.pos[ag[j]] = make_float2(cx[j], cy[j]);
+          B.vel[ag[j]] = make_float2(vx[j], vy[j]);
+          B.fat[ag[j]] = fn[j];
+          B.sleep[ag[j]] = ns[j];
+        }
+        s_slp[i] = ang[j];  // the sleep clocks are dead: the angles for the observation
       }
-      s_slp[tid] = ang;  // the sleep clocks are dead: the angles for the observation
     }
     // the observation reads only LDS: the slot goes back to the pool before the O(N^2) obs writes
     // (release_slot's barrier also orders the s_slp writes before the obs reads)
@@ -732,18 +811,22 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       tdm_obs_block_linear<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid,
                                BS, s_alivew, *TP, s_c, s_slp);
     else if (wide)
-      tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, s_alivew,
-                        *TP, s_c, s_slp);
+      for (int j = 0; j < BPT; ++j)
+        tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N,
+                          tid + j * BS, s_alivew, *TP, s_c, s_slp);
     else
       MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, livem,
                        *TP, s_c, s_slp);
     int alive_teams = 0, last_team = -1;
-    const int myteam = tdm_team_of(*TP, tid);
-    for (int t = 0; t < TP->n_teams; ++t)
-      if (__syncthreads_or(act && myteam == t)) {
+    for (int t = 0; t < TP->n_teams; ++t) {
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) any |= act[j] && tdm_team_of(*TP, tid + j * BS) == t;
+      if (__syncthreads_or(any)) {
         ++alive_teams;
         last_team = t;
       }
+    }
     if (tid == 0) {
       const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz
       uint8_t dn = tp > P.time_limit ? 1 : 0;
@@ -770,33 +853,65 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     }
   } else {
     // ---- rewards (mvmnt.py:160-179) + obs (mvmnt.py:181-222) -------------------------------------------
-    float rew = 0.0f;
-    if (act) {
-      const float tdx = tg.x - cx, tdy = tg.y - cy;  // target - agent.body.position
-      const float td2 = tdx * tdx + tdy * tdy;
-      const double d = sqrt((double)td2);
-      if (coll) rew = -1.0f;
-      else if (P.reward_mode == MACM_REWARD_LINEAR) rew = (float)((-d / 35) + 1);
-      else rew = (d < P.reward_radius) ? 1.0f : 0.0f;
-      rew_out[ag] = rew;
-      if (coll_out) coll_out[ag] = coll ? 1 : 0;
-      if (nbr_out) nbr_out[ag] = bj;
-      if (obs) {
-        const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
-        const float2 cb = recs[bj].c;
-        write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
+    float rew[BPT];
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      rew[j] = 0.0f;
+      if (act[j]) {
+        const float tdx = tg[j].x - cx[j], tdy = tg[j].y - cy[j];  // target - agent.body.position
+        const float td2 = tdx * tdx + tdy * tdy;
+        const double d = sqrt((double)td2);
+        if (coll[j]) rew[j] = -1.0f;
+        else if (P.reward_mode == MACM_REWARD_LINEAR) rew[j] = (float)((-d / 35) + 1);
+        else rew[j] = (d < P.reward_radius) ? 1.0f : 0.0f;
+        rew_out[ag[j]] = rew[j];
+        if (coll_out) coll_out[ag[j]] = coll[j] ? 1 : 0;
+        if (nbr_out) nbr_out[ag[j]] = bj[j];
+        if (obs) {
+          const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+          const float2 cb = recs[bj[j]].c;
+          write_obs<OT>(obs + ag[j] * od, P.coord, ang[j], best[j], cb.x - cx[j], cb.y - cy[j], tdx, tdy, td2);
+        }
       }
     }
-    int dummy;
-    const int ncoll = block_scan_excl(act && coll ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
-    const int npos = block_scan_excl(act && rew > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
-    const double rsum = block_pairwise_sum((double)rew, reinterpret_cast<double*>(s_scan));  // thread 0
-    if (act) {
-      B.pos[ag] = make_float2(cx, cy);
-      B.vel[ag] = make_float2(vx, vy);
-      B.angle[ag] = ang;
-      B.fat[ag] = fn;
-      B.sleep[ag] = ns;
+    int dummy, ncoll = 0, npos = 0;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      ncoll += block_scan_excl(act[j] && coll[j] ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
+      npos += block_scan_excl(act[j] && rew[j] > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
+    }
+    double rsum;  // thread 0: the step's reward sum in agent-slot order (flock_common.hpp)
+    if constexpr (BPT == 1) {
+      rsum = block_pairwise_sum((double)rew[0], reinterpret_cast<double*>(s_scan));
+    } else {
+      double* s_grp = reinterpret_cast<double*>(s_slp);  // the sleep clocks are dead: 64-body group sums
+      const int gw = BS / W;
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        const double g = wave_pairwise_sum((double)rew[j]);
+        if ((tid & (W - 1)) == 0) s_grp[j * gw + tid / W] = g;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        const int ng = BPT * gw;
+        int n2 = 1;
+        while (n2 < ng) n2 <<= 1;
+        for (int q = ng; q < n2; ++q) s_grp[q] = 0.0;
+        for (int h = 1; h < n2; h <<= 1)
+          for (int q = 0; q + h < n2; q += 2 * h) s_grp[q] = s_grp[q] + s_grp[q + h];
+        rsum = s_grp[0];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      if (act[j]) {
+        B.pos[ag[j]] = make_float2(cx[j], cy[j]);
+        B.vel[ag[j]] = make_float2(vx[j], vy[j]);
+        B.angle[ag[j]] = ang[j];
+        B.fat[ag[j]] = fn[j];
+        B.sleep[ag[j]] = ns[j];
+      }
     }
     if (tid == 0) {
       const double tp = B.time_passed[e] + P.inv_hz;  // time_passed += 1/hz (mvmnt.py:134-136)

@@ -1220,9 +1220,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
                                 ctr[1] + (unsigned long long)__popcll(att_m));
         B.env_counters[(size_t)e * 4 + 2] = ctr[2] + (unsigned long long)__popcll(alive0_m & ~livem);
       }
+      const float2 F1 = make_float2(Fx, Fy);
       spill::step_env<OT, false, kTdm>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out,
-                                        reinterpret_cast<unsigned char*>(&s_pool), &TP, &TB, make_float2(Fx, Fy),
-                                        slot);
+                                        reinterpret_cast<unsigned char*>(&s_pool), &TP, &TB, &F1, slot);
       return;
     }
 #endif

@@ -1150,10 +1150,9 @@ __host__ __device__ inline WgLayoutD wg_layout_d(int N, int tcap) {
 // contact took 45 KB, 3 per CU): a contact is new iff its other body has not been popped yet (the
 // first of its two bodies to be popped walks it), and the walk writes the edge's CSR slot, which
 // the record pass turns into the contact through x_adj.
-__global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B, int tcap) {
+__device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers& B, int tcap, int e, unsigned char* lds) {
   using namespace wg;
-  extern __shared__ __align__(16) unsigned char lds[];
-  const int e = wg_env(B), lane = threadIdx.x, N = P.n_agents;
+  const int lane = threadIdx.x, N = P.n_agents;
   const int tid = lane;  // WSTAMP
   (void)tid;
   if (B.x_nisl[e] != kDfsPending) return;  // kernel A walked it, or the spill step stepped it
@@ -1371,6 +1370,11 @@ __global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B,
   WSTAMP(28);
 }
 
+__global__ __launch_bounds__(64) void flock_dfs_wg(StepParams P, WorldBuffers B, int tcap) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  dfs_env(P, B, tcap, wg_env(B), lds);
+}
+
 namespace wg {
 
 // One Gauss-Seidel velocity constraint (b2ContactSolver::SolveVelocityConstraints, one point,
@@ -1447,11 +1451,10 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
 #ifndef MACM_LEVEL_UNROLL  // A/B knob: level steps per loop iteration (1 or 2)
 #define MACM_LEVEL_UNROLL 2
 #endif
-__global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap, Handoff H) {
+__device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffers& B, int tcap, int e,
+                                          unsigned char* lds) {
   using namespace wg;
-  extern __shared__ __align__(16) unsigned char lds[];
-  const int e = wg_env(B), lane = threadIdx.x, N = P.n_agents;
-  const HandoffPublish publish(H, e);  // to kernel C when this body ends (any return)
+  const int lane = threadIdx.x, N = P.n_agents;
   const int IS = wg_isl_stride(N);
   float2* s_v = (float2*)lds;
   float2* s_c = s_v + N;
@@ -1684,6 +1687,23 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   if (lane == 0) B.stamps[(size_t)e * 32 + 12] = (unsigned long long)B.x_nlvl[e] | ((unsigned long long)nc << 32);
 #endif
   for (int i = lane; i < N; i += W) st_wt(B.x_cout + en + i, s_c[i]);
+}
+
+// Kernel B, and with FUSED the dense envs' DFS first in the same wave (kernel A2 + B: one launch, an
+// env's solve starting as soon as its own walk ends instead of after the slowest env's walk; the
+// walk's records reach the solve through this wave's own global stores, ordered by a
+// workgroup-scope fence; the LDS is the larger of the two layouts, 8 waves per CU either way at C5).
+template <bool FUSED>
+__global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap, Handoff H) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int e = wg_env(B);
+  const HandoffPublish publish(H, e);  // to kernel C when this body ends (any return)
+  if constexpr (FUSED) {
+    dfs_env(P, B, tcap, e, lds);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __syncthreads();
+  }
+  solve_env(P, B, tcap, e, lds);
 }
 
 template <typename OT>
@@ -2214,6 +2234,20 @@ int wg_lds_bytes(int N, int tcap) {
 // Raise the dynamic-LDS limit of the workgroup kernels (world creation). The limit is a property of
 // the kernel, not of a world: it only ever grows (per device), so creating a world of fewer agents
 // after a larger one cannot make the larger world's launches fail.
+// kernel B with the dense envs' DFS in the same wave (flock_solve_wg<true>): the larger LDS layout
+static int wg_fused_lds(int N, int tcap) {
+  const int d = wg::wg_layout_d(N, tcap).total, b = wg_solve_lds(N);
+  return d > b ? d : b;
+}
+// MACM_FUSE_DFS overrides the default (A/B sessions)
+#ifndef MACM_FUSE_DFS_DEFAULT
+#define MACM_FUSE_DFS_DEFAULT 0
+#endif
+static bool fuse_dfs() {
+  const char* x = getenv("MACM_FUSE_DFS");
+  return wg::kDfsKernel && (x ? atoi(x) : MACM_FUSE_DFS_DEFAULT) != 0;
+}
+
 hipError_t wg_configure(int N, int tcap) {
   static std::mutex mu;
   static std::map<int, int> high;  // device -> the largest N configured
@@ -2228,11 +2262,11 @@ hipError_t wg_configure(int N, int tcap) {
   for (const void* f : fi)
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, wg_init_lds_bytes(N));
   const void* fsplit[] = {(const void*)flock_step_wg_a<float>, (const void*)flock_step_wg_a<double>,
-                          (const void*)flock_solve_wg, (const void*)flock_step_wg_c<float>,
-                          (const void*)flock_step_wg_c<double>};
+                          (const void*)flock_solve_wg<false>, (const void*)flock_step_wg_c<float>,
+                          (const void*)flock_step_wg_c<double>, (const void*)flock_solve_wg<true>};
   const int la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
-  const int lsplit[] = {la, la, wg_solve_lds(N), lc, lc};
-  for (int i = 0; i < 5; ++i)
+  const int lsplit[] = {la, la, wg_solve_lds(N), lc, lc, wg_fused_lds(N, tcap)};
+  for (int i = 0; i < 6; ++i)
     if (e == hipSuccess) e = hipFuncSetAttribute(fsplit[i], hipFuncAttributeMaxDynamicSharedMemorySize, lsplit[i]);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)flock_dfs_wg, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2274,8 +2308,12 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   else
     hipLaunchKernelGGL(flock_step_wg_a<float>, grid, block, la, s, P, B, cur, tcap, actions, (float*)obs, nbr, rew,
                        coll, done);
-  if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
-  hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
+  if (fuse_dfs()) {
+    hipLaunchKernelGGL(flock_solve_wg<true>, grid, dim3(64), wg_fused_lds(N, tcap), s, P, B, tcap, H);
+  } else {
+    if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
+    hipLaunchKernelGGL(flock_solve_wg<false>, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
+  }
   if (!H.q) {
     launch_c(s);
     return hipGetLastError();

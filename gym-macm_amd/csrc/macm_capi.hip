@@ -58,6 +58,16 @@ hipError_t launch_bots_flock(const void* obs, bool obs_f64, int od, long long ro
 hipError_t launch_bots_combat(const void* obs, const uint8_t* mask, bool obs_f64, int N, long long rows,
                               uint8_t* act, hipStream_t s);
 hipError_t wg_configure(int N, int tcap);
+// worlds of 1024 < N <= 4096 agents (flock_big.hip)
+hipError_t big_configure(int N);
+int big_step_lds(int N);
+int big_init_lds(int N);
+hipError_t launch_step_big(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
+                           bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
+hipError_t launch_init_big(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr,
+                           const uint8_t* mask, hipStream_t s);
+hipError_t launch_observe_big(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
+                              hipStream_t s);
 int wg_block(int N);
 int wg_lds_bytes(int N, int tcap);
 hipError_t launch_check_actions(const void* actions, int mode, const uint8_t* alive, long long rows,
@@ -75,6 +85,7 @@ struct macm_world {
   int cur;  // which contact-list buffer holds the current ordered list
   int device;
   bool wave;  // N <= 64: one wavefront per env (flock_step_w64); else one workgroup per env
+  bool big;   // N > 1024: the spill step with several bodies per thread (flock_big.hip)
   int tcap;   // touching-contact capacity per env of the fast kernels (more: the spill step)
   std::vector<int32_t> tidx;
   std::vector<void*> allocs;
@@ -262,6 +273,10 @@ static int solo_envs() {
   return n > 0 ? n : 0;
 }
 
+// The most agents per env (Flock and TDM): one workgroup of 1024 threads, up to 4 bodies per thread
+// (flock_big.hip, the spill step's BPT), 16-bit body ids in the lists (b < 32768 with a flag bit)
+constexpr int kMaxAgents = 4096;
+
 Capacity default_capacity(int N, int E, int64_t max_contacts, size_t free_bytes) {
   const int64_t all_pairs = (int64_t)N * (N - 1) / 2;
   const int64_t budget = std::max<int64_t>((int64_t)(free_bytes / 8), 256LL << 20);
@@ -303,6 +318,7 @@ hipError_t launch_init(macm_world* w, const macm_outputs* out, const uint8_t* ma
   void* obs = out ? out->obs : nullptr;
   int32_t* nbr = out ? out->nbr_id : nullptr;
   if (w->wave) return launch_init_w64(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, mask, s);
+  if (w->big) return launch_init_big(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, mask, s);
   return launch_init_wg(w->P, w->B, w->cur, obs, w->cfg.obs_f64 != 0, nbr, mask, s);
 }
 
@@ -318,8 +334,8 @@ void save_stream(std::vector<uint32_t>& host, int e, const PyMT19937& r) {
 extern "C" {
 
 const char* macm_version(void) {
-  return "macm-hip 0.5.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernels N<=1024, "
-         "spill step for dense envs; TDM: wave-per-env kernel N<=64, workgroup step N<=1024)";
+  return "macm-hip 0.6.0 (gfx950; Flock: wave-per-env kernel N<=64, workgroup-per-env kernels N<=1024, "
+         "spill step for dense envs and N<=4096; TDM: wave-per-env kernel N<=64, workgroup step N<=4096)";
 }
 int macm_abi_version(void) { return MACM_ABI_VERSION; }
 const char* macm_last_error(void) { return g_last_error.c_str(); }
@@ -360,8 +376,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   const macm_config& c = *cfg;
   if (n_envs <= 0) return fail(MACM_E_INVALID, "n_envs must be > 0");
   if (c.n_agents < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2 (get_obs needs another agent)");
-  if (c.n_agents > 1024)
-    return fail(MACM_E_UNSUPPORTED, "n_agents > 1024 is not built (one workgroup per env, <= 1024 threads)");
+  if (c.n_agents > kMaxAgents)
+    return fail(MACM_E_UNSUPPORTED, "n_agents > 4096 is not built (one workgroup per env, <= 4 bodies per thread)");
   if (c.n_targets < 1) return fail(MACM_E_INVALID, "n_targets must be >= 1");
   if (!(c.hz > 0.0)) return fail(MACM_E_INVALID, "hz must be > 0");
   if (c.velocity_iterations < 0 || c.position_iterations < 0) return fail(MACM_E_INVALID, "iterations < 0");
@@ -396,11 +412,12 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   w->cur = 0;
   w->tidx = tidx;
   w->wave = N <= 64;
+  w->big = N > 1024;  // flock_big.hip: the spill step with several bodies per thread
   w->solo.n = w->wave ? solo_envs() : 0;
   {
     const int bs = N <= 64 ? 64 : wg_block(N);
     const int want = N <= 64 ? 256 : 5 * bs;  // register staging holds 5 records per thread
-    w->tcap = want < 4608 ? want : 4608;
+    w->tcap = w->big ? C : want < 4608 ? want : 4608;  // big: every touching contact takes the spill step
   }
   StepParams& P = w->P;
   P.n_envs = n_envs;
@@ -436,8 +453,8 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
 #ifdef MACM_STAMPS
       || (rc = dalloc(w, &B.stamps, (size_t)n_envs * 32))
 #endif
-      || (!w->wave && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap))) ||
-      (!w->wave && ((rc = dalloc(w, &B.x_cst, (size_t)n_envs * w->tcap)) ||
+      || (!w->wave && !w->big && (rc = dalloc(w, &B.scratch, (size_t)n_envs * w->tcap))) ||
+      (!w->wave && !w->big && ((rc = dalloc(w, &B.x_cst, (size_t)n_envs * w->tcap)) ||
                     (rc = dalloc(w, &B.x_cimp, (size_t)n_envs * w->tcap)) ||
                     (rc = dalloc(w, &B.x_ord, (size_t)n_envs * w->tcap)) ||
                     (rc = dalloc(w, &B.x_ic, (size_t)n_envs * (N / 2 + 2))) ||
@@ -480,7 +497,16 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   w->slots_alloc = (int)SL;
   w->pool0 = B.sp_pool;
   if (e == hipSuccess && B.sp_lock) e = hipMemset(B.sp_lock, 0, sizeof(uint32_t) * SL);
-  if (e == hipSuccess && !w->wave) {
+  if (e == hipSuccess && w->big) {
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e == hipSuccess && (size_t)std::max(big_step_lds(N), big_init_lds(N)) > prop.sharedMemPerBlock) {
+      free_world(w);
+      delete w;
+      return fail(MACM_E_UNSUPPORTED, "per-env LDS layout exceeds the device's LDS per workgroup");
+    }
+    if (e == hipSuccess) e = big_configure(N);
+  } else if (e == hipSuccess && !w->wave) {
     hipDeviceProp_t prop;
     e = hipGetDeviceProperties(&prop, device);
     if (e == hipSuccess && (size_t)wg_lds_bytes(N, w->tcap) > prop.sharedMemPerBlock) {
@@ -625,7 +651,7 @@ static int overflow_error(uint32_t st) {
 #endif
 static constexpr bool kHandoffDefault = MACM_HANDOFF_DEFAULT != 0;
 static HandoffStream* handoff_for(macm_world* w) {
-  if (w->wave || w->ho_tried) return w->ho;
+  if (w->wave || w->big || w->ho_tried) return w->ho;
   w->ho_tried = true;
   const char* v = getenv("MACM_HANDOFF");
   if (!(v ? atoi(v) != 0 : kHandoffDefault)) return nullptr;
@@ -659,6 +685,9 @@ int macm_world_step(macm_world* w, const void* actions, const macm_outputs* out,
   }
   if (w->wave)
     HIP_TRY(launch_step_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
+                            out->collided, out->done, (hipStream_t)stream));
+  else if (w->big)
+    HIP_TRY(launch_step_big(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
                             out->collided, out->done, (hipStream_t)stream));
   else
     HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id,
@@ -822,7 +851,7 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
     return MACM_OK;
   }
   const unsigned char* act = static_cast<const unsigned char*>(actions);
-  if (w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents)
+  if (!w->big && w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents)
     return rollout_wg_slices(w, kSlices, act, n_steps, astride, out, traj, s);
   // workgroup path: its three launches per step (and the bot's), in order
   const long long rows = (long long)w->P.n_envs * w->P.n_agents;
@@ -830,8 +859,12 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
   for (int k = 0; k < n_steps; ++k) {
     const macm_outputs ok = step_outputs(w, out, k, traj);
     const unsigned char* act_k = act + k * kstride;
-    HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, act_k, ok.obs, w->cfg.obs_f64 != 0, ok.nbr_id, ok.reward,
-                           ok.collided, ok.done, s, handoff_for(w)));
+    if (w->big)
+      HIP_TRY(launch_step_big(w->P, w->B, w->cur, act_k, ok.obs, w->cfg.obs_f64 != 0, ok.nbr_id, ok.reward,
+                              ok.collided, ok.done, s));
+    else
+      HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, act_k, ok.obs, w->cfg.obs_f64 != 0, ok.nbr_id, ok.reward,
+                             ok.collided, ok.done, s, handoff_for(w)));
     w->cur ^= 1;
     if (bots)
       HIP_TRY(launch_bots_flock(ok.obs, w->cfg.obs_f64 != 0, obs_dim(w->cfg), rows,
@@ -863,6 +896,8 @@ int macm_world_observe(macm_world* w, const macm_outputs* out, void* stream) {
   DeviceGuard g(w->device);
   if (w->wave)
     HIP_TRY(launch_observe_w64(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
+  else if (w->big)
+    HIP_TRY(launch_observe_big(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
   else
     HIP_TRY(launch_observe_wg(w->P, w->B, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, (hipStream_t)stream));
   return MACM_OK;
@@ -1137,7 +1172,7 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
   if (N < 2) return fail(MACM_E_INVALID, "n_agents must be >= 2");
   // N > 64: the workgroup step (tdm_step_wg.hip), one thread per agent and 16-bit body ids in the
   // contact list, as the Flock workgroup path
-  if (N > 1024) return fail(MACM_E_UNSUPPORTED, "TDM with more than 1024 agents per env is not built");
+  if (N > kMaxAgents) return fail(MACM_E_UNSUPPORTED, "TDM with more than 4096 agents per env is not built");
   if (!(c.hz > 0.0)) return fail(MACM_E_INVALID, "hz must be > 0");
   if (c.velocity_iterations < 0 || c.position_iterations < 0) return fail(MACM_E_INVALID, "iterations < 0");
   if (!(c.radius > 0.0f)) return fail(MACM_E_INVALID, "radius must be > 0");

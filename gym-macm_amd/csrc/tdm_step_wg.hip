@@ -1,8 +1,9 @@
-// tdm_step_wg.hip — TDM.step (gym_macm/envs/combat.py:104-184) for 64 < N <= 1024 agents per env:
+// tdm_step_wg.hip — TDM.step (gym_macm/envs/combat.py:104-184) for 64 < N <= 4096 agents per env:
 // the reference takes any team sizes (combat.py:82-83) in an uncapped b2World (cm_framework.py:161);
 // the wave kernel (flock_step_w64.hip, env_step_w64<kTdm>) holds one agent per lane, N <= 64.
 //
-// One workgroup per env, one thread per agent (blockDim = N rounded up to 64):
+// One workgroup per env, one thread per agent (blockDim = N rounded up to 64); above 1024 agents 1024
+// threads with 2 or 4 agents each (round 5: the pair records then in HBM):
 //   1. the action loop (combat.py:121-155) exactly as the wave kernel's: rotation (f32
 //      SetTransform), force with the movement penalty, cooldowns, and the melee ray casts. Bodies do
 //      not move during the loop and deaths come after it, so every cast sees the same world and all
@@ -65,12 +66,13 @@ __host__ __device__ constexpr ObsLayout obs_layout(int N) {
   return L;
 }
 
-// wave w's ballot -> words 2w, 2w + 1 of an LDS bitmap of N bits (call with the whole block)
-__device__ __forceinline__ void ballot_bits(uint32_t* bits, int N, bool v) {
+// wave w's ballot of body chunk j (bodies j BS + 64w ..) -> words 2 (j BS / 64 + w), + 1 of an LDS
+// bitmap of N bits (call with the whole block)
+__device__ __forceinline__ void ballot_bits(uint32_t* bits, int N, bool v, int j = 0) {
   const unsigned long long m = __ballot(v);
   const int tid = threadIdx.x;
   if ((tid & (W - 1)) == 0) {
-    const int q = 2 * (tid / W);
+    const int q = 2 * ((tid + j * (int)blockDim.x) / W);
     if (q < words(N)) bits[q] = (uint32_t)m;
     if (q + 1 < words(N)) bits[q + 1] = (uint32_t)(m >> 32);
   }
@@ -79,19 +81,22 @@ __device__ __forceinline__ void ballot_bits(uint32_t* bits, int N, bool v) {
 }  // namespace tdmwg
 
 int tdm_wg_step_lds(int N) {
-  const int a = tdmwg::pre_layout(N).total, b = spill::layout(N, true).total;
+  // N > 1024 (BPT > 1): the pair records in HBM (spill step RECS_LDS = false)
+  const int a = tdmwg::pre_layout(N).total, b = spill::layout(N, N <= 1024).total;
   return a > b ? a : b;
 }
 int tdm_wg_obs_lds(int N) { return tdmwg::obs_layout(N).total; }
 
-template <typename OT>
+// BPT bodies per thread (round 5: N up to 4096 with 1024 threads; thread t holds t, t + BS, ...); BPT = 1
+// with blockDim = N rounded up to 64 below 1024 agents. Every ordered step (the listener and damage in
+// agent order on thread 0, the spill step's scans) sees the bodies in agent order either way.
+template <typename OT, int BPT = 1>
 __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
                                                     int cur, const uchar4* __restrict__ actions,
                                                     OT* __restrict__ obs, uint8_t* __restrict__ done_out) {
   using namespace tdmwg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x, tid = threadIdx.x, N = P.n_agents;
-  const size_t ag = (size_t)e * N + tid;
+  const int e = blockIdx.x, tid = threadIdx.x, BS = blockDim.x, N = P.n_agents;
   const PreLayout L = pre_layout(N);
   float2* s_c = (float2*)(lds + L.c);
   double* s_hpd = (double*)(lds + L.hp);
@@ -111,69 +116,78 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
     }
     return;
   }
-  bool act = false;
-  float2 p = make_float2(0.0f, 0.0f);
-  float ang = 0.0f;
-  int a0 = 1, a1 = 1, a2 = 1, a3 = 0;
-  double hp = 0.0, cda = 0.0, cdm = 0.0;  // Agent.health, cooldown_atk, cooldown_mov_penalty
-  if (tid < N) {
-    p = B.pos[ag];
-    ang = B.angle[ag];
-    const uchar4 a = actions[ag];
-    a0 = a.x;
-    a1 = a.y;
-    a2 = a.z;
-    a3 = a.w;
-    act = TB.alive[ag] != 0;
-    hp = TB.health[ag];
-    cda = TB.cd_atk[ag];
-    cdm = TB.cd_mov[ag];
-    s_c[tid] = p;
-    s_hpd[tid] = hp;
-  }
-  const bool act0 = act;  // alive when the step starts (acts this step)
-
-  // ---- the action loop (combat.py:121-155), as env_step_w64<kTdm> ------------------------------
-  float Fx = 0.0f, Fy = 0.0f;
-  bool attacking = false;
-  float ray_x = 0.0f, ray_y = 0.0f;
-  if (act) {
-    // agent.body.angle = angle + (a2-1) * rotation_speed * (1/hz) -> SetTransform(float32)
-    float af = (float)((double)ang + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
-    const double ad = (double)af;
-    if (fabs(ad) > M_PI) af = (float)(ad - sgn(ad) * (2.0 * M_PI));
-    ang = af;
-    const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
-    const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
-    // Agent.force = _force * (1 - percent_mov_penalty * int(cooldown_mov_penalty > 0))   combat.py:46-49
-    const double force = P.force * (1.0 - TP.percent_mov_penalty * (double)(cdm > 0.0));
-    double s0, c0, s1, c1;  // np.cos / np.sin of angle and angle + pi/2
-    act_trig(af, &s0, &c0, &s1, &c1);
-    Fx = 0.0f + (float)((c0 * k0 + c1 * k1) * cc * force);  // ApplyForce onto ClearForces' zero
-    Fy = 0.0f + (float)((s0 * k0 + s1 * k1) * cc * force);
-    if (cda <= 0.0) {
-      if (a3) {
-        attacking = true;
-        // point2 = point1 + (range*cos(angle), range*sin(angle)): a float32 add of the
-        // float32-converted tuple
-        ray_x = p.x + (float)(TP.melee_range * c0);
-        ray_y = p.y + (float)(TP.melee_range * s0);
-        cda = TP.cooldown_atk;
-        cdm = TP.cooldown_mov_penalty;
-      }
-    } else {
-      cda -= P.inv_hz;
-      if (TP.decay_mov_penalty) cdm -= P.inv_hz;
+  bool act[BPT], act0[BPT], attacking[BPT];
+  float2 p[BPT], F[BPT];
+  float ang[BPT], ray_x[BPT], ray_y[BPT];
+  double hp[BPT], cda[BPT], cdm[BPT];  // Agent.health, cooldown_atk, cooldown_mov_penalty
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    const size_t ag = (size_t)e * N + i;
+    act[j] = false;
+    p[j] = F[j] = make_float2(0.0f, 0.0f);
+    ang[j] = ray_x[j] = ray_y[j] = 0.0f;
+    hp[j] = cda[j] = cdm[j] = 0.0;
+    attacking[j] = false;
+    int a0 = 1, a1 = 1, a2 = 1, a3 = 0;
+    if (i < N) {
+      p[j] = B.pos[ag];
+      ang[j] = B.angle[ag];
+      const uchar4 a = actions[ag];
+      a0 = a.x;
+      a1 = a.y;
+      a2 = a.z;
+      a3 = a.w;
+      act[j] = TB.alive[ag] != 0;
+      hp[j] = TB.health[ag];
+      cda[j] = TB.cd_atk[ag];
+      cdm[j] = TB.cd_mov[ag];
+      s_c[i] = p[j];
+      s_hpd[i] = hp[j];
     }
+    act0[j] = act[j];  // alive when the step starts (acts this step)
+
+    // ---- the action loop (combat.py:121-155), as env_step_w64<kTdm> ------------------------------
+    if (act[j]) {
+      // agent.body.angle = angle + (a2-1) * rotation_speed * (1/hz) -> SetTransform(float32)
+      float af = (float)((double)ang[j] + ((double)(a2 - 1) * P.rot_step) * P.inv_hz);
+      const double ad = (double)af;
+      if (fabs(ad) > M_PI) af = (float)(ad - sgn(ad) * (2.0 * M_PI));
+      ang[j] = af;
+      const double cc = ((a0 != 1) && (a1 != 1)) ? P.diag_c : 1.0;
+      const double k0 = (double)(a0 - 1), k1 = (double)(a1 - 1);
+      // Agent.force = _force * (1 - percent_mov_penalty * int(cooldown_mov_penalty > 0))   combat.py:46-49
+      const double force = P.force * (1.0 - TP.percent_mov_penalty * (double)(cdm[j] > 0.0));
+      double s0, c0, s1, c1;  // np.cos / np.sin of angle and angle + pi/2
+      act_trig(af, &s0, &c0, &s1, &c1);
+      F[j].x = 0.0f + (float)((c0 * k0 + c1 * k1) * cc * force);  // ApplyForce onto ClearForces' zero
+      F[j].y = 0.0f + (float)((s0 * k0 + s1 * k1) * cc * force);
+      if (cda[j] <= 0.0) {
+        if (a3) {
+          attacking[j] = true;
+          // point2 = point1 + (range*cos(angle), range*sin(angle)): a float32 add of the
+          // float32-converted tuple
+          ray_x[j] = p[j].x + (float)(TP.melee_range * c0);
+          ray_y[j] = p[j].y + (float)(TP.melee_range * s0);
+          cda[j] = TP.cooldown_atk;
+          cdm[j] = TP.cooldown_mov_penalty;
+        }
+      } else {
+        cda[j] -= P.inv_hz;
+        if (TP.decay_mov_penalty) cdm[j] -= P.inv_hz;
+      }
+    }
+    ballot_bits(s_aw, N, act[j], j);
+    ballot_bits(s_atw, N, attacking[j], j);
   }
-  ballot_bits(s_aw, N, act);
-  ballot_bits(s_atw, N, attacking);
   __syncthreads();  // positions, health and both bitmaps visible
 
   // ---- ray casts: b2World::RayCast + RayCastClosestCallback (cm_framework.py:56-86) --------------
-  if (attacking) {
+#pragma unroll
+  for (int jj = 0; jj < BPT; ++jj) {
+    if (!attacking[jj]) continue;
     int hit = -1;
-    const float rvx = ray_x - p.x, rvy = ray_y - p.y;  // r = p2 - p1
+    const float rvx = ray_x[jj] - p[jj].x, rvy = ray_y[jj] - p[jj].y;  // r = p2 - p1
     const float rrr = rvx * rvx + rvy * rvy;
     const float rad2 = P.radius * P.radius;
     float maxf = 1.0f;
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
       for (uint32_t m = s_aw[q]; m; m &= m - 1u) {
         const int j = 32 * q + __builtin_ctz(m);
         const float2 cj = s_c[j];
-        const float sx = p.x - cj.x, sy = p.y - cj.y;  // s = p1 - position
+        const float sx = p[jj].x - cj.x, sy = p[jj].y - cj.y;  // s = p1 - position
         const float bb = (sx * sx + sy * sy) - rad2;
         const float c = sx * rvx + sy * rvy;
         const float sigma = c * c - rrr * bb;
@@ -193,7 +207,7 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
           hit = j;
         }
       }
-    s_hit[tid] = hit;
+    s_hit[tid + jj * BS] = hit;
   }
   __syncthreads();
   int2 lis = make_int2(0, -1);
@@ -213,23 +227,33 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
       }
   }
   __syncthreads();
-  if (tid < N) hp = s_hpd[tid];
-  if (act && hp <= 0.0) act = false;  // deaths: body.active = False (combat.py:157-165)
-  const int n_alive0 = __syncthreads_count(act0);
-  const int n_att = __syncthreads_count(attacking);
-  const int n_died = __syncthreads_count(act0 && !act);
+  int n_alive0 = 0, n_att = 0, n_died = 0;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    if (i < N) hp[j] = s_hpd[i];
+    if (act[j] && hp[j] <= 0.0) act[j] = false;  // deaths: body.active = False (combat.py:157-165)
+    n_alive0 += __syncthreads_count(act0[j]);
+    n_att += __syncthreads_count(attacking[j]);
+    n_died += __syncthreads_count(act0[j] && !act[j]);
+  }
 
   // ---- commit the combat state (the spill step reads it back) ------------------------------------
-  if (tid < N) {
-    if (act0) {
-      B.angle[ag] = ang;
-      TB.cd_atk[ag] = cda;
-      TB.cd_mov[ag] = cdm;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * BS;
+    const size_t ag = (size_t)e * N + i;
+    if (i < N) {
+      if (act0[j]) {
+        B.angle[ag] = ang[j];
+        TB.cd_atk[ag] = cda[j];
+        TB.cd_mov[ag] = cdm[j];
+      }
+      TB.health[ag] = hp[j];
+      TB.alive[ag] = act[j] ? 1 : 0;
+      if (TB.health_out) TB.health_out[ag] = hp[j];
+      if (TB.alive_out) TB.alive_out[ag] = act[j] ? 1 : 0;
     }
-    TB.health[ag] = hp;
-    TB.alive[ag] = act ? 1 : 0;
-    if (TB.health_out) TB.health_out[ag] = hp;
-    if (TB.alive_out) TB.alive_out[ag] = act ? 1 : 0;
   }
   if (tid == 0) {
     TB.listener[e] = lis;
@@ -240,19 +264,22 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
   }
   __threadfence_block();
   // ---- Box2D step of the living bodies, TDM.get_obs, done / winner --------------------------------
-  spill::step_env<OT, true, kTdm>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out, lds, &TP, &TB,
-                                  make_float2(Fx, Fy), slot);
+  // (above 1024 agents the pair records live in the slot's HBM: 48 B per body would not fit beside
+  // the per-body arrays)
+  spill::step_env<OT, BPT == 1, kTdm, BPT>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out, lds, &TP,
+                                           &TB, F, slot);
 }
 
 // TDM world creation (combat.py:78-102) for N > 64: every body active with init_health, zero
 // cooldowns, the fresh listener, fat AABBs and the first FindNewContacts list (every overlapping
-// pair, a descending then b descending, as flock_init_wg), and the initial observation.
+// pair, a descending then b descending, as flock_init_wg), and the initial observation. The bodies in
+// a loop (any N, any block size).
 template <typename OT>
 __global__ __launch_bounds__(1024) void tdm_init_wg(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
                                                     int cur, OT* __restrict__ obs, const uint8_t* __restrict__ mask) {
   using namespace tdmwg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x, tid = threadIdx.x, N = P.n_agents, C = P.max_contacts;
+  const int e = blockIdx.x, tid = threadIdx.x, BS = blockDim.x, N = P.n_agents, C = P.max_contacts;
   if (mask && !mask[e]) return;  // reset_envs: only the masked envs
   const ObsLayout L = obs_layout(N);
   float2* s_c = (float2*)(lds + L.c);
@@ -260,14 +287,12 @@ __global__ __launch_bounds__(1024) void tdm_init_wg(StepParams P, WorldBuffers B
   uint32_t* s_aw = (uint32_t*)(lds + L.aw);
   float4* s_f = (float4*)(lds + L.fat);
   int* s_scan = (int*)(lds + L.scan);
-  const bool act = tid < N;
-  const size_t ag = (size_t)e * N + tid;
-  float4 f = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (act) {
+  for (int i = tid; i < N; i += BS) {
+    const size_t ag = (size_t)e * N + i;
     const float2 p = B.pos[ag];
     const float r = P.radius;
-    f = make_float4((p.x - r) - kAabbExtension, (p.y - r) - kAabbExtension, (p.x + r) + kAabbExtension,
-                    (p.y + r) + kAabbExtension);
+    const float4 f = make_float4((p.x - r) - kAabbExtension, (p.y - r) - kAabbExtension, (p.x + r) + kAabbExtension,
+                                 (p.y + r) + kAabbExtension);
     B.fat[ag] = f;
     B.vel[ag] = make_float2(0.0f, 0.0f);
     B.sleep[ag] = 0.0f;
@@ -277,31 +302,47 @@ __global__ __launch_bounds__(1024) void tdm_init_wg(StepParams P, WorldBuffers B
     TB.alive[ag] = 1;
     if (TB.health_out) TB.health_out[ag] = TP.init_health;
     if (TB.alive_out) TB.alive_out[ag] = 1;
-    s_c[tid] = p;
-    s_a[tid] = B.angle[ag];
-    s_f[tid] = f;
+    s_c[i] = p;
+    s_a[i] = B.angle[ag];
+    s_f[i] = f;
   }
-  ballot_bits(s_aw, N, act);
+  for (int q = tid; q < words(N); q += BS) s_aw[q] = q + 1 < words(N) || N % 32 == 0 ? ~0u : (1u << (N % 32)) - 1u;
   __syncthreads();
-  int cnt = 0;
-  if (act)
-    for (int j = tid + 1; j < N; ++j) cnt += spill::overlap(f, s_f[j]) ? 1 : 0;
-  int excl;
-  const int total = spill::block_scan_excl(cnt, excl, s_scan);
-  if (act && cnt > 0) {
-    int w = total - excl - cnt;  // agents > tid come first
-    for (int j = N - 1; j > tid; --j)
-      if (spill::overlap(f, s_f[j])) {
-        if (w < C) {
-          B.cab[cur][(size_t)e * C + w] = (uint32_t)tid | ((uint32_t)j << 16);
-          B.cimp[cur][(size_t)e * C + w] = make_float2(0.0f, 0.0f);
+  // pairs in (a desc, b desc) order: chunks of BS bodies in body order, the total first
+  int total = 0;
+  for (int i0 = 0; i0 < N; i0 += BS) {
+    const int i = i0 + tid;
+    int cnt = 0;
+    if (i < N)
+      for (int j = i + 1; j < N; ++j) cnt += spill::overlap(s_f[i], s_f[j]) ? 1 : 0;
+    int excl;
+    total += spill::block_scan_excl(cnt, excl, s_scan);
+  }
+  int base = 0;
+  for (int i0 = 0; i0 < N; i0 += BS) {
+    const int i = i0 + tid;
+    int cnt = 0;
+    if (i < N)
+      for (int j = i + 1; j < N; ++j) cnt += spill::overlap(s_f[i], s_f[j]) ? 1 : 0;
+    int excl;
+    const int tot = spill::block_scan_excl(cnt, excl, s_scan);
+    if (i < N && cnt > 0) {
+      int w = total - (base + excl) - cnt;  // agents > i come first
+      for (int j = N - 1; j > i; --j)
+        if (spill::overlap(s_f[i], s_f[j])) {
+          if (w < C) {
+            B.cab[cur][(size_t)e * C + w] = (uint32_t)i | ((uint32_t)j << 16);
+            B.cimp[cur][(size_t)e * C + w] = make_float2(0.0f, 0.0f);
+          }
+          ++w;
         }
-        ++w;
-      }
+    }
+    base += tot;
   }
   const size_t rows = (size_t)e * N * (N - 1);
-  tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, tid, s_aw, TP,
-                    s_c, s_a);
+  for (int i = tid; i - tid < N; i += BS)  // tdm_obs_block returns for i >= N
+    tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, i, s_aw, TP,
+                      s_c, s_a);
   if (tid == 0) {
     const int st = total > C ? MACM_ST_CONTACT_OVERFLOW : 0;
     B.ccount[cur][e] = total > C ? C : total;
@@ -316,33 +357,37 @@ __global__ __launch_bounds__(1024) void tdm_init_wg(StepParams P, WorldBuffers B
   }
 }
 
-// TDM.get_obs of the current state without stepping (N > 64).
+// TDM.get_obs of the current state without stepping (N > 64; the bodies in a loop).
 template <typename OT>
 __global__ __launch_bounds__(1024) void tdm_observe_wg(StepParams P, WorldBuffers B, TdmParams TP, TdmBuffers TB,
                                                        OT* __restrict__ obs) {
   using namespace tdmwg;
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x, tid = threadIdx.x, N = P.n_agents;
+  const int e = blockIdx.x, tid = threadIdx.x, BS = blockDim.x, N = P.n_agents;
   const ObsLayout L = obs_layout(N);
   float2* s_c = (float2*)(lds + L.c);
   float* s_a = (float*)(lds + L.a);
   uint32_t* s_aw = (uint32_t*)(lds + L.aw);
-  const size_t ag = (size_t)e * N + tid;
-  bool live = false;
-  if (tid < N) {
-    s_c[tid] = B.pos[ag];
-    s_a[tid] = B.angle[ag];
-    live = TB.alive[ag] != 0;
+  for (int i0 = 0, j = 0; i0 < N; i0 += BS, ++j) {
+    const int i = i0 + tid;
+    const size_t ag = (size_t)e * N + i;
+    bool live = false;
+    if (i < N) {
+      s_c[i] = B.pos[ag];
+      s_a[i] = B.angle[ag];
+      live = TB.alive[ag] != 0;
+    }
+    ballot_bits(s_aw, N, live, j);
   }
-  ballot_bits(s_aw, N, live);
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
-  tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, tid, s_aw, TP,
-                    s_c, s_a);
+  for (int i = tid; i - tid < N; i += BS)
+    tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, i, s_aw, TP,
+                      s_c, s_a);
 }
 
 // ---- host-side launchers (C++ linkage, used by macm_capi.hip) -------------------------------------
-static int tdm_wg_block(int N) { return ((N + 63) / 64) * 64; }
+static int tdm_wg_block(int N) { return N > 1024 ? 1024 : ((N + 63) / 64) * 64; }
 
 // as wg_configure: the kernels' dynamic-LDS limits only grow (per device)
 hipError_t tdm_wg_configure(int N) {
@@ -355,7 +400,9 @@ hipError_t tdm_wg_configure(int N) {
   if (N <= hw) return hipSuccess;
   hw = N;
   const int ls = tdm_wg_step_lds(N), lo = tdm_wg_obs_lds(N);
-  const void* fs[] = {(const void*)tdm_step_wg<float>, (const void*)tdm_step_wg<double>};
+  const void* fs[] = {(const void*)tdm_step_wg<float>, (const void*)tdm_step_wg<double>,
+                      (const void*)tdm_step_wg<float, 2>, (const void*)tdm_step_wg<double, 2>,
+                      (const void*)tdm_step_wg<float, 4>, (const void*)tdm_step_wg<double, 4>};
   const void* fo[] = {(const void*)tdm_init_wg<float>, (const void*)tdm_init_wg<double>,
                       (const void*)tdm_observe_wg<float>, (const void*)tdm_observe_wg<double>};
   hipError_t e = hipSuccess;
@@ -370,12 +417,17 @@ hipError_t launch_tdm_step_wg(const StepParams& P, const WorldBuffers& B, const 
                               int cur, const void* actions, void* obs, bool obs_f64, uint8_t* done, hipStream_t s) {
   const dim3 grid(P.n_envs), block(tdm_wg_block(P.n_agents));
   const int lds = tdm_wg_step_lds(P.n_agents);
-  if (obs_f64)
-    hipLaunchKernelGGL(tdm_step_wg<double>, grid, block, lds, s, P, B, TP, TB, cur, (const uchar4*)actions,
-                       (double*)obs, done);
-  else
-    hipLaunchKernelGGL(tdm_step_wg<float>, grid, block, lds, s, P, B, TP, TB, cur, (const uchar4*)actions,
-                       (float*)obs, done);
+  const int bpt = P.n_agents <= 1024 ? 1 : P.n_agents <= 2048 ? 2 : 4;
+  const uchar4* a = (const uchar4*)actions;
+  if (obs_f64) {
+    if (bpt == 1) hipLaunchKernelGGL((tdm_step_wg<double, 1>), grid, block, lds, s, P, B, TP, TB, cur, a, (double*)obs, done);
+    else if (bpt == 2) hipLaunchKernelGGL((tdm_step_wg<double, 2>), grid, block, lds, s, P, B, TP, TB, cur, a, (double*)obs, done);
+    else hipLaunchKernelGGL((tdm_step_wg<double, 4>), grid, block, lds, s, P, B, TP, TB, cur, a, (double*)obs, done);
+  } else {
+    if (bpt == 1) hipLaunchKernelGGL((tdm_step_wg<float, 1>), grid, block, lds, s, P, B, TP, TB, cur, a, (float*)obs, done);
+    else if (bpt == 2) hipLaunchKernelGGL((tdm_step_wg<float, 2>), grid, block, lds, s, P, B, TP, TB, cur, a, (float*)obs, done);
+    else hipLaunchKernelGGL((tdm_step_wg<float, 4>), grid, block, lds, s, P, B, TP, TB, cur, a, (float*)obs, done);
+  }
   return hipGetLastError();
 }
 

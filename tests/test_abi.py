@@ -61,12 +61,12 @@ def test_tdm_defaults_match_python_mirror():
     c = _abi.MacmTdmConfig()
     assert L.macm_tdm_config_default(ctypes.byref(c)) == 0
     assert bytes(c) == bytes(_abi.tdm_config_from_defaults())
-    c.team_size[0] = 513  # above the workgroup step's 1024 agents: refused before any HIP call
-    c.team_size[1] = 512
-    c.n_agents = 1025
+    c.team_size[0] = 2049  # above the workgroup step's 4096 agents: refused before any HIP call
+    c.team_size[1] = 2048
+    c.n_agents = 4097
     h = ctypes.c_void_p()
     assert L.macm_tdm_create(ctypes.byref(c), 4, 0, ctypes.byref(h)) == -4
-    c.n_agents = 1024
+    c.n_agents = 4096
     assert L.macm_tdm_create(ctypes.byref(c), 4, 0, ctypes.byref(h)) == -1
 
 
@@ -88,7 +88,7 @@ def test_invalid_config_is_rejected_with_message():
     h = ctypes.c_void_p()
     rc = L.macm_world_create(ctypes.byref(c), None, 4, 0, 0, ctypes.byref(h))
     assert rc == -1 and b"n_agents" in L.macm_last_error()
-    c.n_agents = 1025
+    c.n_agents = 4097  # above 4 bodies per thread of a 1024-thread workgroup (flock_big.hip)
     assert L.macm_world_create(ctypes.byref(c), None, 4, 0, 0, ctypes.byref(h)) == -4
 
 

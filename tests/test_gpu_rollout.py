@@ -290,3 +290,28 @@ def test_handoff_equals_plain_workgroup_step(monkeypatch, E, N, K, kw):
     pb, tb = b.reward_sums()
     np.testing.assert_array_equal(pa, pb)
     assert ta == tb and b.status() == 0
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (6, 1024, 6, {}),                                   # C5-shaped: every env takes the DFS kernel's walk
+    (12, 300, 8, {"start_spread": 8}),                  # dense and sparse envs mixed
+    (40, 100, 10, {"reward_mode": "linear"}),
+])
+@pytest.mark.parametrize("handoff", ["0", "1"])
+def test_fused_dfs_solve_equals_split(monkeypatch, E, N, K, kw, handoff):
+    """Kernel B with the dense envs' DFS in the same wave (MACM_FUSE_DFS=1, flock_solve_wg<true>) gives the
+    split kernels' results bit for bit, with and without the B -> C handoff."""
+    monkeypatch.setenv("MACM_HANDOFF", handoff)
+    monkeypatch.setenv("MACM_FUSE_DFS", "1")
+    b = FlockVec(E, n_agents=[N], seed=3 * E + N, device="cuda:0", **kw)
+    a = FlockVec(E, n_agents=[N], seed=3 * E + N, device="cuda:0", **kw)
+    acts = flock_actions(K, E, N, 13)
+    for k in range(K):
+        monkeypatch.setenv("MACM_FUSE_DFS", "0")
+        a.step(acts[k])
+        monkeypatch.setenv("MACM_FUSE_DFS", "1")
+        b.step(acts[k])
+    assert_same(a, b, "fused DFS + solve")
+    pa, _ = a.reward_sums()
+    pb, _ = b.reward_sums()
+    np.testing.assert_array_equal(pa, pb)
