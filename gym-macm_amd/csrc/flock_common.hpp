@@ -157,6 +157,18 @@ __device__ __forceinline__ void st_wt(uint8_t* p, uint8_t v) {
 __device__ __forceinline__ uint8_t ld_wt(const uint8_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void st_wt(uint16_t* p, uint16_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint16_t ld_wt(const uint16_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_wt(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Host side of a world's handoff (macm_capi.hip): kernel C's stream, the join event, the device
 // words of Handoff, the last step's tag and the b_started count the next step waits for.

@@ -267,10 +267,72 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
   write_obs_row(o, coord, obs_sqrt<OT>(best), t0, obs_sqrt<OT>(td2), t1);
 }
 
+// The same two functions on (x, y) pairs: v_pk_mul_f32 / v_pk_add_f32 are, lane by lane, the
+// scalar form's IEEE operations (no contraction: -ffp-contract=off), so results are bit-identical;
+// the dependent chain is ~1/3 shorter (tools/ubench_level.hip V6 vs V1: 287 vs 307 cycles per level
+// step for a wave alone on its SIMD, 293 vs 311 at two waves per SIMD, 389 vs 381 at four).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void warm_start_contact_pk(pf2& vA, pf2& vB, float nx, float ny, float ln, float ltg,
+                                                      float mA, float mB) {
+  const pf2 n = {nx, ny}, t = {ny, -nx};
+  const pf2 P = ln * n + ltg * t;
+  vA = vA - mA * P;
+  vB = vB + mB * P;
+}
+
+__device__ __forceinline__ void solve_velocity_contact_pk(pf2& vA, pf2& vB, float nx, float ny, float& ln,
+                                                          float& ltg, float mA, float mB, float kmass,
+                                                          float friction) {
+  const pf2 n = {nx, ny}, t = {ny, -nx};
+  {  // tangent first
+    const pf2 pr = (vB - vA) * t;
+    const float vt = pr.x + pr.y;
+    float lambda = kmass * (-vt);
+    const float maxf = friction * ln;
+    const float ni = sclamp(ltg + lambda, -maxf, maxf);
+    lambda = ni - ltg;
+    ltg = ni;
+    const pf2 P = lambda * t;
+    vA = vA - mA * P;
+    vB = vB + mB * P;
+  }
+  {  // normal
+    const pf2 pr = (vB - vA) * n;
+    const float vn = pr.x + pr.y;
+    float lambda = -kmass * (vn - 0.0f);
+    const float ni = smax(ln + lambda, 0.0f);
+    lambda = ni - ln;
+    ln = ni;
+    const pf2 P = lambda * n;
+    vA = vA - mA * P;
+    vB = vB + mB * P;
+  }
+}
+
+// The chains outside the wide levels (one-slot levels, per-island lanes, single contacts) on packed
+// pairs too: A/B knob (round 5)
+#ifdef MACM_PACKED_CHAINS
+constexpr bool kPackedChains = true;
+#else
+constexpr bool kPackedChains = false;
+#endif
+#ifdef MACM_PACKED_LEVELS  // A/B knob: the one-slot level steps (T <= 64) on packed pairs
+constexpr bool kPackedLevels = true;
+#else
+constexpr bool kPackedLevels = false;
+#endif
+
 // b2ContactSolver, one circle contact (fixedRotation: no angular terms). Shared by
 // the LDS path and the single-contact register path, so both round identically.
 __device__ __forceinline__ void warm_start_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
                                                    float ny, float ln, float ltg, float mA, float mB) {
+  if constexpr (kPackedChains) {
+    pf2 a = {vAx, vAy}, b = {vBx, vBy};
+    warm_start_contact_pk(a, b, nx, ny, ln, ltg, mA, mB);
+    vAx = a.x; vAy = a.y; vBx = b.x; vBy = b.y;
+    return;
+  }
   const float tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
   const float Px = ln * nx + ltg * tx, Py = ln * ny + ltg * ty;
   vAx = vAx - mA * Px;
@@ -282,6 +344,12 @@ __device__ __forceinline__ void warm_start_contact(float& vAx, float& vAy, float
 __device__ __forceinline__ void solve_velocity_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
                                                        float ny, float& ln, float& ltg, float mA, float mB,
                                                        float kmass, float friction) {
+  if constexpr (kPackedChains) {
+    pf2 a = {vAx, vAy}, b = {vBx, vBy};
+    solve_velocity_contact_pk(a, b, nx, ny, ln, ltg, mA, mB, kmass, friction);
+    vAx = a.x; vAy = a.y; vBx = b.x; vBy = b.y;
+    return;
+  }
   const float tx = ny, ty = -nx;
   {  // tangent first
     const float dvx = vBx - vAx, dvy = vBy - vAy;
@@ -312,9 +380,31 @@ __device__ __forceinline__ void solve_velocity_contact(float& vAx, float& vAy, f
   }
 }
 
+__device__ __forceinline__ float solve_position_contact_pk(pf2& cA, pf2& cB, float radius, float mA, float mB) {
+  const pf2 d = cB - cA;
+  const pf2 d2 = d * d;
+  const float len = sqrt_rn(d2.x + d2.y);
+  const pf2 n = len < kEps ? d : d * rcp_rn(len);  // b2Vec2::Normalize
+  const pf2 pr = d * n;
+  const float sep = (pr.x + pr.y) - radius - radius;
+  const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+  const float K = mA + mB;
+  const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
+  const pf2 P = imp * n;
+  cA = cA - mA * P;
+  cB = cB + mB * P;
+  return sep;
+}
+
 // b2PositionSolverManifold + one SolvePositionConstraints contact; returns sep.
 __device__ __forceinline__ float solve_position_contact(float& cAx, float& cAy, float& cBx, float& cBy,
                                                         float radius, float mA, float mB) {
+  if constexpr (kPackedChains) {
+    pf2 a = {cAx, cAy}, b = {cBx, cBy};
+    const float sep = solve_position_contact_pk(a, b, radius, mA, mB);
+    cAx = a.x; cAy = a.y; cBx = b.x; cBy = b.y;
+    return sep;
+  }
   float nx = cBx - cAx, ny = cBy - cAy;
   normalize(nx, ny);
   const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - radius - radius;
@@ -377,6 +467,11 @@ constexpr bool kWidePriority = false;
 constexpr bool kWideLevelOrder = false;
 #else
 constexpr bool kWideLevelOrder = true;
+#endif
+#ifdef MACM_WIDE_SCALAR  // A/B knob: the wide levels' updates on scalar components (round 4)
+constexpr bool kWidePacked = false;
+#else
+constexpr bool kWidePacked = true;  // round 5: M closed loop -2.6%, metric window -0.5% (r05/abtests/wide_packed/)
 #endif
 
 // S slots per lane; REG: each slot's normal and impulses in registers (S = 2, T <= 128), else read
@@ -556,8 +651,36 @@ struct WideLevels {
           if (kWideRangeSkip && (l < lo[q] || l > hi[q])) continue;  // uniform: no lane of slot q at level l
           if (lvl(lvis[q]) == l) {  // exec-masked; a slot with no contact of this level is skipped
             if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));  // LDS addresses not hoisted (VGPRs)
-            float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
             float cx, cy, nl, nt;
+            if constexpr (kWidePacked) {
+              pf2* const pA = reinterpret_cast<pf2*>(s_v + ia(pw[q]));
+              pf2* const pB = reinterpret_cast<pf2*>(s_v + ib(pw[q]));
+              pf2 vA = *pA, vB = *pB;
+              if constexpr (REG) {
+                cx = nx[q];
+                cy = ny[q];
+                nl = ln[q];
+                nt = lt[q];
+              } else {
+                cx = s_tnx[it(pw[q])];
+                cy = s_tny[it(pw[q])];
+                nl = s_tln[it(pw[q])];
+                nt = s_tlt[it(pw[q])];
+              }
+              if constexpr (decltype(warm)::value) warm_start_contact_pk(vA, vB, cx, cy, nl, nt, mA, mB);
+              else solve_velocity_contact_pk(vA, vB, cx, cy, nl, nt, mA, mB, kmass, friction);
+              *pA = vA;
+              *pB = vB;
+              if constexpr (REG) {
+                ln[q] = nl;
+                lt[q] = nt;
+              } else {
+                s_tln[it(pw[q])] = nl;
+                s_tlt[it(pw[q])] = nt;
+              }
+              continue;
+            }
+            float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
             if constexpr (REG) {
               cx = nx[q];
               cy = ny[q];
@@ -619,10 +742,20 @@ struct WideLevels {
           if (kWideRangeSkip && (l < lo[q] || l > hi[q])) continue;  // uniform (slot ranges, below)
           if (lvl(lvis[q]) == l) {
             if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));
-            float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
-            const float sep = solve_position_contact(cA.x, cA.y, cB.x, cB.y, P.radius, mA, mB);
-            s_c[ia(pw[q])] = cA;
-            s_c[ib(pw[q])] = cB;
+            float sep;
+            if constexpr (kWidePacked) {
+              pf2* const pA = reinterpret_cast<pf2*>(s_c + ia(pw[q]));
+              pf2* const pB = reinterpret_cast<pf2*>(s_c + ib(pw[q]));
+              pf2 cA = *pA, cB = *pB;
+              sep = solve_position_contact_pk(cA, cB, P.radius, mA, mB);
+              *pA = cA;
+              *pB = cB;
+            } else {
+              float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
+              sep = solve_position_contact(cA.x, cA.y, cB.x, cB.y, P.radius, mA, mB);
+              s_c[ia(pw[q])] = cA;
+              s_c[ib(pw[q])] = cB;
+            }
             // order-preserving int of the float for atomicMin
             const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
             atomicMin(&s_pmin[isl(lvis[q])], key);
@@ -1540,11 +1673,26 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         float2* pa = mylvl == 0 ? pda : pdd;
         float2* pb = mylvl == 0 ? pdb : pdd;
         auto step = [&](bool onc, bool onn) {
+          float nl = lln, nt = llt;
+          if constexpr (kPackedLevels) {
+            pf2 vA = *reinterpret_cast<pf2*>(pa), vB = *reinterpret_cast<pf2*>(pb);
+            float2* const na = onn ? pda : pdd;
+            float2* const nb = onn ? pdb : pdd;
+            if constexpr (decltype(warm)::value) warm_start_contact_pk(vA, vB, lnx, lny, nl, nt, mA, mB);
+            else solve_velocity_contact_pk(vA, vB, lnx, lny, nl, nt, mA, mB, kmass, friction);
+            *reinterpret_cast<pf2*>(pa) = vA;
+            *reinterpret_cast<pf2*>(pb) = vB;
+            lln = onc ? nl : lln;
+            llt = onc ? nt : llt;
+            pa = na;
+            pb = nb;
+            level_sync();
+            return;
+          }
           const float2 vA0 = *pa, vB0 = *pb;
           float2* const na = onn ? pda : pdd;
           float2* const nb = onn ? pdb : pdd;
           float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-          float nl = lln, nt = llt;
           if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB);
           else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB, kmass, friction);
           *pa = make_float2(vAx, vAy);
@@ -1752,14 +1900,22 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           float2* pb = mylvl == 0 ? pdb : pdd;
           int* pm = mylvl == 0 ? pmi : pmd;
           auto pstep = [&](bool onn) {
-            const float2 cA0 = *pa, cB0 = *pb;
+            float sep;
             float2* const na = onn ? pda : pdd;
             float2* const nb = onn ? pdb : pdd;
             int* const nm = onn ? pmi : pmd;
-            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-            *pa = make_float2(cAx, cAy);
-            *pb = make_float2(cBx, cBy);
+            if constexpr (kPackedLevels) {
+              pf2 cA = *reinterpret_cast<pf2*>(pa), cB = *reinterpret_cast<pf2*>(pb);
+              sep = solve_position_contact_pk(cA, cB, P.radius, mA, mB);
+              *reinterpret_cast<pf2*>(pa) = cA;
+              *reinterpret_cast<pf2*>(pb) = cB;
+            } else {
+              const float2 cA0 = *pa, cB0 = *pb;
+              float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+              sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+              *pa = make_float2(cAx, cAy);
+              *pb = make_float2(cBx, cBy);
+            }
             // order-preserving int of the float for atomicMin
             const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
             atomicMin(pm, key);

@@ -1207,7 +1207,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
       s_ic[nisl] = (uint16_t)nord;
-      xib[nisl] = (uint16_t)nb;
+      st_wt(xib + nisl, (uint16_t)nb);  // kernel C's (write-through: a fused B hands it over, see solve_wg)
     }
     // the body to pop next with its CSR range and level: the seed (never touched yet: level 0), then
     // the last push of the previous pop (in registers; its stack slot is dropped), else the stack's
@@ -1230,7 +1230,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
         xcur = s_last[bdy] & kLvl;
       }
       top_b = -1;
-      if (lane == 0) xibod[nb] = (uint16_t)bdy;
+      if (lane == 0) st_wt(xibod + nb, (uint16_t)bdy);
       ++nb;
       // levels of the new contacts c_1..c_m of bdy in order: X_i = i + max(X_0, max_{j<=i}(y_j - j + 1))
       // (see par_walk in kernel A). Branch-free up to the stores: lanes past the body's last edge
@@ -1273,7 +1273,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
   }
   if (lane == 0) {
     s_ic[nisl] = (uint16_t)nord;
-    xib[nisl] = (uint16_t)nb;
+    st_wt(xib + nisl, (uint16_t)nb);
   }
   if (kDfsPriority) __builtin_amdgcn_s_setprio(0);
   // this wave's x_dfs stores are read back below (workgroup scope: this CU, this XCD's L2)
@@ -1365,7 +1365,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
   for (int q = lane; q <= nisl; q += W) B.x_ic[(size_t)e * IS + q] = s_ic[q];
   if (lane == 0) {
     B.x_nlvl[e] = dmax;
-    B.x_nisl[e] = nisl;
+    st_wt(B.x_nisl + e, nisl);
   }
   WSTAMP(28);
 }
@@ -1700,6 +1700,9 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   const HandoffPublish publish(H, e);  // to kernel C when this body ends (any return)
   if constexpr (FUSED) {
     dfs_env(P, B, tcap, e, lds);
+    // the walk's records, counts and island ranges reach the solve through this wave's own global
+    // stores (this CU's L1, this XCD's L2); kernel C, which may run on another XCD beside this kernel
+    // (the handoff), reads the island outputs it needs write-through (dfs_env stores them so)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __syncthreads();
   }
@@ -1736,7 +1739,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   uint16_t* s_bjv = (uint16_t*)(lds + L.bjv);
   const float2* g_lam = B.scratch + (size_t)e * tcap;
   const int IS = wg_isl_stride(N);
-  const int nisl = B.x_nisl[e];
+  // With the handoff, a fused kernel B may have walked this env's islands (flock_solve_wg<true>) on
+  // another XCD while this kernel runs: its island outputs are read write-through, as B's solve outputs
+  const bool hwt = H.q != nullptr;
+  const int nisl = hwt ? ld_wt(B.x_nisl + e) : B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
   WSTAMP(0);
 
@@ -1786,7 +1792,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const uint8_t* isolv = B.x_isolv + (size_t)e * IS;
     uint16_t* s_ib = (uint16_t*)(lds + L.gent);     // [nisl + 1] <= N / 2 + 2 (gent: 16 N bytes)
     uint32_t* s_mn = (uint32_t*)(lds + L.gstart);   // [nisl] <= N / 2 (gstart: >= 8 N bytes)
-    for (int I = tid; I <= nisl; I += BS) s_ib[I] = ib[I];
+    for (int I = tid; I <= nisl; I += BS) s_ib[I] = hwt ? ld_wt(ib + I) : ib[I];
     for (int I = tid; I < nisl; I += BS) s_mn[I] = 0x7f7fffffu;  // FLT_MAX, as the serial minimum starts
     __syncthreads();
     const int nb = nisl > 0 ? s_ib[nisl] : 0;
@@ -1796,7 +1802,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int mid = (lo + hi + 1) >> 1;
         if (s_ib[mid] <= k) lo = mid; else hi = mid - 1;
       }
-      atomicMin(&s_mn[lo], __float_as_uint(s_slp[ibod[k]]));
+      atomicMin(&s_mn[lo], __float_as_uint(s_slp[hwt ? ld_wt(ibod + k) : ibod[k]]));
     }
     __syncthreads();
     for (int k = tid; k < nb; k += BS) {
@@ -1805,7 +1811,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int mid = (lo + hi + 1) >> 1;
         if (s_ib[mid] <= k) lo = mid; else hi = mid - 1;
       }
-      s_flag[ibod[k]] = (__uint_as_float(s_mn[lo]) >= kTimeToSleep && ld_wt(isolv + lo)) ? 1 : 0;
+      s_flag[hwt ? ld_wt(ibod + k) : ibod[k]] = (__uint_as_float(s_mn[lo]) >= kTimeToSleep && ld_wt(isolv + lo)) ? 1 : 0;
     }
   }
   __syncthreads();

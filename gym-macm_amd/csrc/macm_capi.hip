@@ -647,7 +647,7 @@ static int overflow_error(uint32_t st) {
 // use it: the workgroup path, when kHandoffDefault or MACM_HANDOFF=1 (A/B; MACM_HANDOFF=0 off). Env
 // slices (rollout_wg_slices) run without it. NULL: kernel C launched after B on the same stream.
 #ifndef MACM_HANDOFF_DEFAULT
-#define MACM_HANDOFF_DEFAULT 0
+#define MACM_HANDOFF_DEFAULT 1  // round 5: C5 window 5.35 -> 4.99 ms (profiles/r05/abtests/handoff_fused/)
 #endif
 static constexpr bool kHandoffDefault = MACM_HANDOFF_DEFAULT != 0;
 static HandoffStream* handoff_for(macm_world* w) {

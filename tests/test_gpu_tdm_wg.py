@@ -51,8 +51,9 @@ def test_tdm_wg_large_teams():
 
 
 def test_tdm_wg_cap_and_refusal():
+    # up to 4096 agents since round 5 (tests/test_gpu_big.py); one more is refused
     with pytest.raises(_abi.MacmError):
-        TdmWorld(tdm_config([513, 512]), 1, device="cuda:0")
+        TdmWorld(tdm_config([2049, 2048]), 1, device="cuda:0")
 
 
 @pytest.mark.parametrize("bots", [False, True])
