@@ -1709,6 +1709,256 @@ __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers 
   solve_env(P, B, tcap, e, lds);
 }
 
+// ---- kernel B with two envs per wave (round 5) -----------------------------------------------------
+// A level step issues the same ~45 VALU however few of its lanes are on the level, and with four
+// waves per SIMD (C3: 4096 envs) the level steps of the SIMD's waves queue for its issue slots
+// (tools/ubench_level.hip: 387 cycles per level step at four waves per SIMD, 288 at two, 278 alone).
+// Here each half of the wave (32 lanes) solves an env of its own, each half on its own levels: the
+// same instructions step two envs, and the launch has half the waves. Envs b and b + 1 of the env
+// order (similar list sizes, so similar depths) share a wave. Each env's arithmetic, its order of
+// updates and its LDS bodies are exactly those of solve_env; only the chunks are 32 records.
+constexpr int kPairLanes = 32;  // lanes per env (half a wave)
+__host__ __device__ inline int wg_solve_lds_env(int N) { return (wg_solve_lds(N) + 15) & ~15; }
+
+__device__ __forceinline__ void solve_env_pair(const StepParams& P, const WorldBuffers& B, int tcap,
+                                               int ev0, int ev1, unsigned char* lds) {
+  using namespace wg;
+  constexpr int GW = kPairLanes;
+  const int lane = threadIdx.x, N = P.n_agents;
+  const int h = lane / GW, hl = lane % GW;  // this lane's half (env) and its lane in the half
+  const int IS = wg_isl_stride(N);
+  // per env (wave-uniform): island count (< 0: no solve: the spill step's, or no env), contacts
+  const int nisl0 = ev0 >= 0 ? B.x_nisl[ev0] : -1, nisl1 = ev1 >= 0 ? B.x_nisl[ev1] : -1;
+  const int nc0 = nisl0 > 0 ? (int)B.x_ic[(size_t)ev0 * IS + nisl0] : 0;
+  const int nc1 = nisl1 > 0 ? (int)B.x_ic[(size_t)ev1 * IS + nisl1] : 0;
+  if (nisl0 < 0 && nisl1 < 0) return;
+  if (kSolvePriority) {
+    int nlvl = 0;
+    if (nisl0 >= 0) nlvl = B.x_nlvl[ev0];
+    if (nisl1 >= 0) nlvl = max(nlvl, B.x_nlvl[ev1]);
+    if (nlvl >= 128) __builtin_amdgcn_s_setprio(3);
+    else if (nlvl >= 64) __builtin_amdgcn_s_setprio(2);
+    else if (nlvl >= 32) __builtin_amdgcn_s_setprio(1);
+  }
+  const int nch0 = (nc0 + GW - 1) / GW, nch1 = (nc1 + GW - 1) / GW;
+  const int nchw = max(nch0, nch1);
+  // this lane's env
+  const int nisl_h = h ? nisl1 : nisl0;
+  const bool hv = nisl_h >= 0;
+  const int e = hv ? (h ? ev1 : ev0) : (nisl0 >= 0 ? ev0 : ev1);  // an inactive half reads a live env's rows
+  const int nisl = hv ? nisl_h : 0, nc = hv ? (h ? nc1 : nc0) : 0;
+  unsigned char* base = lds + h * wg_solve_lds_env(N);
+  float2* s_v = (float2*)base;
+  float2* s_c = s_v + N;
+  float* s_mins = (float*)(s_c + N);
+  uint8_t* s_done = (uint8_t*)s_mins + wg_solve_mins_bytes(N);
+  float2* s_dum = (float2*)s_mins;
+  const size_t en = (size_t)e * N;
+  const float4* cst = B.x_cst + (size_t)e * tcap;
+  float2* cimp = B.x_cimp + (size_t)e * tcap;
+  const uint16_t* xord = B.x_ord + (size_t)e * tcap;
+  float2* g_lam = B.scratch + (size_t)e * tcap;
+  if (hv)
+    for (int i = hl; i < N; i += GW) {
+      s_c[i] = B.pos[en + i];
+      s_v[i] = B.x_vmid[en + i];
+    }
+  for (int I = hl; I < nisl; I += GW) s_done[I] = 0;
+  __syncthreads();
+  const float mA = P.inv_mass, mB = P.inv_mass;
+  const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
+  const float friction = P.friction;
+  auto level_sync = [&]() { wave_lds_sync(); };
+  auto wait_vm = [&]() { __builtin_amdgcn_s_waitcnt(0x0f70); };  // vmcnt(0)
+  struct Slot {
+    float4 r;
+    float2 m;
+    int o;
+  };
+  auto load = [&](int c, Slot& x) {
+    const int k = max(0, min(c * GW + hl, nc - 1));
+    x.r = cst[k];
+    x.m = cimp[k];
+    x.o = xord[k];
+  };
+  // a lane's level relative to its half's first level in the chunk (0x7fff: no record), and the
+  // chunk's number of level steps: the larger of the two halves' level spans
+  auto chunk_levels = [&](int c, const Slot& x, int& rel, int& nsteps) {
+    const bool valid = c * GW + hl < nc;
+    const int mylv = valid ? __float_as_int(x.r.w) >> 16 : 0x7fff;
+    const int cnt0 = min(GW, nc0 - c * GW), cnt1 = min(GW, nc1 - c * GW);  // this chunk's records per env
+    const int lv00 = __builtin_amdgcn_readlane(mylv, 0), lv01 = __builtin_amdgcn_readlane(mylv, GW);
+    const int lv10 = __builtin_amdgcn_readlane(mylv, max(cnt0, 1) - 1);
+    const int lv11 = __builtin_amdgcn_readlane(mylv, GW + max(cnt1, 1) - 1);
+    const int span0 = (nisl0 >= 0 && cnt0 > 0) ? lv10 - lv00 + 1 : 0;
+    const int span1 = (nisl1 >= 0 && cnt1 > 0) ? lv11 - lv01 + 1 : 0;
+    rel = valid ? mylv - (h ? lv01 : lv00) : 0x7fff;
+    nsteps = max(span0, span1);
+  };
+  // level steps 0..nsteps-1 of a chunk (uniform), lane on at step rel; two steps per iteration
+  auto level_loop = [&](int nsteps, int rel, auto&& step) {
+    bool on = rel == 0;
+    int i = 0;
+    for (; i + 1 < nsteps; i += 2) {
+      step(on, rel == i + 1);
+      level_sync();
+      step(rel == i + 1, rel == i + 2);
+      level_sync();
+      on = rel == i + 2;
+    }
+    if (i + 1 == nsteps) {
+      step(on, false);
+      level_sync();
+    }
+  };
+  auto vel_pass = [&](auto warm_c, bool last) {
+    constexpr bool warm = decltype(warm_c)::value;
+    if (nchw == 0) return;
+    Slot cur, nxt;
+    load(0, cur);
+    wait_vm();
+    for (int c = 0; c < nchw; ++c) {
+      load(c + 1, nxt);
+      int rel, nsteps;
+      chunk_levels(c, cur, rel, nsteps);
+      const uint32_t ab = __float_as_uint(cur.r.x);
+      const int a = ab & 0xffffu, b = ab >> 16;
+      float2 im = cur.m;
+      float2* const pa0 = s_v + a;
+      float2* const pb0 = s_v + b;
+      float2* const pd = s_dum + (kSharedDummy ? 0 : hl);
+      float2* pa = rel == 0 ? pa0 : pd;
+      float2* pb = rel == 0 ? pb0 : pd;
+      level_loop(nsteps, rel, [&](bool onc, bool onn) {
+        float2 va = *pa, vb = *pb;
+        float2* const na = onn ? pa0 : pd;
+        float2* const nb = onn ? pb0 : pd;
+        float lx = im.x, ly = im.y;
+        if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB);
+        else gs_velocity(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB, kmass, friction);
+        *pa = va;
+        *pb = vb;
+        im.x = onc ? lx : im.x;
+        im.y = onc ? ly : im.y;
+        pa = na;
+        pb = nb;
+      });
+      const int k = c * GW + hl;
+      if (!warm && k < nc) {
+        if (last) st_wt(g_lam + cur.o, im);
+        else cimp[k] = im;
+      }
+      wait_vm();
+      cur = nxt;
+    }
+  };
+  if (P.warm_starting) vel_pass(std::true_type{}, false);
+  for (int it = 0; it < P.vel_iters; ++it) vel_pass(std::false_type{}, it + 1 == P.vel_iters);
+  if (P.vel_iters == 0)
+    for (int k = hl; k < nc; k += GW) st_wt(g_lam + xord[k], cimp[k]);
+
+  if (hv)
+    for (int i = hl; i < N; i += GW) {
+      const float2 vv = s_v[i];
+      float vx = vv.x, vy = vv.y;
+      const float tx = P.dt * vx, ty = P.dt * vy;
+      if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
+        const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
+        vx = vx * ratio;
+        vy = vy * ratio;
+      }
+      const float2 c = s_c[i];
+      s_c[i] = make_float2(c.x + P.dt * vx, c.y + P.dt * vy);
+      st_wt(B.x_vout + en + i, make_float2(vx, vy));
+    }
+  __syncthreads();
+
+  auto pos_passes = [&](auto kpos_c) {
+    constexpr bool kpos = decltype(kpos_c)::value;
+    for (int it = 0; it < P.pos_iters; ++it) {
+      for (int I = hl; I < nisl; I += GW) s_mins[I] = 0.0f;
+      __syncthreads();
+      Slot cur, nxt;
+      if (nchw > 0) load(0, cur);
+      wait_vm();
+      for (int c = 0; c < nchw; ++c) {
+        load(c + 1, nxt);
+        int rel, nsteps;
+        chunk_levels(c, cur, rel, nsteps);
+        const int I = __float_as_int(cur.r.w) & 0xffff;
+        const uint32_t ab = __float_as_uint(cur.r.x);
+        const int a = ab & 0xffffu, b = ab >> 16;
+        const bool live = hv && nc > 0 && !s_done[min(I, max(nisl - 1, 0))];
+        float2* const pdd = s_v + (kSharedDummy ? 0 : hl);
+        float* const pmd = reinterpret_cast<float*>(s_v + (kSharedDummy ? 1 + hl : hl));
+        const int relp = live ? rel : 0x7fff;
+        float2* const pca = s_c + a;
+        float2* const pcb = s_c + b;
+        float* const pmi = s_mins + I;
+        float2* pa = relp == 0 ? pca : pdd;
+        float2* pb = relp == 0 ? pcb : pdd;
+        float* pm = relp == 0 ? pmi : pmd;
+        level_loop(nsteps, relp, [&](bool, bool onn) {
+          float2 ca = *pa, cb = *pb;
+          float2* const na = onn ? pca : pdd;
+          float2* const nb = onn ? pcb : pdd;
+          float* const nm = onn ? pmi : pmd;
+          const float sep = gs_position<kpos>(ca, cb, P.radius, mA, mB);
+          *pa = ca;
+          *pb = cb;
+          __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          pa = na;
+          pb = nb;
+          pm = nm;
+        });
+        wait_vm();
+        cur = nxt;
+      }
+      __syncthreads();
+      bool open = false;
+      for (int I = hl; I < nisl; I += GW) {
+        if (s_done[I]) continue;
+        if (s_mins[I] >= -3.0f * kLinearSlop) s_done[I] = 1;
+        else open = true;
+      }
+      const bool any_open = __ballot(open) != 0ull;
+      __syncthreads();
+      if (!any_open) break;
+    }
+  };
+  if (mA + mB > 0.0f) pos_passes(std::true_type{});
+  else pos_passes(std::false_type{});
+  if (!hv) return;
+  uint8_t* isolv = B.x_isolv + (size_t)e * IS;
+  for (int I = hl; I < nisl; I += GW) st_wt(isolv + I, s_done[I]);
+  for (int i = hl; i < N; i += GW) st_wt(B.x_cout + en + i, s_c[i]);
+}
+
+// Kernel B, two envs per wave: envs order[2 b], order[2 b + 1] (one when E is odd). With the handoff,
+// the wave counts both envs as started and publishes both when it ends.
+__global__ __launch_bounds__(64) void flock_solve_wg_pair(StepParams P, WorldBuffers B, int tcap, Handoff H) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int b0 = 2 * (int)blockIdx.x, b1 = b0 + 1;
+  const bool ord = kWgEnvOrder && B.sched;
+  const int ev0 = ord ? (int)B.sched[b0] : b0;
+  const int ev1 = b1 < P.n_envs ? (ord ? (int)B.sched[b1] : b1) : -1;
+  const int nv = ev1 >= 0 ? 2 : 1;
+  if (H.q && threadIdx.x == 0)
+    __hip_atomic_fetch_add(H.b_started, (unsigned long long)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  solve_env_pair(P, B, tcap, ev0, ev1, lds);
+  if (H.q) {
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0) {
+      const unsigned slot = __hip_atomic_fetch_add(&H.ctr[0], (unsigned)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&H.q[slot], ((unsigned long long)H.tag << 32) | (unsigned)ev0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (nv == 2)
+        __hip_atomic_store(&H.q[slot + 1], ((unsigned long long)H.tag << 32) | (unsigned)ev1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <typename OT>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void flock_step_wg_c(StepParams P, WorldBuffers B, int cur, int tcap,
                                                         OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
@@ -2254,6 +2504,18 @@ static bool fuse_dfs() {
   return wg::kDfsKernel && (x ? atoi(x) : MACM_FUSE_DFS_DEFAULT) != 0;
 }
 
+// Kernel B with two envs per wave (flock_solve_wg_pair) where waves would otherwise queue for their
+// SIMDs' issue: many envs of up to kPairMaxAgents agents. MACM_SOLVE_PAIR=0/1 overrides (A/B sessions).
+#ifndef MACM_SOLVE_PAIR_DEFAULT
+#define MACM_SOLVE_PAIR_DEFAULT 0
+#endif
+constexpr int kPairMaxAgents = 512, kPairMinEnvs = 1024;
+static bool solve_pairs(const StepParams& P) {
+  const char* x = getenv("MACM_SOLVE_PAIR");
+  const bool on = x ? atoi(x) != 0 : MACM_SOLVE_PAIR_DEFAULT != 0;
+  return on && P.n_agents <= kPairMaxAgents && P.n_envs >= kPairMinEnvs;
+}
+
 hipError_t wg_configure(int N, int tcap) {
   static std::mutex mu;
   static std::map<int, int> high;  // device -> the largest N configured
@@ -2277,6 +2539,9 @@ hipError_t wg_configure(int N, int tcap) {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)flock_dfs_wg, hipFuncAttributeMaxDynamicSharedMemorySize,
                             wg::wg_layout_d(N, tcap).total);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)flock_solve_wg_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * wg_solve_lds_env(N));
   return e;
 }
 
@@ -2318,7 +2583,11 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
     hipLaunchKernelGGL(flock_solve_wg<true>, grid, dim3(64), wg_fused_lds(N, tcap), s, P, B, tcap, H);
   } else {
     if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
-    hipLaunchKernelGGL(flock_solve_wg<false>, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
+    if (solve_pairs(P))
+      hipLaunchKernelGGL(flock_solve_wg_pair, dim3((P.n_envs + 1) / 2), dim3(64), 2 * wg_solve_lds_env(N), s, P, B,
+                         tcap, H);
+    else
+      hipLaunchKernelGGL(flock_solve_wg<false>, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
   }
   if (!H.q) {
     launch_c(s);

@@ -749,7 +749,13 @@ static macm_outputs step_outputs(const macm_world* w, const macm_outputs* out, i
 #ifndef MACM_SLICE_MAX_AGENTS  // A/B knob
 #define MACM_SLICE_MAX_AGENTS 512
 #endif
-static constexpr int kSlices = 2, kSliceMinEnvs = 1024, kSliceMaxAgents = MACM_SLICE_MAX_AGENTS;
+static constexpr int kSlices = 3, kSliceMinEnvs = 1024, kSliceMaxAgents = MACM_SLICE_MAX_AGENTS;
+// MACM_WG_SLICES=n: n env slices (0: none, the handoff instead; A/B sessions), kSlices by default
+static int n_slices() {
+  const char* v = getenv("MACM_WG_SLICES");
+  const int n = v ? atoi(v) : kSlices;
+  return n < 0 ? 0 : n > 8 ? 8 : n;
+}
 // astride == 0: the closed loop (macm_world_rollout_bots): every step of a slice reads the bot's
 // action rows of its envs and the bots kernel writes the next ones from the slice's obs rows
 // (trajectory form: step k reads action row k and writes row k + 1 of [K + 1, E, N, 3]).
@@ -851,8 +857,8 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
     return MACM_OK;
   }
   const unsigned char* act = static_cast<const unsigned char*>(actions);
-  if (!w->big && w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents)
-    return rollout_wg_slices(w, kSlices, act, n_steps, astride, out, traj, s);
+  if (!w->big && w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents && n_slices() >= 2)
+    return rollout_wg_slices(w, n_slices(), act, n_steps, astride, out, traj, s);
   // workgroup path: its three launches per step (and the bot's), in order
   const long long rows = (long long)w->P.n_envs * w->P.n_agents;
   const unsigned long long kstride = bots ? (traj ? (unsigned long long)rows * 3 : 0ull) : astride;

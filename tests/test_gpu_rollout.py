@@ -315,3 +315,45 @@ def test_fused_dfs_solve_equals_split(monkeypatch, E, N, K, kw, handoff):
     pa, _ = a.reward_sums()
     pb, _ = b.reward_sums()
     np.testing.assert_array_equal(pa, pb)
+
+
+@pytest.mark.parametrize("E,N,K,kw", [
+    (1031, 100, 6, {}),                                  # odd env count: the last wave holds one env
+    (1024, 256, 8, {"targets": [i * 4 // 256 for i in range(256)]}),   # C3-shaped
+    (1026, 300, 4, {"start_spread": 8}),                 # dense and sparse envs, the spill step beside
+    (1024, 120, 6, {"reward_mode": "linear", "obs_dtype": torch.float64}),
+])
+@pytest.mark.parametrize("handoff", ["0", "1"])
+def test_solve_pairs_equal_single(monkeypatch, E, N, K, kw, handoff):
+    """Kernel B with two envs per wave (MACM_SOLVE_PAIR=1, flock_solve_wg_pair) gives the one-env-per-wave
+    kernel's results bit for bit: state, lists, outputs, counters and reward sums, with and without the
+    B -> C handoff."""
+    monkeypatch.setenv("MACM_HANDOFF", handoff)
+    b = FlockVec(E, n_agents=[N], seed=7 * E + N, device="cuda:0", **kw)
+    a = FlockVec(E, n_agents=[N], seed=7 * E + N, device="cuda:0", **kw)
+    acts = flock_actions(K, E, N, 17)
+    for k in range(K):
+        monkeypatch.setenv("MACM_SOLVE_PAIR", "0")
+        a.step(acts[k])
+        monkeypatch.setenv("MACM_SOLVE_PAIR", "1")
+        b.step(acts[k])
+    assert_same(a, b, "paired solve")
+    pa, ta = a.reward_sums()
+    pb, tb = b.reward_sums()
+    np.testing.assert_array_equal(pa, pb)
+    assert ta == tb and b.status() == 0
+
+
+def test_solve_pairs_in_slices(monkeypatch):
+    """The sliced rollout (3 slices of >= 1024 envs) with paired solves equals one-env-per-wave steps."""
+    E, N, K = 3100, 80, 5
+    b = FlockVec(E, n_agents=[N], seed=3, device="cuda:0")
+    a = FlockVec(E, n_agents=[N], seed=3, device="cuda:0")
+    acts = flock_actions(K, E, N, 19)
+    monkeypatch.setenv("MACM_SOLVE_PAIR", "0")
+    for k in range(K):
+        a.step(acts[k])
+    monkeypatch.setenv("MACM_SOLVE_PAIR", "1")
+    monkeypatch.setenv("MACM_WG_SLICES", "3")
+    b.rollout(acts)
+    assert_same(a, b, "paired solve in slices")

@@ -113,6 +113,31 @@ def main():
             out["island_labeling"] = {"envs_frac": float(isl.mean()), "cycles_mean": float(g[isl, 3].mean()),
                                       "cycles_max": float(g[isl, 3].max()), "rounds_mean": float(g[isl, 4].mean()),
                                       "rounds_max": int(g[isl, 4].max())}
+        # the launch-boundary tail. Per env and step, the cycles of each kernel (A, the
+        # dense envs' DFS kernel, B, C); every launch waits for its slowest env (sum over steps of the
+        # per-kernel maxima; with the B -> C handoff, B and C of an env run back to back) against a
+        # per-env pipeline that never waits for another env (max over envs of the env's own sum)
+        dk = d.reshape(args.steps, E, -1)
+        nA, nC, nB = len(PHASES_A), len(PHASES_C), len(PHASES_B)
+        kA = dk[:, :, :nA].sum(2)
+        kC = dk[:, :, nA:nA + nC].sum(2)
+        kB = dk[:, :, nA + nC:nA + nC + nB].sum(2)
+        kD = dk[:, :, nA + nC + nB:].sum(2)
+        per_launch = float((kA.max(1) + kD.max(1) + kB.max(1) + kC.max(1)).sum())
+        handoff = float((kA.max(1) + kD.max(1) + (kB + kC).max(1)).sum())
+        piped = float((kA + kD + kB + kC).sum(0).max())
+        deepest = int((kA + kD + kB + kC).sum(0).argmax())
+        out["pipeline"] = {
+            "steps": args.steps,
+            "per_launch_cycles": per_launch, "handoff_cycles": handoff, "per_env_pipeline_cycles": piped,
+            "pipeline_gain_bound_vs_handoff": 1.0 - piped / handoff,
+            "pipeline_gain_bound_vs_per_launch": 1.0 - piped / per_launch,
+            "deepest_env": deepest,
+            "deepest_env_kernel_cycles": {"A": float(kA[:, deepest].sum()), "DFS": float(kD[:, deepest].sum()),
+                                          "B": float(kB[:, deepest].sum()), "C": float(kC[:, deepest].sum())},
+            "kernel_max_cycles_sum": {"A": float(kA.max(1).sum()), "DFS": float(kD.max(1).sum()),
+                                      "B": float(kB.max(1).sum()), "C": float(kC.max(1).sum())},
+        }
         print(json.dumps(out, indent=1))
         if args.json:
             with open(args.json, "w") as f:
