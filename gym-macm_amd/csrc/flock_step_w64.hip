@@ -213,6 +213,11 @@ __device__ __forceinline__ uint32_t writelane_m0(int x, int l, uint32_t v) {
   return v;
 }
 
+// the number of set bits of m below this lane (v_mbcnt)
+__device__ __forceinline__ int mbcnt64(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
@@ -467,6 +472,16 @@ constexpr bool kWidePriority = false;
 constexpr bool kWideLevelOrder = false;
 #else
 constexpr bool kWideLevelOrder = true;
+#endif
+#ifdef MACM_PAR_DFS  // A/B knob: the scalar island walk a popped body at a time (all its edges at once)
+constexpr bool kParDfs = true;
+#else
+constexpr bool kParDfs = false;
+#endif
+#ifdef MACM_WIDE_REGMIN  // A/B knob: the wide position passes' island minima in registers
+constexpr bool kWideRegMin = true;
+#else
+constexpr bool kWideRegMin = false;
 #endif
 #ifdef MACM_WIDE_SCALAR  // A/B knob: the wide levels' updates on scalar components (round 4)
 constexpr bool kWidePacked = false;
@@ -736,6 +751,11 @@ struct WideLevels {
 #pragma unroll
       for (int q = 0; q < S; ++q) lvis[q] |= ((done >> isl(lvis[q])) & 1ull) ? (uint32_t)kNoLevel : 0u;
       wave_lds_sync();
+      // kWideRegMin: each slot's pass minimum (order-preserving int keys, as the atomics) in a register,
+      // one atomic per slot after the pass instead of one per contact on the level chain
+      int kmin[S];
+#pragma unroll
+      for (int q = 0; q < S; ++q) kmin[q] = 0;  // the pass minimum starts at 0.0f (key 0)
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {  // one slot at a time, busy slots only, as in the velocity passes
@@ -758,9 +778,16 @@ struct WideLevels {
             }
             // order-preserving int of the float for atomicMin
             const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
-            atomicMin(&s_pmin[isl(lvis[q])], key);
+            if constexpr (kWideRegMin) kmin[q] = min(kmin[q], key);
+            else atomicMin(&s_pmin[isl(lvis[q])], key);
           }
         }
+        wave_lds_sync();
+      }
+      if constexpr (kWideRegMin) {
+#pragma unroll
+        for (int q = 0; q < S; ++q)
+          if (lvl(lvis[q]) != kNoLevel) atomicMin(&s_pmin[isl(lvis[q])], kmin[q]);
         wave_lds_sync();
       }
       int km = lane < nisl ? s_pmin[lane] : 0;
@@ -1445,23 +1472,98 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       ++nisl;
     }
     };
+    // The same walk a popped body at a time (kParDfs, round 5): the body's unvisited edges are the set
+    // bits of one mask, so their places in the island order (the mask's bits below each contact lane),
+    // the bodies they push (lanes whose other body is not yet visited: one ballot) and those bodies'
+    // places on the stack are computed by all lanes at once and stored to LDS (s_ord, s_stack); the
+    // last push is popped next straight from registers. Same order, same pushes, same islands: a
+    // batch's contacts all touch the popped body, so no two of them reach the same other body.
+    auto pdfs = [&](auto wide) {
+      constexpr bool W2 = decltype(wide)::value;
+      // a contact's other body from the popped one: a ^ b ^ popped (one register per contact word)
+      const int cx = (int)((tabv & 0xffffu) ^ (tabv >> 16));
+      const int cx1 = (int)((tabv1 & 0xffffu) ^ (tabv1 >> 16));
+      unsigned long long vis = ~hasdeg, cvis = 0ull, cvis1 = 0ull;
+      for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
+        const int s = 63 - __clzll(todo);
+        icv = writelane_m0(nord, nisl, icv);  // s_ic[nisl]
+        const unsigned long long before = vis;
+        vis |= 1ull << s;
+        int sp = 0, b = s;
+        for (;;) {
+          const unsigned long long m = (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_hi, b) << 32) |
+                                        (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_lo, b)) & ~cvis;
+          cvis |= m;
+          const bool inm = (m >> lane) & 1ull;
+          const int o = cx ^ b;
+          const bool nw = inm && !((vis >> o) & 1ull);
+          const unsigned long long pm = __builtin_amdgcn_ballot_w64(nw);
+          if (inm) s_ord[nord + mbcnt64(m)] = (uint8_t)lane;
+          if (nw) s_stack[sp + mbcnt64(pm)] = (uint8_t)o;
+          int nm = __popcll(m), np = __popcll(pm);
+          unsigned long long pm1 = 0ull;
+          int o1 = 0;
+          if constexpr (W2) {
+            const unsigned long long m1 =
+                (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_hi, b) << 32) |
+                 (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_lo, b)) & ~cvis1;
+            cvis1 |= m1;
+            const bool inm1 = (m1 >> lane) & 1ull;
+            o1 = cx1 ^ b;
+            const bool nw1 = inm1 && !((vis >> o1) & 1ull);
+            pm1 = __builtin_amdgcn_ballot_w64(nw1);
+            if (inm1) s_ord[nord + nm + mbcnt64(m1)] = (uint8_t)(64 + lane);
+            if (nw1) s_stack[sp + np + mbcnt64(pm1)] = (uint8_t)o1;
+            nm += __popcll(m1);
+            np += __popcll(pm1);
+          }
+          nord += nm;
+          if (np) {
+            // the pushed bodies: the lanes (bodies) with a pushed contact among their touching ones
+            const unsigned long long hit = (tmask & pm) | (W2 ? (tmask1 & pm1) : 0ull);
+            vis |= __builtin_amdgcn_ballot_w64(hit != 0ull);
+            sp += np - 1;  // the last push is popped next, from registers
+            b = (W2 && pm1) ? __builtin_amdgcn_readlane(o1, 63 - __clzll(pm1))
+                            : __builtin_amdgcn_readlane(o, 63 - __clzll(pm));
+          } else if (sp > 0) {
+            --sp;
+            wave_lds_sync();
+            b = __builtin_amdgcn_readfirstlane((int)s_stack[sp]);
+          } else {
+            break;
+          }
+        }
+        if (((vis & ~before) >> lane) & 1ull) islv = (uint32_t)nisl;  // s_bisl: the island's bodies
+        ++nisl;
+      }
+    };
 #ifdef MACM_AB_DFS_TWICE  // timing-only A/B knob: the walk's cost (run once more, discarded)
     if (TMW == 2 && T > 64) dfs(BoolC<true>{});
     else dfs(BoolC<false>{});
     nord = nisl = nb = 0;
 #endif
-    if (TMW == 2 && T > 64) dfs(BoolC<true>{});
-    else dfs(BoolC<false>{});
+    if constexpr (kParDfs) {
+      if (TMW == 2 && T > 64) pdfs(BoolC<true>{});
+      else pdfs(BoolC<false>{});
+    } else {
+      if (TMW == 2 && T > 64) dfs(BoolC<true>{});
+      else dfs(BoolC<false>{});
+    }
     icv = writelane_m0(nord, nisl, icv);
-    ibv = writelane_m0(nb, nisl, ibv);
-    const bool wrapped = TMW == 2 && nord > 64;  // entries 0..63 in ordv1, 64.. in ordv
-    if (lane < nord) s_ord[lane] = (uint8_t)(wrapped ? ordv1 : ordv);
-    if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv;
-    if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
+    if constexpr (kParDfs) {
+      wave_lds_sync();
+      ordv = lane < nord ? (uint32_t)s_ord[lane] : 0u;  // the level paths read it from registers
+    } else {
+      ibv = writelane_m0(nb, nisl, ibv);
+      const bool wrapped = TMW == 2 && nord > 64;  // entries 0..63 in ordv1, 64.. in ordv
+      if (lane < nord) s_ord[lane] = (uint8_t)(wrapped ? ordv1 : ordv);
+      if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv;
+      if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
+    }
     if ((hasdeg >> lane) & 1ull) s_bisl[lane] = (uint8_t)islv;
     if (lane <= nisl) {
       s_ic[lane] = (uint16_t)icv;
-      s_ib[lane] = (uint8_t)ibv;
+      if constexpr (!kParDfs) s_ib[lane] = (uint8_t)ibv;
     }
     if (lane == 0) {
       s_nisl = nisl;
