@@ -110,8 +110,9 @@ def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20,
                        + ("the GPU leg's own actions" if same else "uniform random discrete actions")
                        + f", OpenMP {threads} threads, {dt:.2f} s timed")
     lv = None
-    if same and levels_budget_s > 0 and w_run == warmup and n >= steps:
-        # untimed replay of the GPU leg's window: the level structure each timed step solves
+    if same and levels_budget_s > 0 and w_run == warmup:
+        # untimed replay of the GPU leg's window: the level structure each timed step solves (the first
+        # steps of the window when the budget ends earlier: chain_floor records steps_sampled)
         orc2 = OracleFlock(cfg, tidx, E, seed)
         t0 = time.perf_counter()
         rows = []

@@ -197,6 +197,11 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 // flags, listener, counters 0-2); each thread passes its force `F`. The physics skips the bodies
 // that are not alive (their contacts were destroyed with their proxies) and the env layer is TDM's:
 // the body state, the [N, N-1, 4] observation, done / winner, counter 3.
+#ifndef MACM_SPILL_CHUNK  // A/B knob: records per HBM chunk of the spill step's serial island solves
+#define MACM_SPILL_CHUNK 8
+#endif
+constexpr int kSpillChunk = MACM_SPILL_CHUNK;
+
 template <typename OT, bool RECS_LDS, int MODE = kFlock, int BPT = 1>
 __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers& B, int e, int cur,
                                          const void* __restrict__ actions, OT* __restrict__ obs,
@@ -521,59 +526,84 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const float friction = P.friction;
 
   // ---- warm start + velocity iterations, one thread per island (b2ContactSolver) ---------------
+  // The records are in HBM (the slot's arrays): an island's thread reads them kSpillChunk at a time,
+  // all loads of a chunk issued before its first update (round 5: one L2 round trip per chunk on the
+  // serial chain instead of one per contact; the updates themselves are unchanged and in order)
+  // (the wave kernels' dense-env fallback, RECS_LDS, keeps one record at a time: its registers are the
+  // wave kernel's, whose occupancy a larger chunk would cost)
+  constexpr int U = RECS_LDS ? 1 : (BPT >= 4 ? kSpillChunk / 2 : kSpillChunk);
   for (int I = tid; I < nisl; I += BS) {
     const int c0 = (int)s_ic[I], c1 = (int)s_ic[I + 1];
+    auto chunk = [&](int k0, float4* r, float2* im) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int k = min(k0 + j, c1 - 1);
+        r[j] = g_cst[k];
+        im[j] = g_cim[k];
+      }
+    };
     if (P.warm_starting) {
-      for (int k = c0; k < c1; ++k) {
-        const float4 r = g_cst[k];
-        const float2 im = g_cim[k];
-        const uint32_t ab = __float_as_uint(r.x);
-        const int a = ab & 0xffffu, b = ab >> 16;
-        const float nx = r.y, ny = r.z, tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
-        const float Px = im.x * nx + im.y * tx, Py = im.x * ny + im.y * ty;
-        float2 va = s_v[a], vb = s_v[b];
-        va.x = va.x - mA * Px;
-        va.y = va.y - mA * Py;
-        vb.x = vb.x + mB * Px;
-        vb.y = vb.y + mB * Py;
-        s_v[a] = va;
-        s_v[b] = vb;
+      for (int k0 = c0; k0 < c1; k0 += U) {
+        float4 r[U];
+        float2 im[U];
+        chunk(k0, r, im);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          if (k0 + j >= c1) break;
+          const uint32_t ab = __float_as_uint(r[j].x);
+          const int a = ab & 0xffffu, b = ab >> 16;
+          const float nx = r[j].y, ny = r[j].z, tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
+          const float Px = im[j].x * nx + im[j].y * tx, Py = im[j].x * ny + im[j].y * ty;
+          float2 va = s_v[a], vb = s_v[b];
+          va.x = va.x - mA * Px;
+          va.y = va.y - mA * Py;
+          vb.x = vb.x + mB * Px;
+          vb.y = vb.y + mB * Py;
+          s_v[a] = va;
+          s_v[b] = vb;
+        }
       }
     }
     for (int it = 0; it < P.vel_iters; ++it) {
-      for (int k = c0; k < c1; ++k) {
-        const float4 r = g_cst[k];
-        float2 im = g_cim[k];
-        const uint32_t ab = __float_as_uint(r.x);
-        const int a = ab & 0xffffu, b = ab >> 16;
-        const float nx = r.y, ny = r.z, tx = ny, ty = -nx;
-        float2 va = s_v[a], vb = s_v[b];
-        {  // tangent first
-          const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-          const float vt = dvx * tx + dvy * ty;
-          float lambda = kmass * (-vt);
-          const float maxf = friction * im.x;
-          const float ni = sclamp(im.y + lambda, -maxf, maxf);
-          lambda = ni - im.y;
-          im.y = ni;
-          const float Px = lambda * tx, Py = lambda * ty;
-          va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-          vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+      for (int k0 = c0; k0 < c1; k0 += U) {
+        float4 r[U];
+        float2 imc[U];
+        chunk(k0, r, imc);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          if (k0 + j >= c1) break;
+          float2 im = imc[j];
+          const uint32_t ab = __float_as_uint(r[j].x);
+          const int a = ab & 0xffffu, b = ab >> 16;
+          const float nx = r[j].y, ny = r[j].z, tx = ny, ty = -nx;
+          float2 va = s_v[a], vb = s_v[b];
+          {  // tangent first
+            const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+            const float vt = dvx * tx + dvy * ty;
+            float lambda = kmass * (-vt);
+            const float maxf = friction * im.x;
+            const float ni = sclamp(im.y + lambda, -maxf, maxf);
+            lambda = ni - im.y;
+            im.y = ni;
+            const float Px = lambda * tx, Py = lambda * ty;
+            va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+            vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+          }
+          {  // normal (velocityBias == 0: restitution 0)
+            const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+            const float vn = dvx * nx + dvy * ny;
+            float lambda = -kmass * (vn - 0.0f);
+            const float ni = fmaxf(im.x + lambda, 0.0f);
+            lambda = ni - im.x;
+            im.x = ni;
+            const float Px = lambda * nx, Py = lambda * ny;
+            va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+            vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+          }
+          s_v[a] = va;
+          s_v[b] = vb;
+          g_cim[k0 + j] = im;
         }
-        {  // normal (velocityBias == 0: restitution 0)
-          const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-          const float vn = dvx * nx + dvy * ny;
-          float lambda = -kmass * (vn - 0.0f);
-          const float ni = fmaxf(im.x + lambda, 0.0f);
-          lambda = ni - im.x;
-          im.x = ni;
-          const float Px = lambda * nx, Py = lambda * ny;
-          va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-          vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
-        }
-        s_v[a] = va;
-        s_v[b] = vb;
-        g_cim[k] = im;
       }
     }
   }
@@ -610,8 +640,14 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     int solved = 0;
     for (int it = 0; it < P.pos_iters; ++it) {
       float min_sep = 0.0f;
-      for (int k = c0; k < c1; ++k) {
-        const uint32_t ab = __float_as_uint(g_cst[k].x);
+      for (int k0 = c0; k0 < c1; k0 += U) {
+        uint32_t abc[U];  // the chunk's pairs, loaded before its first update
+#pragma unroll
+        for (int j = 0; j < U; ++j) abc[j] = __float_as_uint(g_cst[min(k0 + j, c1 - 1)].x);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+        if (k0 + j >= c1) break;
+        const uint32_t ab = abc[j];
         const int a = ab & 0xffffu, b = ab >> 16;
         float2 ca = s_c[a], cb = s_c[b];
         float nx = cb.x - ca.x, ny = cb.y - ca.y;
@@ -626,6 +662,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
         cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
         s_c[a] = ca;
         s_c[b] = cb;
+        }
       }
       if (min_sep >= -3.0f * kLinearSlop) {
         solved = 1;
