@@ -267,10 +267,23 @@ struct Capacity {
 #ifndef MACM_SOLO_ENVS_DEFAULT
 #define MACM_SOLO_ENVS_DEFAULT 0
 #endif
+// Kernel dispatches run one at a time: HIP's serialisation switches, or a profiler collecting counters
+// (rocprofv3 --pmc serialises dispatches to attribute counters to them). The two producer/consumer
+// launches (the solo split, the B -> C handoff) need their consumer to run BESIDE the producer: under
+// serialisation the consumer's wait would time out and the step be left incomplete, so they are off.
+static bool serialized_dispatch() {
+  for (const char* k : {"AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING"}) {
+    const char* v = getenv(k);
+    if (v && atoi(v) != 0) return true;
+  }
+  const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
+  return pmc && *pmc && strcmp(pmc, "0") != 0 && strcasecmp(pmc, "false") != 0;
+}
+
 static int solo_envs() {
   const char* v = getenv("MACM_SOLO_ENVS");
   const int n = v ? atoi(v) : MACM_SOLO_ENVS_DEFAULT;
-  return n > 0 ? n : 0;
+  return (n > 0 && !serialized_dispatch()) ? n : 0;
 }
 
 // The most agents per env (Flock and TDM): one workgroup of 1024 threads, up to 4 bodies per thread
@@ -654,7 +667,7 @@ static HandoffStream* handoff_for(macm_world* w) {
   if (w->wave || w->big || w->ho_tried) return w->ho;
   w->ho_tried = true;
   const char* v = getenv("MACM_HANDOFF");
-  if (!(v ? atoi(v) != 0 : kHandoffDefault)) return nullptr;
+  if (!(v ? atoi(v) != 0 : kHandoffDefault) || serialized_dispatch()) return nullptr;
   HandoffStream* h = new HandoffStream{};
   bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&h->done, hipEventDisableTiming) == hipSuccess &&

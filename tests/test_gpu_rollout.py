@@ -357,3 +357,39 @@ def test_solve_pairs_in_slices(monkeypatch):
     monkeypatch.setenv("MACM_WG_SLICES", "3")
     b.rollout(acts)
     assert_same(a, b, "paired solve in slices")
+
+
+def test_handoff_is_off_under_serialized_dispatch():
+    """With kernel dispatches serialised (AMD_SERIALIZE_KERNEL, or a profiler collecting counters:
+    ROCPROF_COUNTER_COLLECTION) the B -> C handoff's consumer cannot run beside its producer; the
+    library then steps without it, and the results are complete and equal to the default run's."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, "gym-macm_amd")
+from gym_macm.vec import FlockVec
+E, N, K = 48, 100, 3
+v = FlockVec(E, n_agents=[N], seed=9, device="cuda:0")
+g = torch.Generator(device="cuda:0"); g.manual_seed(3)
+for _ in range(K):
+    v.step(torch.randint(0, 3, (E, N, 3), dtype=torch.uint8, device="cuda:0", generator=g))
+torch.cuda.synchronize()
+assert v.status() == 0, v.status()
+c = v.counters()
+assert int(c[0]) == E * N * K, c
+np.save(sys.argv[1], v.get_state()["pos"])
+'''
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for extra in ({"ROCPROF_COUNTER_COLLECTION": "1"}, {"AMD_SERIALIZE_KERNEL": "3"}, {}):
+        env = dict(os.environ, MACM_HANDOFF="1", **extra)
+        out = os.path.join(repo, "gpurun_out", f"serialized_{len(outs)}.npy")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        r = subprocess.run([sys.executable, "-c", code, out], cwd=repo, env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, (extra, r.stdout[-2000:], r.stderr[-2000:])
+        outs.append(np.load(out))
+    np.testing.assert_array_equal(outs[0], outs[2])
+    np.testing.assert_array_equal(outs[1], outs[2])
