@@ -21,6 +21,7 @@
 #include <type_traits>
 #include <mutex>
 
+#include "bots.hpp"
 #include "flock_common.hpp"
 #include "flock_spill.hpp"
 #include "flock_grid.hpp"
@@ -1963,7 +1964,8 @@ template <typename OT>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void flock_step_wg_c(StepParams P, WorldBuffers B, int cur, int tcap,
                                                         OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
                                                         float* __restrict__ rew_out, uint8_t* __restrict__ coll_out,
-                                                        uint8_t* __restrict__ done_out, Handoff H) {
+                                                        uint8_t* __restrict__ done_out, Handoff H,
+                                                        uint8_t* __restrict__ bot_act) {
   using namespace wg;
   extern __shared__ __align__(16) unsigned char lds[];
   // in kernel B's finish order (the block scan's scratch words carry the env to the block)
@@ -1993,7 +1995,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   // another XCD while this kernel runs: its island outputs are read write-through, as B's solve outputs
   const bool hwt = H.q != nullptr;
   const int nisl = hwt ? ld_wt(B.x_nisl + e) : B.x_nisl[e];
-  if (nisl < 0) return;  // stepped whole by the spill step in kernel A
+  if (nisl < 0) {  // stepped whole by the spill step in kernel A (its observation is written)
+    if (bot_act && obs && act) {
+      const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
+      bot_flock_row<OT>(obs + ag * od, od, bot_act + ag * 3);
+    }
+    return;
+  }
   WSTAMP(0);
 
   const uint32_t* cab = B.cab[cur] + (size_t)e * C;
@@ -2427,6 +2435,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       const int od = P.coord == MACM_COORD_CARTESIAN ? 6 : 4;
       const float2 cb = s_c[bj];
       write_obs<OT>(obs + ag * od, P.coord, ang, best, cb.x - cx, cb.y - cy, tdx, tdy, td2);
+      // the closed loop's next action (bots.flock on the row as stored: this thread's own stores)
+      if (bot_act) bot_flock_row<OT>(obs + ag * od, od, bot_act + ag * 3);
     }
   }
   int dummy;  // both counts in one scan (collided in the low half, rewarded in the high)
@@ -2551,7 +2561,7 @@ hipError_t wg_configure(int N, int tcap) {
 // caller's stream waits for C at the end, so the call's results are complete on `s` as before.
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
-                          hipStream_t s, HandoffStream* HS) {
+                          hipStream_t s, HandoffStream* HS, uint8_t* bot_act) {
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
   Handoff H{nullptr, nullptr, nullptr, 0u};
   if (HS && kWgEnvOrder && B.sched) {
@@ -2568,10 +2578,10 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   auto launch_c = [&](hipStream_t cs) {
     if (obs_f64)
       hipLaunchKernelGGL(flock_step_wg_c<double>, grid, block, lc, cs, P, B, cur, tcap, (double*)obs, nbr, rew, coll,
-                         done, H);
+                         done, H, bot_act);
     else
       hipLaunchKernelGGL(flock_step_wg_c<float>, grid, block, lc, cs, P, B, cur, tcap, (float*)obs, nbr, rew, coll,
-                         done, H);
+                         done, H, bot_act);
   };
   if (obs_f64)
     hipLaunchKernelGGL(flock_step_wg_a<double>, grid, block, la, s, P, B, cur, tcap, actions, (double*)obs, nbr, rew,

@@ -27,7 +27,7 @@ hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* 
                               hipStream_t s);
 hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, int tcap, const void* actions,
                           void* obs, bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
-                          hipStream_t s, HandoffStream* HS);
+                          hipStream_t s, HandoffStream* HS, uint8_t* bot_act = nullptr);
 hipError_t launch_init_wg(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64, int32_t* nbr,
                           const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_wg(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
@@ -814,12 +814,11 @@ static int rollout_wg_slices(macm_world* w, int S, const unsigned char* actions,
       auto row = [e0](auto* p, size_t per_env) { return p ? p + e0 * per_env : p; };
       unsigned char* obs_i = ok.obs ? static_cast<unsigned char*>(ok.obs) + e0 * od : nullptr;
       const unsigned char* act_k = actions + k * kstride + e0 * abytes;
-      hipError_t he = launch_step_wg(Ps[i], Bs[i], cur, w->tcap, act_k, obs_i, w->cfg.obs_f64 != 0,
-                                     row(ok.nbr_id, N), row(ok.reward, N), row(ok.collided, N), row(ok.done, 1),
-                                     w->slice_streams[i], nullptr);
-      if (he == hipSuccess && bots)
-        he = launch_bots_flock(obs_i, w->cfg.obs_f64 != 0, obs_dim(w->cfg), (long long)Ps[i].n_envs * N,
-                               const_cast<unsigned char*>(act_k) + (traj ? (size_t)E * abytes : 0), w->slice_streams[i]);
+      // closed loop: kernel C takes the bot's next actions from the rows it writes (no bots launch)
+      uint8_t* const bot = bots ? const_cast<unsigned char*>(act_k) + (traj ? (size_t)E * abytes : 0) : nullptr;
+      const hipError_t he = launch_step_wg(Ps[i], Bs[i], cur, w->tcap, act_k, obs_i, w->cfg.obs_f64 != 0,
+                                           row(ok.nbr_id, N), row(ok.reward, N), row(ok.collided, N),
+                                           row(ok.done, 1), w->slice_streams[i], nullptr, bot);
       if (he != hipSuccess) rc = fail(MACM_E_HIP, std::string("rollout launch: ") + hipGetErrorString(he));
     }
     if (rc == MACM_OK) ++launched;
@@ -883,9 +882,10 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
                               ok.collided, ok.done, s));
     else
       HIP_TRY(launch_step_wg(w->P, w->B, w->cur, w->tcap, act_k, ok.obs, w->cfg.obs_f64 != 0, ok.nbr_id, ok.reward,
-                             ok.collided, ok.done, s, handoff_for(w)));
+                             ok.collided, ok.done, s, handoff_for(w),
+                             bots ? const_cast<unsigned char*>(act_k) + (traj ? rows * 3 : 0) : nullptr));
     w->cur ^= 1;
-    if (bots)
+    if (bots && w->big)
       HIP_TRY(launch_bots_flock(ok.obs, w->cfg.obs_f64 != 0, obs_dim(w->cfg), rows,
                                 const_cast<unsigned char*>(act_k) + (traj ? rows * 3 : 0), s));
   }

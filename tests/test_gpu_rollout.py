@@ -162,6 +162,8 @@ def test_tdm_rollout_equals_per_step(teams, K, obs_f64):
     (32, 20, 8, {"obs_dtype": torch.float64, "coord": "cartesian"}),
     (4, 100, 4, {"start_spread": 12}),  # workgroup path: step + bots launches
     (1031, 100, 4, {"start_spread": 12}),  # workgroup path in env slices on their own streams
+    (8, 100, 4, {"start_spread": 4}),  # dense: spill-stepped envs' next actions from kernel C too
+    (6, 100, 3, {"start_spread": 12, "coord": "cartesian", "obs_dtype": torch.float64}),
 ])
 def test_flock_closed_loop_rollout_equals_per_step(E, N, K, kw):
     """macm_world_rollout_bots vs K x (step, bots.flock) launches: same state, outputs and actions."""
