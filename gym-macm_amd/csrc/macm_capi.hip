@@ -557,6 +557,7 @@ int macm_world_info_get(const macm_world* w, macm_world_info* info) {
   info->max_touching = w->tcap;
   info->device = w->device;
   info->spill_slots = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;
+  info->launch_flags = w->ho ? MACM_LAUNCH_HANDOFF : 0;
   return MACM_OK;
 }
 

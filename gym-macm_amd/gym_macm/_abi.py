@@ -76,6 +76,9 @@ class MacmState(Structure):
         "contact_imp", "step_count", "time_passed")] + [("contact_stride", c_int64)]
 
 
+LAUNCH_HANDOFF = 1  # macm_world_info.launch_flags
+
+
 class MacmWorldInfo(Structure):
     _fields_ = [
         ("n_envs", c_int32),
@@ -86,6 +89,7 @@ class MacmWorldInfo(Structure):
         ("max_touching", c_int32),
         ("device", c_int32),
         ("spill_slots", c_int32),
+        ("launch_flags", c_int32),
     ]
 
 

@@ -336,6 +336,16 @@ class World:
         _abi.check(self.L.macm_world_counters(self.h, out, self._stream()), "macm_world_counters")
         return np.array(list(out), np.int64)
 
+    def launch_flags(self) -> int:
+        """macm_world_info.launch_flags (MACM_LAUNCH_*): how the workgroup step launches, decided at the
+        world's first step (the B -> C handoff)."""
+        info = _abi.MacmWorldInfo()
+        _abi.check(self.L.macm_world_info_get(self.h, ctypes.byref(info)), "macm_world_info_get")
+        return int(info.launch_flags)
+
+    def uses_handoff(self) -> bool:
+        return bool(self.launch_flags() & _abi.LAUNCH_HANDOFF)
+
     def reward_sums(self):
         """(per-env reward totals [E] float64, their sum in env order) accumulated since creation or
         reset_counters, in the device's fixed order (macm_world_reward_sums; restated on the host by

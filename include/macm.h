@@ -266,7 +266,11 @@ typedef struct macm_world_info {
   int32_t max_touching;   /* per-env solver capacity               */
   int32_t device;
   int32_t spill_slots;    /* spill working-set slots (= n_envs: one per env; fewer: a pool) */
+  int32_t launch_flags;   /* MACM_LAUNCH_* of the workgroup step, decided at the first step (ABI 8) */
 } macm_world_info;
+
+/* macm_world_info.launch_flags */
+#define MACM_LAUNCH_HANDOFF 1  /* kernel C as kernel B's consumer on a second stream (MACM_HANDOFF) */
 
 typedef struct macm_world macm_world;
 

@@ -274,14 +274,15 @@ def test_handoff_equals_plain_workgroup_step(monkeypatch, E, N, K, kw):
     taking the envs in kernel B's finish order, B's outputs handed over write-through) gives the plain
     launch order's results bit for bit: state, lists, outputs, counters and reward sums, per-step and
     rollout launches."""
-    monkeypatch.setenv("MACM_HANDOFF", "1")
     b = FlockVec(E, n_agents=[N], seed=E + N, device="cuda:0", **kw)
-    monkeypatch.setenv("MACM_HANDOFF", "0")
     a = FlockVec(E, n_agents=[N], seed=E + N, device="cuda:0", **kw)
     acts = flock_actions(2 * K, E, N, 7)
-    for k in range(K):
+    for k in range(K):  # a world takes its handoff decision at its first workgroup step
+        monkeypatch.setenv("MACM_HANDOFF", "0")
         a.step(acts[k])
+        monkeypatch.setenv("MACM_HANDOFF", "1")
         b.step(acts[k])
+    assert b.world.uses_handoff() and not a.world.uses_handoff()
     assert_same(a, b, "handoff per-step launches")
     for k in range(K, 2 * K):
         a.step(acts[k])
