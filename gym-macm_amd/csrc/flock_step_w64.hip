@@ -478,6 +478,11 @@ constexpr bool kParDfs = true;
 #else
 constexpr bool kParDfs = false;
 #endif
+#ifdef MACM_PAR_DFS_WIDE  // A/B knob: the same for more than 64 touching contacts only (converged flocks)
+constexpr bool kParDfsWide = true;
+#else
+constexpr bool kParDfsWide = false;
+#endif
 #ifdef MACM_WIDE_REGMIN  // A/B knob: the wide position passes' island minima in registers
 constexpr bool kWideRegMin = true;
 #else
@@ -1542,15 +1547,18 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     else dfs(BoolC<false>{});
     nord = nisl = nb = 0;
 #endif
+    const bool par = kParDfs || (kParDfsWide && TMW == 2 && T > 64);
     if constexpr (kParDfs) {
       if (TMW == 2 && T > 64) pdfs(BoolC<true>{});
       else pdfs(BoolC<false>{});
+    } else if (par) {
+      pdfs(BoolC<true>{});
     } else {
       if (TMW == 2 && T > 64) dfs(BoolC<true>{});
       else dfs(BoolC<false>{});
     }
     icv = writelane_m0(nord, nisl, icv);
-    if constexpr (kParDfs) {
+    if (par) {
       wave_lds_sync();
       ordv = lane < nord ? (uint32_t)s_ord[lane] : 0u;  // the level paths read it from registers
     } else {
@@ -1563,7 +1571,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     if ((hasdeg >> lane) & 1ull) s_bisl[lane] = (uint8_t)islv;
     if (lane <= nisl) {
       s_ic[lane] = (uint16_t)icv;
-      if constexpr (!kParDfs) s_ib[lane] = (uint8_t)ibv;
+      if (!par) s_ib[lane] = (uint8_t)ibv;
     }
     if (lane == 0) {
       s_nisl = nisl;
