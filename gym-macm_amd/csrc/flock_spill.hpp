@@ -202,6 +202,22 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 #endif
 constexpr int kSpillChunk = MACM_SPILL_CHUNK;
 
+// Diagnostic build (MACM_STAMPS): phase clocks of the worlds above 1024 agents (BPT > 1: only the spill
+// step runs there), stamps 16.. of the env's row (tools/big_phases.py)
+#ifdef MACM_STAMPS
+#define SSTAMP(k)                                                                  \
+  do {                                                                             \
+    if constexpr (BPT > 1) {                                                       \
+      __syncthreads();                                                             \
+      if (threadIdx.x == 0) B.stamps[(size_t)e * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    }                                                                              \
+  } while (0)
+#else
+#define SSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 template <typename OT, bool RECS_LDS, int MODE = kFlock, int BPT = 1>
 __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers& B, int e, int cur,
                                          const void* __restrict__ actions, OT* __restrict__ obs,
@@ -287,6 +303,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   float2* g_cim = B.sp_cim + (size_t)slot * C;
   float2* g_lam = B.sp_lam + (size_t)slot * C;
 
+  SSTAMP(0);
   // ---- loads ------------------------------------------------------------------------------
   const uint32_t* cab = B.cab[cur] + (size_t)e * C;
   const float2* cimp = B.cimp[cur] + (size_t)e * C;
@@ -365,6 +382,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
   __syncthreads();
 
+  SSTAMP(1);
   // ---- Collide: ordered compaction of the touching contacts (list order) ----------------------
   const float rr = (P.radius + P.radius) * (P.radius + P.radius);
   const float dt_ratio = step_count > 0 ? P.inv_dt * P.dt : 0.0f;  // m_inv_dt0 * dt
@@ -397,6 +415,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
   __syncthreads();
 
+  SSTAMP(2);
   // ---- CSR touching edges, each body's segment in list (= Box2D edge) order -------------------
   for (int t = tid; t < T; t += BS) {
     const uint32_t ab = g_tab[t];
@@ -448,6 +467,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
   __syncthreads();
 
+  SSTAMP(3);
   // ---- island DFS in Box2D order, serial on thread 0 ---------------------------------------------
   // Seeds: bodies with touching edges, highest index first (reverse creation order). A body is
   // visited once its s_todo bit is cleared; a contact once bit 31 of its g_tab entry is set
@@ -495,6 +515,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const int nisl = s_misc[0];
   const int nord = nisl > 0 ? (int)s_ic[nisl] : 0;
 
+  SSTAMP(4);
   // ---- integrate velocities + damping; island-ordered records with normals --------------------
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
@@ -525,6 +546,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;  // normalMass == tangentMass
   const float friction = P.friction;
 
+  SSTAMP(5);
   // ---- warm start + velocity iterations, one thread per island (b2ContactSolver) ---------------
   // The records are in HBM (the slot's arrays): an island's thread reads them kSpillChunk at a time,
   // all loads of a chunk issued before its first update (round 5: one L2 round trip per chunk on the
@@ -610,6 +632,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   __syncthreads();
   for (int k = tid; k < nord; k += BS) g_lam[g_ord[k]] = g_cim[k];  // StoreImpulses, list order
 
+  SSTAMP(6);
   // ---- integrate positions ----------------------------------------------------------------------
   float cx[BPT], cy[BPT], vx[BPT], vy[BPT];
 #pragma unroll
@@ -634,6 +657,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
   __syncthreads();
 
+  SSTAMP(7);
   // ---- position iterations, one thread per island (early exit at -3 linearSlop) ---------------------
   for (int I = tid; I < nisl; I += BS) {
     const int c0 = (int)s_ic[I], c1 = (int)s_ic[I + 1];
@@ -672,6 +696,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     s_isolv[I] = (uint8_t)solved;
   }
 
+  SSTAMP(8);
   // ---- sleep clock + island sleep decision (b2Island::Solve) --------------------------------------
   float ns[BPT];
 #pragma unroll
@@ -734,6 +759,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   }
   __syncthreads();
 
+  SSTAMP(9);
   // ---- all-pairs sweep: collisions, new-pair counts, nearest neighbour (mvmnt.py:185-196) ------------
   //   world.contacts after the step = Ov(F_{t-1}) U Ov(F_t); new contacts = Ov(F_t) \ Ov(F_{t-1})
   bool coll[BPT];
@@ -762,6 +788,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       }
     }
   }
+  SSTAMP(10);
   // ---- next ordered list: new pairs (a desc, b desc) ++ surviving old pairs -------------------------
   uint32_t* ocab = B.cab[nxt] + (size_t)e * C;
   float2* ocimp = B.cimp[nxt] + (size_t)e * C;
@@ -970,6 +997,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       add_reward_sum(B, e, rsum);
       if (B.spill_count) B.spill_count[e] += 1u;
     }
+    SSTAMP(11);
     release_slot(B, slot);  // the observation above reads recs (HBM when !RECS_LDS)
   }
 }
