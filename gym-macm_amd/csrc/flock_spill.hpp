@@ -546,6 +546,164 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;  // normalMass == tangentMass
   const float friction = P.friction;
 
+  // ---- BPT > 1 (worlds above 1024 agents): Gauss-Seidel levels, as the workgroup path's kernel B ---
+  // level(k) = 1 + the level of the last earlier contact (island order) sharing a body with k, so a
+  // level's contacts share no body and every body keeps Box2D's sequence of updates; one wave then
+  // steps the levels with 64 contacts at a time instead of one thread per island walking its
+  // contacts one by one (round 5). The records stay in island order (g_cst, g_cim); g_lidx lists
+  // them in level order. Working arrays dead by now: g_adj (the walk's CSR edges), g_tab (the
+  // touching pairs, read by the records above), s_deg, s_off, s_stk, s_slp.
+  uint32_t* g_lvl = g_adj;       // [nord] level | island << 16 of island-order contact k
+  uint32_t* g_lidx = g_adj + C;  // [nord] the island-order index of the p-th contact in level order
+  uint32_t* g_hist = g_tab;      // [levels] counts, then positions
+  auto level_body = [&](float4 r, float2& im, bool warm, float2& va, float2& vb) {
+    const float nx = r.y, ny = r.z, tx = ny, ty = -nx;
+    if (warm) {
+      const float Px = im.x * nx + im.y * tx, Py = im.x * ny + im.y * ty;
+      va.x = va.x - mA * Px;
+      va.y = va.y - mA * Py;
+      vb.x = vb.x + mB * Px;
+      vb.y = vb.y + mB * Py;
+      return;
+    }
+    {  // tangent first
+      const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+      const float vt = dvx * tx + dvy * ty;
+      float lambda = kmass * (-vt);
+      const float maxf = friction * im.x;
+      const float ni = sclamp(im.y + lambda, -maxf, maxf);
+      lambda = ni - im.y;
+      im.y = ni;
+      const float Px = lambda * tx, Py = lambda * ty;
+      va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+      vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+    }
+    {  // normal (velocityBias == 0: restitution 0)
+      const float dvx = vb.x - va.x, dvy = vb.y - va.y;
+      const float vn = dvx * nx + dvy * ny;
+      float lambda = -kmass * (vn - 0.0f);
+      const float ni = fmaxf(im.x + lambda, 0.0f);
+      lambda = ni - im.x;
+      im.x = ni;
+      const float Px = lambda * nx, Py = lambda * ny;
+      va.x = va.x - mA * Px; va.y = va.y - mA * Py;
+      vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+    }
+  };
+  // one wave walks the level-ordered contacts in chunks of 64 (one per lane, loaded a chunk ahead); in
+  // a chunk it steps its levels, the lanes of the current level updating together and the others on a
+  // dummy LDS slot (branch-free); a level cut by a chunk boundary is finished in the next chunk
+  struct LSlot {
+    float4 r;
+    float2 m;
+    uint32_t li;
+    int k;
+  };
+  const int nlev_chunks = (nord + W - 1) / W;
+  auto lload = [&](int c, LSlot& x) {
+    const int q = min(c * W + (tid & (W - 1)), nord - 1);
+    x.k = (int)g_lidx[q];
+    x.r = g_cst[x.k];
+    x.m = g_cim[x.k];
+    x.li = g_lvl[x.k];
+  };
+  auto lwait = [&]() { __builtin_amdgcn_s_waitcnt(0x0f70); };  // vmcnt(0)
+  auto lsync = [&]() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); };
+  auto lchunk = [&](int c, const LSlot& x, int& rel, int& nsteps) {
+    const int lane = tid & (W - 1);
+    const bool valid = c * W + lane < nord;
+    const int mylv = valid ? (int)(x.li & 0xffffu) : 0x7fff;
+    const int lv0 = __builtin_amdgcn_readfirstlane(mylv);
+    const int lv1 = __builtin_amdgcn_readlane(mylv, min(W, nord - c * W) - 1);
+    rel = valid ? mylv - lv0 : 0x7fff;
+    nsteps = lv1 - lv0 + 1;
+  };
+  bool leveled = false;
+  if constexpr (BPT > 1) {
+    for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0u;
+    __syncthreads();
+    if (tid == 0) {  // the levels, serial in island order (its pairs read 16 records ahead)
+      int dmax = 0, I = 0;
+      constexpr int LA = 16;
+      uint32_t abq[LA];
+#pragma unroll
+      for (int j = 0; j < LA; ++j) abq[j] = __float_as_uint(g_cst[min(j, max(nord - 1, 0))].x);
+      for (int k0 = 0; k0 < nord; k0 += LA) {
+#pragma unroll
+        for (int j = 0; j < LA; ++j) {
+          const int k = k0 + j;
+          if (k >= nord) continue;
+          const uint32_t ab = abq[j];
+          abq[j] = __float_as_uint(g_cst[min(k + LA, nord - 1)].x);
+          while (I + 1 < nisl && (int)s_ic[I + 1] <= k) ++I;
+          const int a = ab & 0xffffu, b = ab >> 16;
+          const int l = (int)max(s_deg[a], s_deg[b]);
+          s_deg[a] = s_deg[b] = (uint32_t)(l + 1);
+          g_lvl[k] = (uint32_t)l | ((uint32_t)I << 16);
+          dmax = max(dmax, l + 1);
+        }
+      }
+      s_misc[2] = dmax;
+    }
+    __syncthreads();
+    const int nlev = s_misc[2];
+    for (int q = tid; q < nlev; q += BS) g_hist[q] = 0u;
+    __syncthreads();
+    for (int k = tid; k < nord; k += BS) atomicAdd(&g_hist[g_lvl[k] & 0xffffu], 1u);
+    __syncthreads();
+    {  // exclusive scan of the level counts
+      int base = 0;
+      for (int q0 = 0; q0 < nlev; q0 += BS) {
+        const int q = q0 + tid;
+        const int c = q < nlev ? (int)g_hist[q] : 0;
+        int off;
+        const int tot = block_scan_excl(c, off, s_scan);
+        if (q < nlev) g_hist[q] = (uint32_t)(base + off);
+        base += tot;
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    for (int k = tid; k < nord; k += BS) g_lidx[atomicAdd(&g_hist[g_lvl[k] & 0xffffu], 1u)] = (uint32_t)k;
+    __syncthreads();
+    leveled = true;
+    if (tid < W && nord > 0) {
+      float2* const s_dum = reinterpret_cast<float2*>(s_off);  // the walk's CSR offsets: dead
+      auto vel_pass = [&](bool warm) {
+        LSlot cur, nxt;
+        lload(0, cur);
+        lwait();
+        for (int c = 0; c < nlev_chunks; ++c) {
+          lload(c + 1, nxt);
+          int rel, nsteps;
+          lchunk(c, cur, rel, nsteps);
+          const uint32_t ab = __float_as_uint(cur.r.x);
+          float2* const pa0 = s_v + (ab & 0xffffu);
+          float2* const pb0 = s_v + (ab >> 16);
+          float2* const pd = s_dum;  // one shared dummy slot
+          float2 im = cur.m;
+          for (int i = 0; i < nsteps; ++i) {
+            const bool on = rel == i;
+            float2* const pa = on ? pa0 : pd;
+            float2* const pb = on ? pb0 : pd;
+            float2 va = *pa, vb = *pb;
+            float2 lm = im;
+            level_body(cur.r, lm, warm, va, vb);
+            *pa = va;
+            *pb = vb;
+            im = on ? lm : im;
+            lsync();
+          }
+          if (!warm && c * W + (tid & (W - 1)) < nord) g_cim[cur.k] = im;
+          lwait();
+          cur = nxt;
+        }
+      };
+      if (P.warm_starting) vel_pass(true);
+      for (int it = 0; it < P.vel_iters; ++it) vel_pass(false);
+    }
+  }
+
   SSTAMP(5);
   // ---- warm start + velocity iterations, one thread per island (b2ContactSolver) ---------------
   // The records are in HBM (the slot's arrays): an island's thread reads them kSpillChunk at a time,
@@ -554,7 +712,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   // (the wave kernels' dense-env fallback, RECS_LDS, keeps one record at a time: its registers are the
   // wave kernel's, whose occupancy a larger chunk would cost)
   constexpr int U = RECS_LDS ? 1 : (BPT >= 4 ? kSpillChunk / 2 : kSpillChunk);
-  for (int I = tid; I < nisl; I += BS) {
+  for (int I = leveled ? nisl : tid; I < nisl; I += BS) {
     const int c0 = (int)s_ic[I], c1 = (int)s_ic[I + 1];
     auto chunk = [&](int k0, float4* r, float2* im) {
 #pragma unroll
@@ -658,8 +816,70 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   __syncthreads();
 
   SSTAMP(7);
+  if constexpr (BPT > 1) {
+    // the position passes by levels (leveled: BPT > 1), as kernel B: an island leaves after the
+    // first pass whose minimum separation (from 0) is >= -3 linearSlop; the minimum by LDS float
+    // atomics (order-independent), the islands' flags in s_isolv
+    for (int I = tid; I < nisl; I += BS) s_isolv[I] = 0;
+    __syncthreads();
+    if (tid < W && nord > 0) {
+      float* const s_mins = s_slp;                              // [nisl] (the sleep clocks come later)
+      float2* const pdd = reinterpret_cast<float2*>(s_off);     // a shared dummy slot
+      float* const pmd = reinterpret_cast<float*>(s_off) + 2 + (tid & (W - 1));  // a dummy minimum per lane
+      const float K = mA + mB;
+      for (int it = 0; it < P.pos_iters; ++it) {
+        for (int I = tid; I < nisl; I += W) s_mins[I] = 0.0f;
+        lsync();
+        LSlot cur, nxt;
+        lload(0, cur);
+        lwait();
+        for (int c = 0; c < nlev_chunks; ++c) {
+          lload(c + 1, nxt);
+          int rel, nsteps;
+          lchunk(c, cur, rel, nsteps);
+          const int I = (int)(cur.li >> 16);
+          const bool live = c * W + (tid & (W - 1)) < nord && !s_isolv[I];
+          const int relp = live ? rel : 0x7fff;
+          const uint32_t ab = __float_as_uint(cur.r.x);
+          float2* const pca = s_c + (ab & 0xffffu);
+          float2* const pcb = s_c + (ab >> 16);
+          for (int i = 0; i < nsteps; ++i) {
+            const bool on = relp == i;
+            float2* const pa = on ? pca : pdd;
+            float2* const pb = on ? pcb : pdd;
+            float* const pm = on ? s_mins + I : pmd;
+            float2 ca = *pa, cb = *pb;
+            float nx = cb.x - ca.x, ny = cb.y - ca.y;
+            normalize(nx, ny);
+            const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - P.radius - P.radius;
+            const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+            const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
+            const float Px = imp * nx, Py = imp * ny;
+            ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
+            cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
+            *pa = ca;
+            *pb = cb;
+            __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            lsync();
+          }
+          lwait();
+          cur = nxt;
+        }
+        lsync();
+        bool open = false;
+        for (int I = tid; I < nisl; I += W) {
+          if (s_isolv[I]) continue;
+          if (s_mins[I] >= -3.0f * kLinearSlop) s_isolv[I] = 1;
+          else open = true;
+        }
+        lsync();
+        if (__ballot(open) == 0ull) break;
+      }
+    }
+    __syncthreads();
+  }
   // ---- position iterations, one thread per island (early exit at -3 linearSlop) ---------------------
-  for (int I = tid; I < nisl; I += BS) {
+  for (int I = leveled ? nisl : tid; I < nisl; I += BS) {
     const int c0 = (int)s_ic[I], c1 = (int)s_ic[I + 1];
     int solved = 0;
     for (int it = 0; it < P.pos_iters; ++it) {
