@@ -218,7 +218,7 @@ constexpr int kSpillChunk = MACM_SPILL_CHUNK;
   } while (0)
 #endif
 
-template <typename OT, bool RECS_LDS, int MODE = kFlock, int BPT = 1>
+template <typename OT, bool RECS_LDS, int MODE = kFlock, int BPT = 1, bool LEVELS = (BPT > 1)>
 __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers& B, int e, int cur,
                                          const void* __restrict__ actions, OT* __restrict__ obs,
                                          int32_t* __restrict__ nbr_out, float* __restrict__ rew_out,
@@ -546,7 +546,8 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;  // normalMass == tangentMass
   const float friction = P.friction;
 
-  // ---- BPT > 1 (worlds above 1024 agents): Gauss-Seidel levels, as the workgroup path's kernel B ---
+  // ---- LEVELS (the workgroup callers: worlds above 1024 agents, TDM above 64, dense workgroup envs):
+  //      Gauss-Seidel levels, as the workgroup path's kernel B --------------------------------------
   // level(k) = 1 + the level of the last earlier contact (island order) sharing a body with k, so a
   // level's contacts share no body and every body keeps Box2D's sequence of updates; one wave then
   // steps the levels with 64 contacts at a time instead of one thread per island walking its
@@ -619,7 +620,10 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     nsteps = lv1 - lv0 + 1;
   };
   bool leveled = false;
-  if constexpr (BPT > 1) {
+  // few touching contacts (sparse envs): the islands' own threads are as fast and skip the set-up
+  // (TDM 2 x 64 at 1024 envs: +2% with levels; 2 x 256: -38%)
+  constexpr int kLevelMinContacts = 64;
+  if (LEVELS && nord >= kLevelMinContacts) {
     for (int q = tid; q < N + 2; q += BS) s_deg[q] = 0u;
     __syncthreads();
     if (tid == 0) {  // the levels, serial in island order (its pairs read 16 records ahead)
@@ -816,8 +820,8 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   __syncthreads();
 
   SSTAMP(7);
-  if constexpr (BPT > 1) {
-    // the position passes by levels (leveled: BPT > 1), as kernel B: an island leaves after the
+  if (leveled) {
+    // the position passes by levels (LEVELS), as kernel B: an island leaves after the
     // first pass whose minimum separation (from 0) is >= -3 linearSlop; the minimum by LDS float
     // atomics (order-independent), the islands' flags in s_isolv
     for (int I = tid; I < nisl; I += BS) s_isolv[I] = 0;

@@ -607,7 +607,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     // More touching contacts than this kernel's LDS holds: the env's whole step runs here as the
     // spill step (HBM working set, flock_spill.hpp) from its untouched start-of-step state (only
     // scratch has been written so far), and kernels B and C skip it.
-    spill::step_env<OT, false>(P, B, e, cur, actions, obs, nbr_out, rew_out, coll_out, done_out, lds);
+    spill::step_env<OT, false, kFlock, 1, true>(P, B, e, cur, actions, obs, nbr_out, rew_out, coll_out, done_out, lds);
     if (tid == 0) B.x_nisl[e] = -1;
     return;
   }

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(1024) void tdm_step_wg(StepParams P, WorldBuffers B
   // ---- Box2D step of the living bodies, TDM.get_obs, done / winner --------------------------------
   // (above 1024 agents the pair records live in the slot's HBM: 48 B per body would not fit beside
   // the per-body arrays)
-  spill::step_env<OT, BPT == 1, kTdm, BPT>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out, lds, &TP,
+  spill::step_env<OT, BPT == 1, kTdm, BPT, true>(P, B, e, cur, actions, obs, nullptr, nullptr, nullptr, done_out, lds, &TP,
                                            &TB, F, slot);
 }
 
