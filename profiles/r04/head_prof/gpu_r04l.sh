@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 box session: per-kernel traces and SQ PMC at HEAD (tools/prof_r04.sh), phase cycles of the
+# Round-4 box session: per-kernel traces and SQ PMC at HEAD (profiles/r04/scripts/prof_r04.sh), phase cycles of the
 # closed loops and windows (stamp build of HEAD: ab/stamps_cand.so).
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -7,7 +7,7 @@ cd "$R"
 OUT=gpurun_out/${1:-r04l}
 mkdir -p "$OUT"
 st() { echo "$1 rc=$2" | tee -a "$OUT/status.txt"; [ "$2" -eq 0 ] || exit "$2"; }
-bash tools/prof_r04.sh "$(basename $OUT)/prof" > "$OUT/prof.log" 2>&1; st prof $?
+bash profiles/r04/scripts/prof_r04.sh "$(basename $OUT)/prof" > "$OUT/prof.log" 2>&1; st prof $?
 cd "$R"
 S="$R/ab/stamps_cand.so"
 MACM_STAMPS_LIB=$S timeout -k 10 200 python tools/phase_profile.py --envs 4096 --agents 64 --policy bots --warmup 300 --steps 10 --json $OUT/mbots.json > $OUT/mbots.log 2>&1; st mbots $?

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 per-kernel evidence for the level-step work: rocprofv3 kernel-trace stats of the C5 window,
 # the M and C3 closed loops, and SQ PMC passes of the C5 window (kernel B = flock_solve_wg).
-#   tools/prof_r04.sh OUTNAME [MACM_LIB path]
+#   profiles/r04/scripts/prof_r04.sh OUTNAME [MACM_LIB path]
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$R/gpurun_out/${1:-prof_r04}"
