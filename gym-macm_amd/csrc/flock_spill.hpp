@@ -28,6 +28,15 @@
 namespace macm {
 namespace spill {
 
+// The level steps' contact updates on packed (x, y) pairs, as kernel B (flock_step_wg.hip
+// kWgPacked): bit-identical, contraction off. -DMACM_WG_SCALAR restores the scalar form.
+#ifdef MACM_WG_SCALAR
+constexpr bool kLevelPacked = false;
+#else
+constexpr bool kLevelPacked = true;
+#endif
+typedef float lpf2 __attribute__((ext_vector_type(2)));
+
 
 constexpr int W = 64;
 
@@ -559,6 +568,40 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   uint32_t* g_hist = g_tab;      // [levels] counts, then positions
   auto level_body = [&](float4 r, float2& im, bool warm, float2& va, float2& vb) {
     const float nx = r.y, ny = r.z, tx = ny, ty = -nx;
+    if constexpr (kLevelPacked) {  // the same IEEE operations on (x, y) pairs (v_pk_mul / v_pk_add)
+      const lpf2 n = {nx, ny}, t = {ny, -nx};
+      lpf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
+      if (warm) {
+        const lpf2 Pv = im.x * n + im.y * t;
+        vA = vA - mA * Pv;
+        vB = vB + mB * Pv;
+      } else {
+        {
+          const lpf2 pr = (vB - vA) * t;
+          float lambda = kmass * (-(pr.x + pr.y));
+          const float maxf = friction * im.x;
+          const float ni = sclamp(im.y + lambda, -maxf, maxf);
+          lambda = ni - im.y;
+          im.y = ni;
+          const lpf2 Pv = lambda * t;
+          vA = vA - mA * Pv;
+          vB = vB + mB * Pv;
+        }
+        {
+          const lpf2 pr = (vB - vA) * n;
+          float lambda = -kmass * ((pr.x + pr.y) - 0.0f);
+          const float ni = fmaxf(im.x + lambda, 0.0f);
+          lambda = ni - im.x;
+          im.x = ni;
+          const lpf2 Pv = lambda * n;
+          vA = vA - mA * Pv;
+          vB = vB + mB * Pv;
+        }
+      }
+      va = make_float2(vA.x, vA.y);
+      vb = make_float2(vB.x, vB.y);
+      return;
+    }
     if (warm) {
       const float Px = im.x * nx + im.y * tx, Py = im.x * ny + im.y * ty;
       va.x = va.x - mA * Px;
@@ -853,6 +896,22 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
             float2* const pb = on ? pcb : pdd;
             float* const pm = on ? s_mins + I : pmd;
             float2 ca = *pa, cb = *pb;
+            if constexpr (kLevelPacked) {
+              const lpf2 cA = {ca.x, ca.y}, cB = {cb.x, cb.y};
+              const lpf2 d = cB - cA, d2 = d * d;
+              const float len = sqrt_rn(d2.x + d2.y);
+              const lpf2 n = len < kEps ? d : d * rcp_rn(len);  // b2Vec2::Normalize
+              const lpf2 pr = d * n;
+              const float sep = (pr.x + pr.y) - P.radius - P.radius;
+              const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+              const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
+              const lpf2 Pv = imp * n, nA = cA - mA * Pv, nB = cB + mB * Pv;
+              *pa = make_float2(nA.x, nA.y);
+              *pb = make_float2(nB.x, nB.y);
+              __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+              lsync();
+              continue;
+            }
             float nx = cb.x - ca.x, ny = cb.y - ca.y;
             normalize(nx, ny);
             const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - P.radius - P.radius;

@@ -1380,8 +1380,48 @@ namespace wg {
 
 // One Gauss-Seidel velocity constraint (b2ContactSolver::SolveVelocityConstraints, one point,
 // fixedRotation bodies): the fused kernel's arithmetic.
+// Kernel B's contact updates on packed (x, y) pairs (v_pk_mul_f32 / v_pk_add_f32, each lane of a pair
+// the scalar form's IEEE operation, no contraction: bit-identical). Round 5: C5 -1.2%, C3 even
+// (profiles/r05/abtests/wg_packed); -DMACM_WG_SCALAR restores the scalar form.
+#ifdef MACM_WG_SCALAR
+constexpr bool kWgPacked = false;
+#else
+constexpr bool kWgPacked = true;
+#endif
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void gs_velocity(float2& va, float2& vb, float nx, float ny, float& ln, float& ltg,
                                             float mA, float mB, float kmass, float friction) {
+  if constexpr (kWgPacked) {
+    pf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
+    const pf2 n = {nx, ny}, t = {ny, -nx};
+    {
+      const pf2 pr = (vB - vA) * t;
+      const float vt = pr.x + pr.y;
+      float lambda = kmass * (-vt);
+      const float maxf = friction * ln;
+      const float ni = sclamp(ltg + lambda, -maxf, maxf);
+      lambda = ni - ltg;
+      ltg = ni;
+      const pf2 Pv = lambda * t;
+      vA = vA - mA * Pv;
+      vB = vB + mB * Pv;
+    }
+    {
+      const pf2 pr = (vB - vA) * n;
+      const float vn = pr.x + pr.y;
+      float lambda = -kmass * (vn - 0.0f);
+      const float ni = smax(ln + lambda, 0.0f);
+      lambda = ni - ln;
+      ln = ni;
+      const pf2 Pv = lambda * n;
+      vA = vA - mA * Pv;
+      vB = vB + mB * Pv;
+    }
+    va = make_float2(vA.x, vA.y);
+    vb = make_float2(vB.x, vB.y);
+    return;
+  }
   const float tx = ny, ty = -nx;
   {
     const float dvx = vb.x - va.x, dvy = vb.y - va.y;
@@ -1410,6 +1450,16 @@ __device__ __forceinline__ void gs_velocity(float2& va, float2& vb, float nx, fl
 
 __device__ __forceinline__ void gs_warm(float2& va, float2& vb, float nx, float ny, float ln, float lt, float mA,
                                         float mB) {
+  if constexpr (kWgPacked) {
+    const pf2 n = {nx, ny}, t = {ny, -nx};
+    const pf2 Pv = ln * n + lt * t;
+    pf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
+    vA = vA - mA * Pv;
+    vB = vB + mB * Pv;
+    va = make_float2(vA.x, vA.y);
+    vb = make_float2(vB.x, vB.y);
+    return;
+  }
   const float tx = ny, ty = -nx;
   const float Px = ln * nx + lt * tx, Py = ln * ny + lt * ty;
   va.x = va.x - mA * Px;
@@ -1422,6 +1472,23 @@ __device__ __forceinline__ void gs_warm(float2& va, float2& vb, float nx, float 
 // KPOS: K = mA + mB is known to be > 0 (else the impulse is 0, b2ContactSolver's K > 0 test).
 template <bool KPOS = false>
 __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radius, float mA, float mB) {
+  if constexpr (kWgPacked) {
+    const pf2 cA = {ca.x, ca.y}, cB = {cb.x, cb.y};
+    const pf2 d = cB - cA;
+    const pf2 d2 = d * d;
+    const float len = sqrt_rn(d2.x + d2.y);
+    const pf2 n = len < kEps ? d : d * rcp_rn(len);
+    const pf2 pr = d * n;
+    const float sep = (pr.x + pr.y) - radius - radius;
+    const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
+    const float K = mA + mB;
+    const float imp = KPOS ? div_by_invariant(-Cc, K) : K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
+    const pf2 Pv = imp * n;
+    const pf2 nA = cA - mA * Pv, nB = cB + mB * Pv;
+    ca = make_float2(nA.x, nA.y);
+    cb = make_float2(nB.x, nB.y);
+    return sep;
+  }
   float nx = cb.x - ca.x, ny = cb.y - ca.y;
   normalize(nx, ny);
   const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
