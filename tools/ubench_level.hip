@@ -65,6 +65,21 @@ __device__ __forceinline__ float gsp(float2& ca, float2& cb, float radius, float
   return sep;
 }
 
+// packed position step (flock_step_wg.hip gs_position with kWgPacked, round 5)
+__device__ __forceinline__ float gsp_pk(f2v& ca, f2v& cb, float radius, float mA, float mB) {
+  const f2v d = cb - ca, d2 = d * d;
+  const float len = macm::sqrt_rn(d2.x + d2.y);
+  const f2v n = len < macm::kEps ? d : d * macm::rcp_rn(len);
+  const f2v pr = d * n;
+  const float sep = (pr.x + pr.y) - radius - radius;
+  const float Cc = __builtin_amdgcn_fmed3f(macm::kBaumgarte * (sep + macm::kLinearSlop), -macm::kMaxLinearCorrection, 0.0f);
+  const float imp = macm::div_by_invariant(-Cc, mA + mB);
+  const f2v P = imp * n;
+  ca = ca - mA * P;
+  cb = cb + mB * P;
+  return sep;
+}
+
 // packed form: the same IEEE ops on (x, y) pairs
 __device__ __forceinline__ void gsv_pk(f2v& va, f2v& vb, f2v n, f2v t, float& ln, float& ltg, float mA,
                                        float kmass, float friction) {
@@ -345,6 +360,39 @@ __global__ __launch_bounds__(64) void lvl(float2* out, long long* cyc, int nlev,
         pm = nm;
         wave_lds_sync();
       }
+    } else if constexpr (VAR == 16) {  // the packed position step's VALU chain alone (round 5)
+      f2v ca = *(f2v*)pa0, cb = {pa0->x + 0.9f, pa0->y + 0.1f};
+      float mn = 0.0f;
+      for (int lv = 0; lv < nlev; ++lv) {
+        const float sep = gsp_pk(ca, cb, 0.5f, mA, mA);
+        mn = fminf(mn, sep);
+      }
+      *(f2v*)pa0 = ca;
+      *(f2v*)pb0 = cb;
+      ln += mn;
+    } else if constexpr (VAR == 17) {  // V15 on packed pairs: kernel B's position level step (round 5)
+      float* const s_min = reinterpret_cast<float*>(s_v + 1024 + 32);
+      float* const pmi = reinterpret_cast<float*>(s_v + 1024) + (lane & 1);
+      float* const pmd = s_min + lane;
+      bool on = mylv == 0;
+      f2v* pa = (f2v*)(on ? pa0 : pd);
+      f2v* pb = (f2v*)(on ? pb0 : pd);
+      float* pm = on ? pmi : pmd;
+      for (int lv = 0; lv < nlev; ++lv) {
+        f2v ca = *pa, cb = *pb;
+        on = mylv == lv + 1;
+        f2v* const na = (f2v*)(on ? pa0 : pd);
+        f2v* const nb = (f2v*)(on ? pb0 : pd);
+        float* const nm = on ? pmi : pmd;
+        const float sep = gsp_pk(ca, cb, 0.5f, mA, mA);
+        *pa = ca;
+        *pb = cb;
+        __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        pa = na;
+        pb = nb;
+        pm = nm;
+        wave_lds_sync();
+      }
     } else if constexpr (VAR == 5) {  // packed VALU chain alone
       f2v va = *(f2v*)pa0, vb = *(f2v*)pb0;
       const f2v n = {nx, ny}, t = {ny, -nx};
@@ -411,6 +459,8 @@ int main() {
     run<14>("V14 position VALU chain only", blocks, nlev, iters);
     run<15>("V15 position, kernel B form", blocks, nlev, iters);
     run<5>("V5 packed VALU chain only", blocks, nlev, iters);
+    run<16>("V16 packed position chain", blocks, nlev, iters);
+    run<17>("V17 packed position, B form", blocks, nlev, iters);
     run<4>("V4 LDS round trip only", blocks, nlev, iters);
   }
   return 0;
