@@ -156,11 +156,13 @@ constexpr bool kIslPriority = false;
 #else
 constexpr bool kIslPriority = true;
 #endif
-// Kernel B: issue priority by the env's Gauss-Seidel depth. -DMACM_NO_SOLVE_PRIORITY: off.
-#ifdef MACM_NO_SOLVE_PRIORITY
-constexpr bool kSolvePriority = false;
-#else
+// Kernel B: issue priority by the env's Gauss-Seidel depth (round 4). Off since the packed level
+// steps (round 5: C3 window -1.3 / -1.7%, C3 closed loop -1.9%, C5 even; profiles/r05/abtests/
+// solve_priority). -DMACM_SOLVE_PRIORITY: on.
+#ifdef MACM_SOLVE_PRIORITY
 constexpr bool kSolvePriority = true;
+#else
+constexpr bool kSolvePriority = false;
 #endif
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
 #ifndef MACM_SERIAL_PREFETCH  // A/B knob: kernel A's one-thread island walks read the next edge ahead
