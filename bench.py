@@ -193,9 +193,55 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n):
+    """`--gpus N > 1` without a launcher: start torch.distributed.run with N ranks (this script, the same
+    arguments) as a CHILD process and return its exit code. Called before anything touches the GPU; the
+    parent never initialises the device and never re-execs itself. The child's stdout is this process's
+    (rank 0's JSON line goes straight through)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"--gpus {n} without a launcher: starting {n} ranks under torch.distributed.run")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args, rank, world):
+    """--dry-run (test hook, no device work): the launch, the process group, the shard split and the
+    counter all-reduce of a real run; every rank contributes its env count. Rank 0 prints the line with
+    value null. Lets the CPU suite check that `--gpus N` yields N ranks and N shards."""
+    from gym_macm import dist as gdist
+    strong = args.total_envs > 0
+    if strong:
+        e_off, E = gdist.strong_split(args.total_envs, world, rank)
+        shards = [list(gdist.strong_split(args.total_envs, world, r)) for r in range(world)]
+    else:
+        E = args.envs
+        e_off = gdist.env_offset(rank, E)
+        shards = [[gdist.env_offset(r, E), E] for r in range(world)]
+    envs = int(gdist.reduce_counters([E])[0])
+    ranks = int(gdist.reduce_counters([1])[0])
+    if rank == 0:
+        print(json.dumps({"metric": "dry run", "value": None, "n_gpus": world, "ranks_reporting": ranks,
+                          "dry_run": True, "config": {"envs_per_gpu": E, "total_envs": envs, "shards": shards,
+                                                      "first_env": e_off}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: the launcher's WORLD_SIZE, else 1. N > 1 without a "
+                         "launcher starts torch.distributed.run with N ranks as a child process")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="test hook: launch, process group, shards and the counter all-reduce only (no GPU)")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
@@ -241,6 +287,16 @@ def main():
     ap.add_argument("--dump-final", default=None,
                     help="test hook: every rank writes its final state and counters to PATH.rank<r>.npz")
     args = ap.parse_args()
+    # --gpus against the launcher, before any GPU call: the driver's scaling leg may
+    # run `python bench.py --gpus N` (no launcher) or `torchrun --nproc-per-node N bench.py --gpus N`
+    launcher = "WORLD_SIZE" in os.environ or "MASTER_ADDR" in os.environ
+    if args.gpus is not None and args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least one rank")
+    if not launcher and (args.gpus or 1) > 1:
+        sys.exit(_launch_ranks(args.gpus))
+    if launcher and args.gpus is not None and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE="
+                         f"{os.environ.get('WORLD_SIZE', '1')} ranks: they must agree")
     if args.traffic_json is None:
         args.traffic_json = os.path.join(REPO, "profiles", "pmc_flock_step.json" if args.env == "flock"
                                          else "pmc_tdm_step.json")
@@ -257,6 +313,13 @@ def main():
     # `torchrun --nproc-per-node 1` runs the RCCL branch (init, barriers, device all-reduces) on a
     # one-GPU box; a plain `python bench.py` (the driver's N=1 run) has no process group
     launched = world > 1 or "MASTER_ADDR" in os.environ
+    if args.dry_run:
+        if launched:
+            dist.init_process_group("gloo")
+        dry_run(args, rank, world)
+        if launched:
+            dist.destroy_process_group()
+        return
     if launched and args.dist_backend == "nccl":
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)

@@ -45,6 +45,25 @@ def test_two_ranks_sharded_bench(env, extra):
     assert d["value"] > 0 and d["ms_per_step"] > 0
 
 
+def test_gpus_2_without_launcher_runs_two_ranks():
+    """`python bench.py --gpus 2` with no launcher environment: bench.py starts the two
+    ranks itself as a child torch.distributed.run before touching the GPU; both step their shard on
+    the box's one GPU (gloo counters) and the line reports the whole job."""
+    E, K, W = 128, 4, 2
+    env_vars = {k: v for k, v in os.environ.items()
+                if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env_vars.update(HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", str(K), "--warmup", str(W),
+           "--envs", str(E), "--dist-backend", "gloo", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env_vars, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["shards"] == [[0, E], [E, E]]
+    assert d["counters"]["agent_steps"] == 2 * E * d["config"]["n_agents"] * K
+
+
 def _run(cmd):
     env_vars = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env_vars, cwd=REPO)
