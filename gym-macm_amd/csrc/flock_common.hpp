@@ -175,6 +175,7 @@ __device__ __forceinline__ int ld_wt(const int* p) {
 struct HandoffStream {
   hipStream_t stream;
   hipEvent_t done;
+  hipEvent_t pre_b;  // recorded on the caller's stream just before kernel B: the watcher's stream waits on it
   unsigned long long* b_started;
   unsigned int* ctr;
   unsigned long long* q;

@@ -2657,16 +2657,25 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
       hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL, true>), dim3(H), dim3(W), 0, solo->stream, A);
       // the watcher (flock_step_wg.hip wait_count) is launched only behind a solo launch that was
       // accepted: its H waves start (they wait for nothing) and end it
-      bool ok = hipPeekAtLastError() == hipSuccess;
-      if (ok) {
-        solo->expected += (unsigned long long)H;
-        ok = launch_wait_count(solo->started, solo->expected, B.host_status, s) == hipSuccess;
-      }
       A.sched_off = H;
-      if (ok) hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs - H), dim3(W), 0, s, A);
-      // joined whatever happened above (no unjoined work on the solo stream)
-      (void)hipEventRecord(solo->join, solo->stream);
-      (void)hipStreamWaitEvent(s, solo->join, 0);
+      if (hipPeekAtLastError() != hipSuccess) {  // solo launch refused: the error stays for the caller
+        (void)hipEventRecord(solo->join, solo->stream);
+        (void)hipStreamWaitEvent(s, solo->join, 0);
+        return;
+      }
+      solo->expected += (unsigned long long)H;
+      // a watcher that cannot be launched (its error is consumed here): the ordinary instance runs
+      // after the solo one instead of beside it, so every env is still stepped
+      const bool watched = launch_wait_count(solo->started, solo->expected, B.host_status, s) == hipSuccess;
+      if (!watched) {
+        (void)hipEventRecord(solo->join, solo->stream);
+        (void)hipStreamWaitEvent(s, solo->join, 0);
+      }
+      hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs - H), dim3(W), 0, s, A);
+      if (watched) {  // joined (no unjoined work on the solo stream)
+        (void)hipEventRecord(solo->join, solo->stream);
+        (void)hipStreamWaitEvent(s, solo->join, 0);
+      }
     }
     return;
   }

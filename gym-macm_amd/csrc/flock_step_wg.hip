@@ -2039,7 +2039,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   extern __shared__ __align__(16) unsigned char lds[];
   // in kernel B's finish order (the block scan's scratch words carry the env to the block)
   const int e = H.q ? handoff_take(B, H, reinterpret_cast<int*>(lds + wg_layout_c(P.n_agents).scan)) : wg_env(B);
-  if (e < 0) return;
+  if (e < 0) {
+    // this block cannot know which env it missed: every env carries the bit, so
+    // macm_world_status shows the world's results as invalid wherever they were read
+    for (int i = threadIdx.x; i < P.n_envs; i += blockDim.x) atomicOr(&B.status[i], (int)MACM_ST_HANDOFF);
+    return;
+  }
   const int tid = threadIdx.x;
   const int BS = blockDim.x;
   const int N = P.n_agents;
@@ -2658,10 +2663,19 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   else
     hipLaunchKernelGGL(flock_step_wg_a<float>, grid, block, la, s, P, B, cur, tcap, actions, (float*)obs, nbr, rew,
                        coll, done);
+  // the watcher's clock starts only once kernel B's dependencies have finished: HS->stream
+  // waits for this event, recorded on `s` right before B, so work queued on the caller's stream ahead
+  // of the step (a policy update, another world's launches) cannot run the watcher out of time
+  bool pre_b = false;
+  auto record_pre_b = [&]() {
+    if (H.q) pre_b = hipEventRecord(HS->pre_b, s) == hipSuccess;
+  };
   if (fuse_dfs()) {
+    record_pre_b();
     hipLaunchKernelGGL(flock_solve_wg<true>, grid, dim3(64), wg_fused_lds(N, tcap), s, P, B, tcap, H);
   } else {
     if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
+    record_pre_b();
     if (solve_pairs(P))
       hipLaunchKernelGGL(flock_solve_wg_pair, dim3((P.n_envs + 1) / 2), dim3(64), 2 * wg_solve_lds_env(N), s, P, B,
                          tcap, H);
@@ -2679,7 +2693,9 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   hipError_t e = hipPeekAtLastError();
   if (e != hipSuccess) return e;  // B not launched: nothing on the second stream, no count to wait for
   HS->expected += (unsigned long long)P.n_envs;
-  if (launch_wait_count(HS->b_started, HS->expected, B.host_status, HS->stream) != hipSuccess) {
+  if (!pre_b || hipStreamWaitEvent(HS->stream, HS->pre_b, 0) != hipSuccess ||
+      launch_wait_count(HS->b_started, HS->expected, B.host_status, HS->stream) != hipSuccess) {
+    (void)hipGetLastError();
     launch_c(s);
     return hipGetLastError();
   }

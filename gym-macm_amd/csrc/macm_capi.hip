@@ -197,6 +197,7 @@ static void free_handoff(HandoffStream*& h) {
   if (!h) return;
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->done) (void)hipEventDestroy(h->done);
+  if (h->pre_b) (void)hipEventDestroy(h->pre_b);
   if (h->b_started) (void)hipFree(h->b_started);
   if (h->ctr) (void)hipFree(h->ctr);
   if (h->q) (void)hipFree(h->q);
@@ -651,7 +652,8 @@ static int overflow_error(uint32_t st) {
   if (st & MACM_ST_TOUCH_OVERFLOW) what += " touching-contact capacity;";
   if (st & MACM_ST_DEGREE_OVERFLOW) what += " per-body contact capacity;";
   if (st & MACM_ST_SPILL_WAIT) what += " spill working-set pool (a dense env waited ~1 s for a slot);";
-  if (st & MACM_ST_HANDOFF) what += " B -> C handoff (a kernel-C block waited ~1 s for an env);";
+  if (st & MACM_ST_HANDOFF) what += " B -> C handoff (kernel B's waves did not all start, or a kernel-C block found no env, within ~1 s; every "
+                                        "env is marked: rebuild the world or reset it);";
   return fail(MACM_E_OVERFLOW, "an env outgrew its" + what +
                                    " the results since that step are not the reference's (status bits " +
                                    std::to_string(st) + "; reset, place or set_state clears them)");
@@ -672,6 +674,7 @@ static HandoffStream* handoff_for(macm_world* w) {
   HandoffStream* h = new HandoffStream{};
   bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&h->done, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&h->pre_b, hipEventDisableTiming) == hipSuccess &&
             hipMalloc(&h->b_started, sizeof(unsigned long long)) == hipSuccess &&
             hipMalloc(&h->ctr, 2 * sizeof(unsigned int)) == hipSuccess &&
             hipMalloc(&h->q, (size_t)w->P.n_envs * sizeof(unsigned long long)) == hipSuccess;

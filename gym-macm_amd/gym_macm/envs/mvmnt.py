@@ -10,9 +10,10 @@ the global RNG in the same state.
 
 Observations are computed in float64 on the GPU (config obs_f64); rewards are the
 reference's Python types (int -1/0/1 in binary mode, float in linear mode).
-Documented differences: ``reset()`` works (the reference's raises AttributeError,
-:224-233), and iteration order of the rewards dict follows agent id (dict
-equality with the reference's holds; the reference inserts contact agents first).
+The rewards dict keeps the reference's insertion order (:160-179): the two agents of
+every contact in ``world.contacts`` order first (fixture A, then B), then the others
+in ascending id (``reward_key_order``). Documented difference: ``reset()`` works (the
+reference's raises AttributeError, :224-233).
 """
 from __future__ import annotations
 
@@ -24,6 +25,30 @@ import torch
 from gym_macm import spaces
 from gym_macm.settings import flockSettings, to_config
 from gym_macm.world import World
+
+
+def reward_key_order(prev_ab, next_ab, n_agents):
+    """The key order of the reference's rewards dict after a step (mvmnt.py:160-179): -1 goes in
+    for ``contact.fixtureA`` then ``contact.fixtureB`` of every contact in ``world.contacts`` order,
+    then every other agent in ascending id.
+
+    ``world.contacts`` at that point is Box2D's list after the step: the contacts created by the
+    step's closing FindNewContacts, prepended (``b2ContactManager::AddPair``), ahead of the contacts
+    that survived the step's Collide in their order. The world keeps an ordered list per env of the
+    contacts that survive the NEXT Collide (entries a | b << 16, fixture A in the low half): before the
+    step (``prev_ab``) that is exactly what the step's Collide keeps; after it (``next_ab``) it is the
+    new contacts ahead of the survivors that still overlap. So ``world.contacts`` = the entries of
+    ``next_ab`` absent from ``prev_ab``, in order, followed by ``prev_ab``."""
+    prev = [int(x) for x in prev_ab]
+    old = set(prev)
+    order = dict()
+    for x in [int(x) for x in next_ab if int(x) not in old] + prev:
+        order.setdefault(x & 0xFFFF, None)
+        order.setdefault(x >> 16, None)
+    n_contact = len(order)
+    for i in range(n_agents):
+        order.setdefault(i, None)
+    return list(order), n_contact
 
 
 class Color(object):
@@ -146,6 +171,7 @@ class Flock(object):
         self._N = N
         self._cache = None
         obs, nbr = self.world.place(pos[None], ang[None], tg[None])
+        self._ab = self.world.contact_list(0)  # world.contacts order as of the next step's start
         self.create_space()
         self.create_space_flag = False
         self.obs = self._obs_dict(obs, nbr)
@@ -194,9 +220,13 @@ class Flock(object):
         obs = obs_t[0].numpy()
         rew = rew_t[0].numpy()
         half = obs.shape[1] // 2
+        nxt = self.world.contact_list(0)
+        keys, n_contact = reward_key_order(self._ab, nxt, self._N)
+        self._ab = nxt
+        if n_contact != int((rew == -1.0).sum()) or any(rew[i] != -1.0 for i in keys[:n_contact]):
+            raise RuntimeError("the contact list and the step's -1 rewards disagree (a capacity overflowed?)")
         rewards = {}
-        for agent in self.agents:
-            i = agent.id
+        for i in keys:
             if rew[i] == -1.0:
                 rewards[i] = -1
             elif self.settings.reward_mode == "linear":
@@ -243,6 +273,7 @@ class Flock(object):
             pos[i] = (x, y)
         tg = np.array([[t.x, t.y] for t in self.targets], np.float32)
         obs, nbr = self.world.place(pos[None], ang[None], tg[None])
+        self._ab = self.world.contact_list(0)
         self._cache = None
         self.create_space()
         self.obs = self._obs_dict(obs, nbr)

@@ -304,6 +304,18 @@ class World:
         s["contact_imp"][idx] = 0
         return s
 
+    def contact_list(self, e: int = 0) -> np.ndarray:
+        """Env e's ordered contact list (uint32 a | b << 16, world-list order: the contacts that
+        survive the next Collide, newest first), read without the rest of the state."""
+        cnt = np.zeros((self.E,), np.int32)
+        _abi.check(self.L.macm_world_get_state(self.h, ctypes.byref(self._state_struct({"contact_count": cnt}, 0)),
+                                               self._stream()), "macm_world_get_state")
+        stride = max(1, int(cnt.max(initial=0)))
+        ab = np.zeros((self.E, stride), np.uint32)
+        _abi.check(self.L.macm_world_get_state(self.h, ctypes.byref(self._state_struct(
+            {"contact_count": cnt, "contact_ab": ab}, stride)), self._stream()), "macm_world_get_state")
+        return ab[e, :int(cnt[e])].copy()
+
     def set_state(self, s: dict) -> None:
         """Inject a state (get_state's layout; the contact rows may have any length >= the counts,
         e.g. another world's max_contacts). A list longer than this world's capacity raises

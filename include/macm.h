@@ -72,16 +72,19 @@ enum {
   MACM_ST_INVALID_ACTION = 8,   /* validate_actions: an action outside the action space  */
   MACM_ST_SPILL_WAIT = 16,      /* a dense env found no free spill working-set slot for ~1 s
                                    (a pooled world: fewer slots than envs) and was not stepped */
-  MACM_ST_HANDOFF = 32          /* workgroup path: a kernel-C block waited ~1 s for kernel B to hand
-                                   it an env (never expected: B's waves wait for nothing) and
-                                   skipped it; results since then are invalid (ABI 8)          */
+  MACM_ST_HANDOFF = 32          /* workgroup path: kernel B's waves did not all start within ~1 s
+                                   of B's dependencies finishing, or a kernel-C block waited ~1 s
+                                   for B to hand it an env and skipped it (never expected: B's
+                                   waves wait for nothing). Every env of the world carries the bit
+                                   (the skipped env is unknown); results since then are invalid
+                                   (ABI 8)                                                      */
 };
 
 /* macm_world_set_debug / macm_tdm_set_debug flags (test hooks; 0 = product behaviour; TDM takes
  * FORCE_SPILL, SPILL_POOL and SPILL_FAIL). */
 enum {
   MACM_DEBUG_FORCE_SPILL = 1,     /* every env takes the spill step (parity tests of that path)  */
-  MACM_DEBUG_SWEEP_CELLS = 2,     /* N > 64: pair sweep over strip cells at any N (else N >= 512) */
+  MACM_DEBUG_SWEEP_CELLS = 2,     /* N > 64: pair sweep over strip cells at any N (else N >= 256) */
   MACM_DEBUG_SWEEP_ALL_PAIRS = 4, /* N > 64: all-pairs pair sweep at any N                        */
   MACM_DEBUG_SPILL_POOL = 8,      /* the spill working set as a pool of (flags >> 8) slots, at most
                                      the slots allocated (pooled-slot tests at small E)            */
@@ -133,7 +136,7 @@ typedef struct macm_config {
 typedef struct macm_tdm_config {
   int32_t n_teams;              /* len(n_agents)                      combat.py:70-73 */
   int32_t team_size[4];         /* n_agents[i]                                        */
-  int32_t n_agents;             /* sum(n_agents) (<= 1024; > 64: the workgroup step)   */
+  int32_t n_agents;             /* sum(n_agents) (<= 4096; > 64: the workgroup step)   */
   int32_t velocity_iterations;  /* 8                                                  */
   int32_t position_iterations;  /* 3                                                  */
   int32_t warm_starting;        /* 1                                                  */
@@ -434,7 +437,7 @@ typedef struct macm_tdm macm_tdm;
 int macm_tdm_config_default(macm_tdm_config* cfg);
 
 /*
- * Create E TDM envs (N = sum(team_size) <= 1024 agents; MACM_E_UNSUPPORTED above). Replaces
+ * Create E TDM envs (N = sum(team_size) <= 4096 agents; MACM_E_UNSUPPORTED above). Replaces
  * TDM.__init__'s world + body creation (combat.py:61-102). State is undefined until reset/place.
  * N <= 64: one wave per env (the fast kernel, its spill step for crowded envs); N > 64: one
  * workgroup per env (tdm_step_wg.hip: the action loop, then the spill step's physics with its HBM

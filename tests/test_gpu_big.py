@@ -1,7 +1,7 @@
 """Worlds above 1024 agents per env: the reference steps any sum(n_agents)
 (gym_macm/envs/mvmnt.py:61) in one uncapped b2World. Here an env of 1024 < N <= 4096 agents is one
 workgroup of 1024 threads with up to 4 bodies per thread (csrc/flock_big.hip: the spill step, its
-HBM working set, the island DFS and each island's Gauss-Seidel serial). Bar: bit-exact against the
+HBM working set, the island DFS, and Gauss-Seidel levels stepped by one wave). Bar: bit-exact against the
 oracle (oracle/, the C restatement of mvmnt.py over b2lite) in state, contact lists, rewards,
 neighbour ids, done, reward sums, and the observation within the f32 tolerance of tests/parity.py,
 sparse and dense, through the tensor API (step, rollout, trajectory, per-env resets) and the dict API.

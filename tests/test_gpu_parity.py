@@ -195,6 +195,8 @@ def test_dropin_flock_matches_reference_goldens(name):
             acts = {i: g["actions"][t][i].astype(np.int64) for i in range(N)}
         obs, rewards = env.step(acts)
         assert [rewards[i] for i in range(N)] == list(g["reward"][t]), f"rewards step {t}"
+        # the reference's insertion order (contact agents first, world.contacts order)
+        assert list(rewards.keys()) == [int(x) for x in g["reward_order"][t]], f"reward dict order step {t}"
         nbr = np.array([obs[i]["nodes"][0]["id"] for i in range(N)])
         np.testing.assert_array_equal(nbr, g["nbr"][t], err_msg=f"nbr step {t}")
         pos = np.array([np.concatenate([obs[i]["nodes"][0]["position"], obs[i]["nodes"][1]["position"]])

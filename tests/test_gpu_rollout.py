@@ -295,6 +295,39 @@ def test_handoff_equals_plain_workgroup_step(monkeypatch, E, N, K, kw):
     assert ta == tb and b.status() == 0
 
 
+def test_handoff_after_a_long_backlog_on_the_callers_stream(monkeypatch):
+    """the handoff's watcher (kernel C's stream) must start its ~1 s clock only when kernel
+    B's dependencies have finished, not when its own stream is idle. A > 1.5 s spin kernel queued on the
+    caller's stream ahead of every handoff step (a PPO update between rollouts, say) must leave the
+    steps' status 0 and their results equal to the plain launch order's."""
+    import time
+    E, N, K = 64, 100, 2
+    monkeypatch.setenv("MACM_HANDOFF", "0")
+    a = FlockVec(E, n_agents=[N], seed=41, device="cuda:0")
+    monkeypatch.setenv("MACM_HANDOFF", "1")
+    b = FlockVec(E, n_agents=[N], seed=41, device="cuda:0")
+    acts = flock_actions(K, E, N, 23)
+    # calibrate torch's spin kernel (its clock's rate is the device's) to ~2 s
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(1000)
+    e0.record()
+    torch.cuda._sleep(10 ** 7)
+    e1.record()
+    torch.cuda.synchronize()
+    cycles = int(10 ** 7 * 2000.0 / max(e0.elapsed_time(e1), 1e-3))
+    for k in range(K):
+        a.step(acts[k])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        torch.cuda._sleep(cycles)  # the backlog, on the stream the world steps on
+        b.step(acts[k])
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 > 1.5, "the backlog kernel did not spin long enough to test this"
+    assert b.world.uses_handoff()
+    assert b.status() == 0, b.status()
+    assert_same(a, b, "handoff behind a backlog")
+
+
 @pytest.mark.parametrize("E,N,K,kw", [
     (6, 1024, 6, {}),                                   # C5-shaped: every env takes the DFS kernel's walk
     (12, 300, 8, {"start_spread": 8}),                  # dense and sparse envs mixed

@@ -67,3 +67,36 @@ def test_vectorised_flock_bot_matches_recorded_reference_actions():
         np.testing.assert_array_equal(flock_bot(obs), g["actions"], err_msg=name)
         n += g["actions"].shape[0] * g["actions"].shape[1]
     assert n > 5000
+
+
+@pytest.mark.parametrize("name", goldens.names())
+def test_reward_dict_order_matches_reference(name):
+    """The rewards dict's key order (mvmnt.py:160-179: world.contacts' fixture A then B, then the rest in
+    ascending id) as the reference produced it (golden `reward_order`), two ways:
+    - the oracle's own world list (b2lite's m_contactList order, fo_contacts) gives it directly;
+    - the drop-in's reconstruction (gym_macm.envs.mvmnt.reward_key_order) from the ordered per-env lists
+      the product keeps (the oracle's export of the same layout, before and after each step) gives it too.
+    """
+    from gym_macm.envs.mvmnt import reward_key_order
+    g = goldens.load(name)
+    cfg, tidx = goldens.config(g)
+    N = cfg.n_agents
+    C = N * (N - 1) // 2
+    orc = OracleFlock(cfg, tidx, 1, g["meta"]["seed"])
+    prev = orc.get_state(C)
+    prev_ab = prev["contact_ab"][0, :prev["contact_count"][0]].copy()
+    for t in range(g["meta"]["steps"]):
+        orc.step(g["actions"][t][None])
+        want = [int(x) for x in g["reward_order"][t]]
+        world = dict()
+        for a, b, _touching in orc.contacts(0):
+            world.setdefault(int(a), None)
+            world.setdefault(int(b), None)
+        direct = list(world) + [i for i in range(N) if i not in world]
+        assert direct == want, f"oracle world list order, step {t}"
+        s = orc.get_state(C)
+        nxt = s["contact_ab"][0, :s["contact_count"][0]].copy()
+        keys, n_contact = reward_key_order(prev_ab, nxt, N)
+        assert keys == want, f"reconstructed order, step {t}"
+        assert n_contact == int((g["reward"][t] == -1).sum())
+        prev_ab = nxt
