@@ -81,6 +81,47 @@ def test_headline_rollout_launch_all_envs_match_oracle():
     assert tot[1] > 0
 
 
+def test_headline_trajectory_launch_all_envs_match_oracle():
+    """The driver's exact timed launch (bench.py's default `--outputs trajectory`: one
+    macm_world_rollout_traj of K = 20 steps after the W = 5-step warm-up rollout), pinned row by row:
+    trajectory row k (rewards, neighbour ids, collision flags, done bit-exact; observations <= 1 ulp of
+    the oracle's float64 rounded to float32) equals the oracle's step W + k over all 4096 envs, and the
+    state after the launch, the counters and the reward sums equal the oracle's (VERDICT r05 #4)."""
+    vec = FlockVec(E, n_agents=[N], seed=SEED, device="cuda:0")
+    gen = torch.Generator(device="cuda:0")
+    gen.manual_seed(SEED + 1)  # bench.py, rank 0
+    acts = torch.randint(0, 3, (W + K, E, N, 3), dtype=torch.uint8, device="cuda:0", generator=gen)
+    sh = torch.cuda.current_stream().cuda_stream
+    traj = vec.world.trajectory_buffers(K)
+    vec.world.rollout_raw(acts.data_ptr(), W, sh)
+    torch.cuda.synchronize()
+    vec.world.reset_counters()
+    vec.world.rollout_traj_raw(acts[W:].data_ptr(), K, traj, sh)  # bench.py's timed call
+    torch.cuda.synchronize()
+    a = acts.cpu().numpy()
+    rows = {k: v.cpu().numpy() for k, v in traj.items()}
+    orc = oracle()
+    tot = np.zeros(4, np.int64)
+    rs = np.zeros(E, np.float64)
+    for k in range(W + K):
+        r = orc.step(a[k], n_threads=THREADS)
+        if k < W:
+            continue
+        j = k - W
+        np.testing.assert_array_equal(rows["reward"][j], r["reward"].astype(np.float32), err_msg=f"reward row {j}")
+        np.testing.assert_array_equal(rows["nbr_id"][j], r["nbr_id"], err_msg=f"nbr_id row {j}")
+        np.testing.assert_array_equal(rows["collided"][j], r["collided"], err_msg=f"collided row {j}")
+        np.testing.assert_array_equal(rows["done"][j], r["done"], err_msg=f"done row {j}")
+        f32_obs_mismatch(rows["obs"][j], r["obs"])
+        tot += [E * N, int(r["collided"].sum()), int((r["reward"] > 0).sum()), int(r["done"].sum())]
+        rs += pairwise_reward_sum(r["reward"])
+    assert vec.status() == 0
+    assert_state_equal(vec.get_state(), orc.get_state(vec.world.C), "after the trajectory launch")
+    np.testing.assert_array_equal(vec.counters(), tot)
+    check_reward_sums(vec, rs)
+    assert tot[1] > 0
+
+
 def test_headline_closed_loop_launch_all_envs_match_oracle():
     vec = FlockVec(E, n_agents=[N], seed=SEED, device="cuda:0")
     loop = flock_actions(vec.obs)
