@@ -220,6 +220,10 @@ struct TdmBuffers {
   double* health_out;    // [E, N]
   uint8_t* alive_out;    // [E, N]
   int32_t* winner_out;   // [E]
+  // the split observation (round 6, tdm_obs_snap.hip): non-NULL, the step writes each agent's pose
+  // after the step here, (x, y, angle, alive ? 1 : 0), instead of the observation, and
+  // tdm_observe_snap writes the observation and mask from it in a launch of its own
+  float4* snap_out;      // [E, N]
 };
 
 __host__ __device__ inline int tdm_team_of(const TdmParams& T, int i) {

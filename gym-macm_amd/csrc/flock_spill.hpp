@@ -1154,7 +1154,13 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
     release_slot(B, slot);
     __syncthreads();
     const size_t rows = (size_t)e * N * (N - 1);
-    if (wide && kTdmBlockObsLinear)
+    if (TB->snap_out) {  // the split observation (tdm_obs_snap.hip): the pose snapshot instead
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        const int i = tid + j * BS;
+        if (i < N) TB->snap_out[(size_t)e * N + i] = make_float4(s_c[i].x, s_c[i].y, s_slp[i], act[j] ? 1.0f : 0.0f);
+      }
+    } else if (wide && kTdmBlockObsLinear)
       tdm_obs_block_linear<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid,
                                BS, s_alivew, *TP, s_c, s_slp);
     else if (wide)

@@ -2360,6 +2360,12 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     }
     s_ang[lane] = ang;
     __syncthreads();
+    if (TB.snap_out) {  // the split observation: the pose snapshot tdm_observe_snap observes
+      if (lane < N) {
+        const float2 c = s_c[lane];
+        TB.snap_out[ag] = make_float4(c.x, c.y, ang, act ? 1.0f : 0.0f);
+      }
+    } else {
     const size_t rows = (size_t)e * N * (N - 1);
     OT* const obs_e = obs ? obs + rows * 4 : nullptr;
     uint8_t* const mask_e = TB.mask_out ? TB.mask_out + rows : nullptr;
@@ -2380,6 +2386,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         tdm_obs_pairs_smask<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<uint8_t*>(&s_pool));
       else
         MACM_TDM_OBS<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang);
+    }
     }
   }
   STAMP(12);
@@ -2595,6 +2602,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : 4)
       TB.health_out = traj_row(TB.health_out, kr, EN);
       TB.alive_out = traj_row(TB.alive_out, kr, EN);
       TB.winner_out = traj_row(TB.winner_out, kr, (size_t)A.P.n_envs);
+      TB.snap_out = traj_row(TB.snap_out, kr, EN);
     }
     const size_t abytes = MODE == kTdm ? 4 : 3;  // closed loop: uint8 actions per agent
     uint8_t* const pol_in = A.policy_act ? A.policy_act + kr * EN * abytes : nullptr;

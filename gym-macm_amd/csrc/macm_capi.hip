@@ -49,6 +49,8 @@ hipError_t launch_tdm_init_wg(const StepParams& P, const WorldBuffers& B, const 
                               int cur, void* obs, bool obs_f64, const uint8_t* mask, hipStream_t s);
 hipError_t launch_tdm_observe_wg(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                  const TdmBuffers& TB, void* obs, bool obs_f64, hipStream_t s);
+hipError_t launch_tdm_observe_snap(const TdmParams& TP, int N, size_t rows, const float4* snap, void* obs,
+                                   bool obs_f64, uint8_t* mask, hipStream_t s);
 hipError_t tdm_wg_configure(int N);
 int tdm_wg_step_lds(int N);
 int tdm_wg_obs_lds(int N);
@@ -122,6 +124,12 @@ struct macm_tdm {
   unsigned long long* bad = nullptr;
   int slots_alloc = 0;  // as macm_world
   int pool0 = 0;
+  // the split observation (tdm_obs_snap.hip, tdm_split_obs): pose snapshots in two halves of
+  // snap_rows (step, env) rows each, the observation stream and the chunk events (created on first use)
+  float4* snap = nullptr;
+  size_t snap_rows = 0;
+  hipStream_t obs_stream = nullptr;
+  hipEvent_t ev_phys[2] = {nullptr, nullptr}, ev_obs[2] = {nullptr, nullptr};
 };
 
 static thread_local std::string g_last_error;
@@ -1176,6 +1184,15 @@ int macm_tdm_config_default(macm_tdm_config* c) {
 static void free_tdm(macm_tdm* w) {
   for (void* p : w->allocs) (void)hipFree(p);
   w->allocs.clear();
+  if (w->snap) (void)hipFree(w->snap);
+  w->snap = nullptr;
+  if (w->obs_stream) (void)hipStreamDestroy(w->obs_stream);
+  w->obs_stream = nullptr;
+  for (int b = 0; b < 2; ++b) {
+    if (w->ev_phys[b]) (void)hipEventDestroy(w->ev_phys[b]);
+    if (w->ev_obs[b]) (void)hipEventDestroy(w->ev_obs[b]);
+    w->ev_phys[b] = w->ev_obs[b] = nullptr;
+  }
   if (w->hstat) (void)hipHostFree(w->hstat);
   w->hstat = nullptr;
 }
@@ -1283,7 +1300,11 @@ int macm_tdm_create(const macm_tdm_config* cfg, int32_t n_envs, int32_t device, 
       (rc = dalloc(A, &B.sp_cim, (size_t)SL * C)) || (rc = dalloc(A, &B.sp_lam, (size_t)SL * C)) ||
       (rc = dalloc(A, (float4**)&B.sp_rec, (size_t)SL * N * 3)) ||  // 48-B records
       (SL < n_envs && (rc = dalloc(A, &B.sp_lock, (size_t)SL))) || (rc = dalloc(A, &B.spill_count, E)) ||
-      (w->wave && (rc = dalloc(A, &B.sched, (size_t)E)))) {
+      (w->wave && (rc = dalloc(A, &B.sched, (size_t)E)))
+#ifdef MACM_STAMPS
+      || (rc = dalloc(A, &B.stamps, E * 32))
+#endif
+  ) {
     free_tdm(w);
     delete w;
     return rc;
@@ -1417,6 +1438,61 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
   return resync_host_status(w->hstat, w->B.status, w->P.n_envs, s);
 }
 
+// The split observation (round 6, tdm_obs_snap.hip). The wave kernel (N <= 64) observes on its one
+// wave after the physics: 55% of its cycles at 2 x 16 (tools/tdm_phase.py). With fewer envs than
+// SIMDs (BASELINE C4's per-GPU shard: 512 envs, 0.5 waves per SIMD) that observation is one wave's
+// latency chain. Split, the step writes pose snapshots and tdm_observe_snap observes every
+// (step, env) row with a workgroup of its own; a trajectory rollout runs in chunks of
+// kTdmSplitChunk steps, each chunk's observation on a second stream beside the next chunk's physics.
+// Bit-identical either way. Measured (profiles/r06/split/, 2 x 16, one box): 512 envs 13.2 -> 11.6 us
+// per step at steady state, 18.8 -> 18.1 us in the driver's window; 1024 envs even; 2048 and 4096 envs
+// slower (26 / 50 us against 20 / 28: with every SIMD busy the observation kernel only competes with
+// the physics). The physics alone takes ~11 us per step at 512 envs (rocprof: the chunk launches),
+// one wave's latency chain, which bounds the shard whatever the observation costs.
+// Below kTdmSplitMaxEnvs envs by default; MACM_TDM_SPLIT_OBS=0/1 overrides
+// (tests, A/B). The closed loop (the bots read each step's observation inside the launch) and the
+// workgroup step (N > 64) keep the fused form.
+#ifndef MACM_TDM_SPLIT_MAX_ENVS
+#define MACM_TDM_SPLIT_MAX_ENVS 1024
+#endif
+static constexpr int kTdmSplitMaxEnvs = MACM_TDM_SPLIT_MAX_ENVS;
+#ifndef MACM_TDM_SPLIT_CHUNK
+#define MACM_TDM_SPLIT_CHUNK 8
+#endif
+static constexpr int kTdmSplitChunk = MACM_TDM_SPLIT_CHUNK;
+
+static bool tdm_split_obs(const macm_tdm* w) {
+  if (!w->wave) return false;
+  const char* v = getenv("MACM_TDM_SPLIT_OBS");
+  return v ? atoi(v) != 0 : w->P.n_envs < kTdmSplitMaxEnvs;
+}
+
+// snapshot halves of at least `rows` rows each (grown on demand; the caller's stream has finished
+// every earlier use: each split call ends with the stream joined to the observation stream)
+static int tdm_split_buffers(macm_tdm* w, size_t rows, hipStream_t s) {
+  if (!w->obs_stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&w->obs_stream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_phys[b], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_obs[b], hipEventDisableTiming));
+    }
+  }
+  if (rows > w->snap_rows) {
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipStreamSynchronize(w->obs_stream));
+    if (w->snap) HIP_TRY(hipFree(w->snap));
+    w->snap = nullptr;
+    w->snap_rows = 0;
+    if (hipMalloc(&w->snap, 2 * rows * (size_t)w->P.n_agents * sizeof(float4)) != hipSuccess) {
+      (void)hipGetLastError();
+      w->snap = nullptr;
+      return fail(MACM_E_OOM, "hipMalloc (split observation snapshots)");
+    }
+    w->snap_rows = rows;
+  }
+  return MACM_OK;
+}
+
 int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out, void* stream) {
   if (!w || !actions) return fail(MACM_E_INVALID, "tdm/actions is NULL");
   if (const uint32_t st = read_host_status(w->hstat)) return overflow_error(st);
@@ -1425,10 +1501,72 @@ int macm_tdm_step(macm_tdm* w, const void* actions, const macm_tdm_outputs* out,
     const int rc = check_actions(w->bad, actions, 2, w->TB.alive, w->P.n_envs, w->P.n_agents, (hipStream_t)stream);
     if (rc) return rc;
   }
-  const TdmBuffers TB = tdm_with_outputs(w, out);
-  HIP_TRY(tdm_launch_step(w, TB, w->cur, actions, out ? out->obs : nullptr, out ? out->done : nullptr,
-                          (hipStream_t)stream));
+  TdmBuffers TB = tdm_with_outputs(w, out);
+  hipStream_t s = (hipStream_t)stream;
+  void* obs = out ? out->obs : nullptr;
+  if ((obs || TB.mask_out) && tdm_split_obs(w)) {
+    const int rc = tdm_split_buffers(w, (size_t)w->P.n_envs, s);
+    if (rc) return rc;
+    TB.snap_out = w->snap;
+    HIP_TRY(tdm_launch_step(w, TB, w->cur, actions, nullptr, out->done, s));
+    w->cur ^= 1;
+    HIP_TRY(launch_tdm_observe_snap(w->TP, w->P.n_agents, (size_t)w->P.n_envs, w->snap, obs, w->cfg.obs_f64 != 0,
+                                    TB.mask_out, s));
+    return MACM_OK;
+  }
+  HIP_TRY(tdm_launch_step(w, TB, w->cur, actions, obs, out ? out->done : nullptr, s));
   w->cur ^= 1;
+  return MACM_OK;
+}
+
+// A wave-kernel rollout (not the closed loop) with the split observation: the overwrite form keeps
+// one snapshot row per env (the last step's) and observes it once; the trajectory form steps
+// chunks of kTdmSplitChunk steps into alternating snapshot halves, each chunk observed on the
+// observation stream while the caller's stream steps the next chunk.
+static int tdm_rollout_split(macm_tdm* w, const TdmBuffers& TB, const void* actions, int n_steps,
+                             const macm_tdm_outputs* out, hipStream_t s, unsigned long long astride, bool traj) {
+  const size_t E = w->P.n_envs, N = w->P.n_agents, EN = E * N, S = N - 1;
+  const bool f64 = w->cfg.obs_f64 != 0;
+  const size_t orow = EN * S * 4 * (f64 ? sizeof(double) : sizeof(float));  // obs bytes per step
+  if (!traj) {
+    int rc = tdm_split_buffers(w, E, s);
+    if (rc) return rc;
+    TdmBuffers TBs = TB;
+    TBs.snap_out = w->snap;
+    HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TBs, w->cur, actions, nullptr, f64, out ? out->done : nullptr, s,
+                                   n_steps, astride, 0));
+    if (n_steps & 1) w->cur ^= 1;
+    HIP_TRY(launch_tdm_observe_snap(w->TP, (int)N, E, w->snap, out->obs, f64, TB.mask_out, s));
+    return MACM_OK;
+  }
+  const int KC = n_steps < kTdmSplitChunk ? n_steps : kTdmSplitChunk;
+  int rc = tdm_split_buffers(w, (size_t)KC * E, s);
+  if (rc) return rc;
+  const unsigned char* act = static_cast<const unsigned char*>(actions);
+  unsigned char* obs = static_cast<unsigned char*>(out->obs);
+  int c = 0;
+  for (int k0 = 0; k0 < n_steps; k0 += KC, ++c) {
+    const int kc = n_steps - k0 < KC ? n_steps - k0 : KC, b = c & 1;
+    float4* snap = w->snap + (size_t)b * w->snap_rows * N;
+    if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, w->ev_obs[b], 0));  // chunk c - 2's observation has read this half
+    TdmBuffers TBc = TB;
+    auto row = [k0](auto* p, size_t per) { return p ? p + (size_t)k0 * per : p; };
+    TBc.mask_out = nullptr;
+    TBc.health_out = row(TB.health_out, EN);
+    TBc.alive_out = row(TB.alive_out, EN);
+    TBc.winner_out = row(TB.winner_out, E);
+    TBc.snap_out = snap;
+    HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TBc, w->cur, act + (size_t)k0 * astride, nullptr, f64,
+                                   row(out->done, E), s, kc, astride, 1));
+    if (kc & 1) w->cur ^= 1;
+    HIP_TRY(hipEventRecord(w->ev_phys[b], s));
+    HIP_TRY(hipStreamWaitEvent(w->obs_stream, w->ev_phys[b], 0));
+    HIP_TRY(launch_tdm_observe_snap(w->TP, (int)N, (size_t)kc * E, snap, obs ? obs + (size_t)k0 * orow : nullptr, f64,
+                                    row(TB.mask_out, EN * S), w->obs_stream));
+    HIP_TRY(hipEventRecord(w->ev_obs[b], w->obs_stream));
+  }
+  // joined: the caller's stream waits for the last chunk's observation (the stream is in order)
+  HIP_TRY(hipStreamWaitEvent(s, w->ev_obs[(c - 1) & 1], 0));
   return MACM_OK;
 }
 
@@ -1480,6 +1618,8 @@ static int tdm_rollout(macm_tdm* w, const void* actions, int n_steps, const macm
     }
     return MACM_OK;
   }
+  if (!bots && out && (out->obs || out->mask) && tdm_split_obs(w))
+    return tdm_rollout_split(w, TB, actions, n_steps, out, s, astride, traj);
   HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TB, w->cur, actions, out ? out->obs : nullptr,
                                  w->cfg.obs_f64 != 0, out ? out->done : nullptr, s, n_steps, astride, traj ? 1 : 0));
   if (n_steps & 1) w->cur ^= 1;
@@ -1662,6 +1802,13 @@ int macm_bots_combat(const void* obs, const uint8_t* mask, int32_t obs_f64, int3
 // Diagnostic build only: copy the per-env phase stamps [E, 32] of the last step (the wave kernel
 // uses rows of 16).
 int macm_debug_stamps(macm_world* w, unsigned long long* out) {
+  if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
+  DeviceGuard g(w->device);
+  HIP_TRY(hipMemcpy(out, w->B.stamps, (size_t)w->P.n_envs * 32 * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  return MACM_OK;
+}
+int macm_debug_tdm_stamps(macm_tdm* w, unsigned long long* out) {
   if (!w || !out) return fail(MACM_E_INVALID, "NULL argument");
   DeviceGuard g(w->device);
   HIP_TRY(hipMemcpy(out, w->B.stamps, (size_t)w->P.n_envs * 32 * sizeof(unsigned long long),

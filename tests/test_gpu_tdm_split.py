@@ -1,0 +1,100 @@
+"""The split TDM observation (round 6, csrc/tdm_obs_snap.hip): the wave kernel writes
+pose snapshots and tdm_observe_snap observes every (step, env) row with a workgroup of its own. It
+must give the fused form's outputs bit for bit (obs, mask, health, alive, done, winner, state,
+counters) through every entry point that takes it: per-step launches, the overwrite rollout and the
+trajectory rollout in chunks (K = 19: chunks of 8, 8 and 3 on two snapshot halves), float32 and
+float64 observations, deaths, and envs that take the spill step (MACM_DEBUG_FORCE_SPILL). The fused
+form itself is pinned to the oracle by test_gpu_tdm.py; the split form is the default below 1024 envs,
+so those tests run it too. MACM_TDM_SPLIT_OBS=0/1 selects the form per call."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from gym_macm import _abi  # noqa: E402
+from gym_macm.tdm_world import TdmWorld, tdm_config  # noqa: E402
+
+
+def actions(K, E, N, seed, p_attack=0.5):
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    a = torch.randint(0, 3, (K, E, N, 4), dtype=torch.uint8, device="cuda:0", generator=g)
+    a[..., 3] = (torch.rand((K, E, N), device="cuda:0", generator=g) < p_attack).to(torch.uint8)
+    return a
+
+
+def same_outputs(a, b, ctx):
+    for x, y, nm in zip(a.outputs(), b.outputs(), ("obs", "mask", "health", "alive", "done", "winner")):
+        assert torch.equal(x, y), f"{ctx}: {nm}"
+
+
+def same_state(a, b, ctx):
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"{ctx}: state[{k}]")
+    np.testing.assert_array_equal(a.counters(), b.counters(), err_msg=f"{ctx}: counters")
+
+
+def pair(monkeypatch, E, teams, seed, debug=0, **kw):
+    ws = []
+    for _ in range(2):
+        w = TdmWorld(tdm_config(teams, **kw), E, device="cuda:0")
+        if debug:
+            w.set_debug(debug)
+        w.reset(seed, 0)
+        ws.append(w)
+    return ws
+
+
+def call(monkeypatch, split, fn, *args):
+    monkeypatch.setenv("MACM_TDM_SPLIT_OBS", "1" if split else "0")
+    r = fn(*args)
+    monkeypatch.delenv("MACM_TDM_SPLIT_OBS")
+    return r
+
+
+@pytest.mark.parametrize("E,teams,kw,debug", [
+    (512, [16, 16], {}, 0),                                   # BASELINE C4's per-GPU shard
+    (37, [16, 16], {"obs_f64": True}, 0),
+    (64, [3, 3, 3], {"fresh_raycast": True}, 0),
+    (24, [32, 32], {}, 0),                                    # N = 64: the 64-lane instantiation
+    (16, [8, 8], {"world_width": 8.0, "world_height": 8.0}, 0),   # crowded: deaths early
+    (12, [16, 16], {}, _abi.DEBUG_FORCE_SPILL),               # every env through the spill step
+])
+def test_split_equals_fused(monkeypatch, E, teams, kw, debug):
+    N = sum(teams)
+    K = 19
+    a, b = pair(monkeypatch, E, teams, 1000 + E + N, debug, **kw)
+    acts = actions(3 * K + 2, E, N, E * N)
+    for k in range(K):  # per-step launches
+        call(monkeypatch, False, a.step, acts[k])
+        call(monkeypatch, True, b.step, acts[k])
+        same_outputs(a, b, f"step {k}")
+    same_state(a, b, "per-step launches")
+    ta = call(monkeypatch, False, a.rollout_traj, acts[K:2 * K])  # trajectory: chunks 8, 8, 3
+    tb = call(monkeypatch, True, b.rollout_traj, acts[K:2 * K])
+    for key in ta:
+        assert torch.equal(ta[key], tb[key]), f"trajectory rollout: {key}"
+    same_state(a, b, "trajectory rollout")
+    call(monkeypatch, False, a.rollout, acts[2 * K:3 * K + 2])  # overwrite: the last step's outputs
+    call(monkeypatch, True, b.rollout, acts[2 * K:3 * K + 2])
+    same_outputs(a, b, "overwrite rollout")
+    same_state(a, b, "overwrite rollout")
+    assert a.status() == 0 and b.status() == 0
+    if debug:
+        assert b.spilled() > 0
+
+
+def test_split_is_the_default_below_1024_envs(monkeypatch):
+    """The launch form the library picks itself equals the forced fused form at 512 envs (C4's shard),
+    in the trajectory rollout the benchmark times."""
+    E, teams, K = 512, [16, 16], 20
+    monkeypatch.delenv("MACM_TDM_SPLIT_OBS", raising=False)
+    a, b = pair(monkeypatch, E, teams, 77)
+    acts = actions(K, E, 32, 5)
+    ta = call(monkeypatch, False, a.rollout_traj, acts)
+    tb = b.rollout_traj(acts)  # default
+    for key in ta:
+        assert torch.equal(ta[key], tb[key]), key
+    same_state(a, b, "default form")
