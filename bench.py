@@ -520,6 +520,29 @@ def main():
                             "uniform random discrete actions (MultiDiscrete[3,3,3]) pre-generated on device"
                             if args.policy == "random" else "closed loop with the device bots.flock kernel (timed)") +
                         f", from reset (seed {args.seed:#x})")
+        # MACM_LAUNCH_SPLIT_OBS: every TDM step / rollout but the closed-loop rollout (its bot reads each
+        # step's observation inside the launch)
+        split = (args.env == "tdm" and N <= 64 and bool(world_h.launch_flags() & 2)
+                 and not (rollout and args.policy == "bots"))
+        slices = world_h.rollout_slices() if (args.env == "flock" and N > 64) else 0
+        if split:  # TDM below 1024 envs: pose snapshots, the observation in a kernel of its own
+            kname += " + tdm_observe_snap<" + ("double" if args.obs_f64 else "float") + ">"
+        if rollout and N <= 64:
+            if split and traj is not None:
+                launch_desc = (f"{rname}: the K timed steps in rollout launches of 8 steps that write pose "
+                               "snapshots, each chunk's observation (tdm_observe_snap) on a second stream beside "
+                               "the next chunk's physics")
+            elif split:
+                launch_desc = f"one {rname} launch for the K timed steps, the last step's observation by tdm_observe_snap"
+            else:
+                launch_desc = f"one {rname}{'_bots' if args.policy == 'bots' else ''} launch for the K timed steps"
+        elif not rollout:
+            launch_desc = "one step per launch" + (" (+ tdm_observe_snap)" if split else "")
+        elif slices:
+            launch_desc = (f"{rname}, workgroup path: {slices} env slices on streams of their own, 3 launches per "
+                           "step each, no join between steps")
+        else:
+            launch_desc = f"{rname}, workgroup path: 3 launches per step"
         out = {
             "metric": metric,
             "value": value,
@@ -551,12 +574,7 @@ def main():
                 # defaults from 1/8 of the device's free memory)
                 "max_contacts": int(world_h.C) if args.env == "flock" else None,
                 "spill_slots": int(world_h.spill_slots) if args.env == "flock" else None,
-                "launch": (f"one {rname}{'_bots' if args.policy == 'bots' else ''} launch for the K timed steps"
-                           if rollout and N <= 64
-                           else "one step per launch" if not rollout
-                           else f"{rname}, workgroup path: 2 env slices on streams of their own, 3 launches per "
-                                "step each, no join between steps" if E >= 1024 and N < 512
-                           else f"{rname}, workgroup path: 3 launches per step"),
+                "launch": launch_desc,
                 # what the caller gets back: the reference returns (obs, rewards) from every env.step
                 # (mvmnt.py:140); the plain rollout launch overwrites its outputs every step
                 "outputs": ("every step's ([K, E, N, ...] trajectory buffers)" if traj is not None

@@ -556,6 +556,8 @@ int macm_world_destroy(macm_world* w) {
   return MACM_OK;
 }
 
+static int wg_rollout_slices(const macm_world* w);
+
 int macm_world_info_get(const macm_world* w, macm_world_info* info) {
   if (!w || !info) return fail(MACM_E_INVALID, "NULL argument");
   info->n_envs = w->P.n_envs;
@@ -567,6 +569,7 @@ int macm_world_info_get(const macm_world* w, macm_world_info* info) {
   info->device = w->device;
   info->spill_slots = w->B.sp_pool > 0 ? w->B.sp_pool : w->P.n_envs;
   info->launch_flags = w->ho ? MACM_LAUNCH_HANDOFF : 0;
+  info->rollout_slices = wg_rollout_slices(w);
   return MACM_OK;
 }
 
@@ -781,6 +784,12 @@ static int n_slices() {
   const int n = v ? atoi(v) : kSlices;
   return n < 0 ? 0 : n > 8 ? 8 : n;
 }
+// the env slices a workgroup-path rollout of this world runs (0: none, one stream)
+static int wg_rollout_slices(const macm_world* w) {
+  if (w->wave || w->big || w->P.n_envs < kSliceMinEnvs || w->P.n_agents >= kSliceMaxAgents) return 0;
+  const int S = n_slices();
+  return S >= 2 ? S : 0;
+}
 // astride == 0: the closed loop (macm_world_rollout_bots): every step of a slice reads the bot's
 // action rows of its envs and the bots kernel writes the next ones from the slice's obs rows
 // (trajectory form: step k reads action row k and writes row k + 1 of [K + 1, E, N, 3]).
@@ -881,8 +890,7 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
     return MACM_OK;
   }
   const unsigned char* act = static_cast<const unsigned char*>(actions);
-  if (!w->big && w->P.n_envs >= kSliceMinEnvs && w->P.n_agents < kSliceMaxAgents && n_slices() >= 2)
-    return rollout_wg_slices(w, n_slices(), act, n_steps, astride, out, traj, s);
+  if (const int S = wg_rollout_slices(w)) return rollout_wg_slices(w, S, act, n_steps, astride, out, traj, s);
   // workgroup path: its three launches per step (and the bot's), in order
   const long long rows = (long long)w->P.n_envs * w->P.n_agents;
   const unsigned long long kstride = bots ? (traj ? (unsigned long long)rows * 3 : 0ull) : astride;
@@ -1754,6 +1762,11 @@ int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream) {
   for (size_t i = 0; i < h.size(); ++i) acc[i & 3] += h[i];
   for (int i = 0; i < 4; ++i) out[i] = (int64_t)acc[i];
   return MACM_OK;
+}
+
+int macm_tdm_launch_flags(const macm_tdm* w) {
+  if (!w) return fail(MACM_E_INVALID, "tdm is NULL");
+  return tdm_split_obs(w) ? MACM_LAUNCH_SPLIT_OBS : 0;
 }
 
 int macm_tdm_spilled(macm_tdm* w, int64_t* env_steps, void* stream) {

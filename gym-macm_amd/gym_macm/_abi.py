@@ -77,6 +77,7 @@ class MacmState(Structure):
 
 
 LAUNCH_HANDOFF = 1  # macm_world_info.launch_flags
+LAUNCH_SPLIT_OBS = 2  # macm_tdm_launch_flags
 
 
 class MacmWorldInfo(Structure):
@@ -90,6 +91,7 @@ class MacmWorldInfo(Structure):
         ("device", c_int32),
         ("spill_slots", c_int32),
         ("launch_flags", c_int32),
+        ("rollout_slices", c_int32),
     ]
 
 
@@ -227,6 +229,7 @@ SIGNATURES = {
     "macm_tdm_status": (c_int, [c_void_p, POINTER(c_int32), c_void_p]),
     "macm_tdm_counters": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_tdm_spilled": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
+    "macm_tdm_launch_flags": (c_int, [c_void_p]),
     "macm_tdm_set_debug": (c_int, [c_void_p, c_int32]),
     "macm_bots_flock": (c_int, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
     "macm_bots_combat": (c_int, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p]),

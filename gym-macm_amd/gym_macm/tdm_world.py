@@ -301,6 +301,13 @@ class TdmWorld:
         _abi.check(self.L.macm_tdm_spilled(self.h, ctypes.byref(v), self._stream()), "macm_tdm_spilled")
         return int(v.value)
 
+    def launch_flags(self) -> int:
+        """MACM_LAUNCH_* of the next step / rollout (macm_tdm_launch_flags): LAUNCH_SPLIT_OBS when the
+        observation is written by its own kernel from pose snapshots (fewer than 1024 envs)."""
+        f = self.L.macm_tdm_launch_flags(self.h)
+        _abi.check(min(f, 0), "macm_tdm_launch_flags")
+        return int(f)
+
     def set_debug(self, flags: int) -> None:
         """Test hooks (macm_tdm_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the spill
         step; DEBUG_SPILL_POOL | slots << 8 shares that many working-set slots; DEBUG_SPILL_FAIL makes

@@ -355,6 +355,13 @@ class World:
         _abi.check(self.L.macm_world_info_get(self.h, ctypes.byref(info)), "macm_world_info_get")
         return int(info.launch_flags)
 
+    def rollout_slices(self) -> int:
+        """macm_world_info.rollout_slices: the env slices a workgroup-path rollout runs on streams of
+        their own (0: none)."""
+        info = _abi.MacmWorldInfo()
+        _abi.check(self.L.macm_world_info_get(self.h, ctypes.byref(info)), "macm_world_info_get")
+        return int(info.rollout_slices)
+
     def uses_handoff(self) -> bool:
         return bool(self.launch_flags() & _abi.LAUNCH_HANDOFF)
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MACM_ABI_VERSION 8
+#define MACM_ABI_VERSION 9
 
 enum {
   MACM_OK = 0,
@@ -270,10 +270,15 @@ typedef struct macm_world_info {
   int32_t device;
   int32_t spill_slots;    /* spill working-set slots (= n_envs: one per env; fewer: a pool) */
   int32_t launch_flags;   /* MACM_LAUNCH_* of the workgroup step, decided at the first step (ABI 8) */
+  int32_t rollout_slices; /* env slices a workgroup-path rollout runs on streams of their own (0: none;
+                             MACM_WG_SLICES overrides the default 3) (ABI 9)                       */
 } macm_world_info;
 
 /* macm_world_info.launch_flags */
 #define MACM_LAUNCH_HANDOFF 1  /* kernel C as kernel B's consumer on a second stream (MACM_HANDOFF) */
+#define MACM_LAUNCH_SPLIT_OBS 2 /* TDM (macm_tdm_launch_flags, ABI 9): the step writes pose snapshots and
+                                   tdm_observe_snap observes them in a launch of its own (fewer than
+                                   1024 envs, N <= 64; MACM_TDM_SPLIT_OBS overrides); same results */
 
 typedef struct macm_world macm_world;
 
@@ -505,6 +510,9 @@ int macm_tdm_counters(macm_tdm* w, int64_t out[4], void* stream);
 
 /* Env-steps taken by the spill step since creation (ABI 6). */
 int macm_tdm_spilled(macm_tdm* w, int64_t* env_steps, void* stream);
+
+/* MACM_LAUNCH_* of the next macm_tdm_step / rollout (not the closed loop) (ABI 9). */
+int macm_tdm_launch_flags(const macm_tdm* w);
 
 /* Test hooks: MACM_DEBUG_FORCE_SPILL, MACM_DEBUG_SPILL_POOL (ABI 6). */
 int macm_tdm_set_debug(macm_tdm* w, int32_t flags);

@@ -72,7 +72,7 @@ def test_tdm_defaults_match_python_mirror():
 
 def test_version_and_defaults_without_gpu():
     L = _abi.lib()
-    assert L.macm_abi_version() == 8
+    assert L.macm_abi_version() == 9
     assert b"gfx950" in L.macm_version()
     c = _abi.MacmConfig()
     assert L.macm_config_default(ctypes.byref(c)) == 0
