@@ -489,8 +489,6 @@ def main():
         tj = load_traffic(args.traffic_json)
         if args.obs_f64:  # the scalar sweep exists only in the float32-obs instantiation
             kname = kname.replace("float", "double").replace("double, true>", "double, false>")
-        if rollout and N <= 64:  # the rollout kernel's last parameter: no solo launch (round 5)
-            kname = kname[:-1] + ", false>"
 
         spl = K if (rollout and N <= 64) else 1  # env steps per launch of the priced kernel
         traffic_src = None

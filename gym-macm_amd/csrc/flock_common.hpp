@@ -103,23 +103,8 @@ struct WorldBuffers {
   uint32_t* spill_count;         // [E]       steps taken by the spill step (macm_world_spilled)
   uint32_t* host_status;         // mapped pinned host word: nonzero once any env set a status bit
   // [E] the env order of a launch, heaviest first (flock_step_w64.hip, rollout_sched): wave-kernel
-  // rollouts, and the workgroup step's kernels (flock_step_wg.hip, kWgEnvOrder)
+  // rollouts, and the workgroup step's kernels (flock_step_wg.hip, wg_env)
   uint32_t* sched;
-};
-
-// The solo split of a balanced wave-kernel rollout (flock_step_w64.hip env_rollout_w64<..., SOLO>):
-// the n heaviest envs in waves that own their SIMD, on `stream` (forked from and joined back into
-// the caller's stream with the two events). n = 0: one launch.
-struct SoloLaunch {
-  int n;
-  hipStream_t stream;
-  hipEvent_t fork, join;
-  // each solo wave adds 1 when it starts (monotonic); the caller's stream runs a watcher kernel
-  // (flock_step_wg.hip wait_count) until all n have, before the ordinary launch, so the solo waves
-  // are placed on empty SIMDs first (else the ordinary launch fills every SIMD and they wait for one
-  // to drain)
-  unsigned long long* started;
-  unsigned long long expected;
 };
 
 // The B -> C handoff of the workgroup step (flock_step_wg.hip, round 5). Kernel C of a step used to
@@ -237,17 +222,12 @@ __host__ __device__ inline int tdm_team_of(const TdmParams& T, int i) {
 // for every float32 angle |a| < 2^19, tools/trig_check.c) in that range, the device libm
 // beyond it (|angle| >= 2^19 only arises from injected state: the step wraps into [-pi, pi]).
 __device__ __forceinline__ void act_trig(float a, double* s0, double* c0, double* s1, double* c1) {
-#ifdef MACM_LIB_TRIG
-  sincos((double)a, s0, c0);
-  sincos((double)a + M_PI / 2, s1, c1);
-#else
   if (fabsf(a) < 524288.0f) {
     macm_action_trig(a, s0, c0, s1, c1);
   } else {
     sincos((double)a, s0, c0);
     sincos((double)a + M_PI / 2, s1, c1);
   }
-#endif
 }
 
 // sqrt((double)x) of a float32 x (b2DistanceSquared), as stored into an OT observation.
@@ -270,26 +250,18 @@ __device__ __forceinline__ double obs_sqrt(float x) {
 // that both results are < FLT_EPSILON, so Normalize takes the same branch.
 // Both checked on the device over every float32 input (tools/rcp_sqrt_gpu_check.hip).
 __device__ __forceinline__ float rcp_rn(float x) {
-#ifdef MACM_LIB_SQRT_DIV
-  return 1.0f / x;
-#else
   const float y = __builtin_amdgcn_rcpf(x);
   const float e = __builtin_fmaf(-x, y, 1.0f);
   return __builtin_fmaf(e, y, y);
-#endif
 }
 
 __device__ __forceinline__ float sqrt_rn(float x) {
-#ifdef MACM_LIB_SQRT_DIV
-  return sqrtf(x);
-#else
   const float s = __builtin_amdgcn_sqrtf(x);
   const float sd = __uint_as_float(__float_as_uint(s) - 1u);
   const float su = __uint_as_float(__float_as_uint(s) + 1u);
   float r = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
   r = __builtin_fmaf(-su, s, x) > 0.0f ? su : r;
   return r;
-#endif
 }
 
 // RN(n / K) for a loop-invariant K > 0 (the position solve's -C / (mA + mB)) from rK = RN(1 / K),
@@ -302,32 +274,23 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 // the default and 255 random configs: 0 mismatches (tools/rcp_sqrt_gpu_check.hip; below 2^-40
 // the sequence can differ, and is never given such n).
 __device__ __forceinline__ float div_by_invariant(float n, float K) {
-#ifdef MACM_LIB_SQRT_DIV
-  return n / K;
-#else
   const float rK = 1.0f / K;
   const float q0 = n * rK;
   const float q1 = __builtin_fmaf(__builtin_fmaf(-K, q0, n), rK, q0);
   // the sign of the quotient is the sign of n (K > 0); copysign keeps it for n = -0, where the
   // fma corrections would return +0 and n / K gives -0 (the sign can reach a zero position)
   return __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-K, q1, n), rK, q1), n);
-#endif
 }
 
 // Between the level steps of a one-wave Gauss-Seidel solve: the next step's lanes read the body
 // updates this step's lanes wrote to LDS. A wave's LDS accesses are performed in issue order, so
 // wavefront-scope release/acquire fences (no wait) are enough: the reads are issued after the
 // writes and cannot pass them. Waiting for the writes to complete (lgkmcnt(0), the round-2
-// first version: -DMACM_LEVEL_WAIT) adds an LDS round trip to every level step.
+// first version) added an LDS round trip to every level step.
 __device__ __forceinline__ void wave_lds_sync() {
-#ifdef MACM_LEVEL_WAIT
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
-  __builtin_amdgcn_wave_barrier();
-#else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
 }
 
 // Inclusive prefix maximum over the 64 lanes of a wave in lane order, by DPP row shifts and row
@@ -336,9 +299,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // is out of its row (no bound_ctrl) or outside the row mask is not written and keeps its own value,
 // which is the maximum's identity there. The compiler does not fold update_dpp into the max (it
 // emits a mov_dpp, an identity mov and the max per step: 24 instructions against 12).
-// -DMACM_NO_DPP_ASM: the builtin form.
 __device__ __forceinline__ int wave_prefix_max(int v) {
-#ifndef MACM_NO_DPP_ASM
   asm volatile(
       "s_nop 1\n\t"
       "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
@@ -354,23 +315,13 @@ __device__ __forceinline__ int wave_prefix_max(int v) {
       "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
       : "+v"(v));
   return v;
-#endif
-  constexpr int kId = -0x40000000;
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return v;
 }
 
 // Inclusive prefix sum over the 64 lanes of a wave in lane order (integers), the DPP form of
 // wave_prefix_max: a lane whose DPP source is outside its row or the row mask is not written and
-// keeps its own partial sum. The whole wave must be active. -DMACM_NO_DPP_ASM: __shfl_up steps
-// (six LDS-crossbar round trips).
+// keeps its own partial sum. The whole wave must be active (__shfl_up steps: six LDS-crossbar
+// round trips).
 __device__ __forceinline__ int wave_prefix_sum(int v) {
-#ifndef MACM_NO_DPP_ASM
   asm volatile(
       "s_nop 1\n\t"
       "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
@@ -386,30 +337,16 @@ __device__ __forceinline__ int wave_prefix_sum(int v) {
       "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
       : "+v"(v));
   return v;
-#else
-  const int lane = threadIdx.x & 63;
-  for (int d = 1; d < 64; d <<= 1) {
-    const int o = __shfl_up(v, d, 64);
-    if (lane >= d) v += o;
-  }
-  return v;
-#endif
 }
 
 // Stores of the Flock step's per-agent outputs (obs, reward, neighbour id, collided): nontemporal
 // (the policy reads them, the step does not): driver window 34.0 -> 33.5 us, steady 21.6 -> 21.4 us
 // (profiles/r02/nt_stores). Not for TDM's [E, N, N-1, 4] obs: its 16-byte pair-tile stores then
 // stop combining in L2 (C4 32.3 -> 62.5 us). Nor for the state and contact list the next step
-// reads (no gain). A/B knobs: -DMACM_PLAIN_OUT, -DMACM_NT_STATE.
+// reads (no gain).
 template <int KIND, typename T>
 __device__ __forceinline__ void st_g(T* p, const T& v) {
-#ifdef MACM_NT_STATE
-  constexpr bool nt = true;
-#elif defined(MACM_PLAIN_OUT)
-  constexpr bool nt = false;
-#else
   constexpr bool nt = KIND == 0;
-#endif
   if constexpr (nt) {
     if constexpr (sizeof(T) == 16) {
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));

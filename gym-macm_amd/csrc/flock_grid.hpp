@@ -35,10 +35,7 @@
 namespace macm {
 namespace grid {
 
-#ifndef MACM_CELLS_MIN_AGENTS  // A/B knob
-#define MACM_CELLS_MIN_AGENTS 256
-#endif
-constexpr int kCellsMinAgents = MACM_CELLS_MIN_AGENTS;  // below: the all-pairs sweep (StepParams.sweep overrides)
+constexpr int kCellsMinAgents = 256;  // below: the all-pairs sweep (StepParams.sweep overrides)
 
 __host__ __device__ inline int buckets(int N) {  // strips: a power of two >= N / 4, at least 64
   int h = 64;

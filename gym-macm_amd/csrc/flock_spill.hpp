@@ -29,24 +29,15 @@ namespace macm {
 namespace spill {
 
 // The level steps' contact updates on packed (x, y) pairs, as kernel B (flock_step_wg.hip
-// kWgPacked): bit-identical, contraction off. -DMACM_WG_SCALAR restores the scalar form.
-#ifdef MACM_WG_SCALAR
-constexpr bool kLevelPacked = false;
-#else
-constexpr bool kLevelPacked = true;
-#endif
+// kWgPacked): bit-identical, contraction off.
 typedef float lpf2 __attribute__((ext_vector_type(2)));
 
 
 constexpr int W = 64;
 
-// TDM above one wave: the observation in memory order (whole-line stores, an atan2 per slot) or by
-// pairs (tdm_obs_block: one atan2 core per pair, scattered 16-B stores). -DMACM_TDM_BLOCK_OBS_PAIRS
-#ifdef MACM_TDM_BLOCK_OBS_PAIRS
-constexpr bool kTdmBlockObsLinear = false;
-#else
-constexpr bool kTdmBlockObsLinear = true;
-#endif
+// TDM above one wave: the observation in memory order (tdm_obs_block_linear: whole-line stores, an
+// atan2 per slot); the pair form (tdm_obs_block: one atan2 core per pair, scattered 16-B stores) was
+// slower there (profiles/r03/abtests/tdm_block_obs/).
 
 struct __align__(16) Rec {  // per-agent pair-sweep record (48 B)
   float4 fn;               // fat AABB after SynchronizeFixtures
@@ -206,10 +197,7 @@ __device__ __forceinline__ void write_obs(OT* o, int coord, float ang, float bes
 // flags, listener, counters 0-2); each thread passes its force `F`. The physics skips the bodies
 // that are not alive (their contacts were destroyed with their proxies) and the env layer is TDM's:
 // the body state, the [N, N-1, 4] observation, done / winner, counter 3.
-#ifndef MACM_SPILL_CHUNK  // A/B knob: records per HBM chunk of the spill step's serial island solves
-#define MACM_SPILL_CHUNK 8
-#endif
-constexpr int kSpillChunk = MACM_SPILL_CHUNK;
+constexpr int kSpillChunk = 8;  // records per HBM chunk of the spill step's serial island solves
 
 // Diagnostic build (MACM_STAMPS): phase clocks of the worlds above 1024 agents (BPT > 1: only the spill
 // step runs there), stamps 16.. of the env's row (tools/big_phases.py)
@@ -567,72 +555,40 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
   uint32_t* g_lidx = g_adj + C;  // [nord] the island-order index of the p-th contact in level order
   uint32_t* g_hist = g_tab;      // [levels] counts, then positions
   auto level_body = [&](float4 r, float2& im, bool warm, float2& va, float2& vb) {
-    const float nx = r.y, ny = r.z, tx = ny, ty = -nx;
-    if constexpr (kLevelPacked) {  // the same IEEE operations on (x, y) pairs (v_pk_mul / v_pk_add)
-      const lpf2 n = {nx, ny}, t = {ny, -nx};
-      lpf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
-      if (warm) {
-        const lpf2 Pv = im.x * n + im.y * t;
+    // the contact update on (x, y) pairs (v_pk_mul / v_pk_add): the same IEEE operations as the
+    // scalar form, contraction off
+    const float nx = r.y, ny = r.z;
+    const lpf2 n = {nx, ny}, t = {ny, -nx};
+    lpf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
+    if (warm) {
+      const lpf2 Pv = im.x * n + im.y * t;
+      vA = vA - mA * Pv;
+      vB = vB + mB * Pv;
+    } else {
+      {
+        const lpf2 pr = (vB - vA) * t;
+        float lambda = kmass * (-(pr.x + pr.y));
+        const float maxf = friction * im.x;
+        const float ni = sclamp(im.y + lambda, -maxf, maxf);
+        lambda = ni - im.y;
+        im.y = ni;
+        const lpf2 Pv = lambda * t;
         vA = vA - mA * Pv;
         vB = vB + mB * Pv;
-      } else {
-        {
-          const lpf2 pr = (vB - vA) * t;
-          float lambda = kmass * (-(pr.x + pr.y));
-          const float maxf = friction * im.x;
-          const float ni = sclamp(im.y + lambda, -maxf, maxf);
-          lambda = ni - im.y;
-          im.y = ni;
-          const lpf2 Pv = lambda * t;
-          vA = vA - mA * Pv;
-          vB = vB + mB * Pv;
-        }
-        {
-          const lpf2 pr = (vB - vA) * n;
-          float lambda = -kmass * ((pr.x + pr.y) - 0.0f);
-          const float ni = fmaxf(im.x + lambda, 0.0f);
-          lambda = ni - im.x;
-          im.x = ni;
-          const lpf2 Pv = lambda * n;
-          vA = vA - mA * Pv;
-          vB = vB + mB * Pv;
-        }
       }
-      va = make_float2(vA.x, vA.y);
-      vb = make_float2(vB.x, vB.y);
-      return;
+      {
+        const lpf2 pr = (vB - vA) * n;
+        float lambda = -kmass * ((pr.x + pr.y) - 0.0f);
+        const float ni = fmaxf(im.x + lambda, 0.0f);
+        lambda = ni - im.x;
+        im.x = ni;
+        const lpf2 Pv = lambda * n;
+        vA = vA - mA * Pv;
+        vB = vB + mB * Pv;
+      }
     }
-    if (warm) {
-      const float Px = im.x * nx + im.y * tx, Py = im.x * ny + im.y * ty;
-      va.x = va.x - mA * Px;
-      va.y = va.y - mA * Py;
-      vb.x = vb.x + mB * Px;
-      vb.y = vb.y + mB * Py;
-      return;
-    }
-    {  // tangent first
-      const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-      const float vt = dvx * tx + dvy * ty;
-      float lambda = kmass * (-vt);
-      const float maxf = friction * im.x;
-      const float ni = sclamp(im.y + lambda, -maxf, maxf);
-      lambda = ni - im.y;
-      im.y = ni;
-      const float Px = lambda * tx, Py = lambda * ty;
-      va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-      vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
-    }
-    {  // normal (velocityBias == 0: restitution 0)
-      const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-      const float vn = dvx * nx + dvy * ny;
-      float lambda = -kmass * (vn - 0.0f);
-      const float ni = fmaxf(im.x + lambda, 0.0f);
-      lambda = ni - im.x;
-      im.x = ni;
-      const float Px = lambda * nx, Py = lambda * ny;
-      va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-      vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
-    }
+    va = make_float2(vA.x, vA.y);
+    vb = make_float2(vB.x, vB.y);
   };
   // one wave walks the level-ordered contacts in chunks of 64 (one per lane, loaded a chunk ahead); in
   // a chunk it steps its levels, the lanes of the current level updating together and the others on a
@@ -895,33 +851,18 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
             float2* const pa = on ? pca : pdd;
             float2* const pb = on ? pcb : pdd;
             float* const pm = on ? s_mins + I : pmd;
-            float2 ca = *pa, cb = *pb;
-            if constexpr (kLevelPacked) {
-              const lpf2 cA = {ca.x, ca.y}, cB = {cb.x, cb.y};
-              const lpf2 d = cB - cA, d2 = d * d;
-              const float len = sqrt_rn(d2.x + d2.y);
-              const lpf2 n = len < kEps ? d : d * rcp_rn(len);  // b2Vec2::Normalize
-              const lpf2 pr = d * n;
-              const float sep = (pr.x + pr.y) - P.radius - P.radius;
-              const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-              const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
-              const lpf2 Pv = imp * n, nA = cA - mA * Pv, nB = cB + mB * Pv;
-              *pa = make_float2(nA.x, nA.y);
-              *pb = make_float2(nB.x, nB.y);
-              __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-              lsync();
-              continue;
-            }
-            float nx = cb.x - ca.x, ny = cb.y - ca.y;
-            normalize(nx, ny);
-            const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - P.radius - P.radius;
+            const float2 ca = *pa, cb = *pb;
+            const lpf2 cA = {ca.x, ca.y}, cB = {cb.x, cb.y};
+            const lpf2 d = cB - cA, d2 = d * d;
+            const float len = sqrt_rn(d2.x + d2.y);
+            const lpf2 n = len < kEps ? d : d * rcp_rn(len);  // b2Vec2::Normalize
+            const lpf2 pr = d * n;
+            const float sep = (pr.x + pr.y) - P.radius - P.radius;
             const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
             const float imp = K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
-            const float Px = imp * nx, Py = imp * ny;
-            ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
-            cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
-            *pa = ca;
-            *pb = cb;
+            const lpf2 Pv = imp * n, nA = cA - mA * Pv, nB = cB + mB * Pv;
+            *pa = make_float2(nA.x, nA.y);
+            *pb = make_float2(nB.x, nB.y);
             __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             lsync();
           }
@@ -1160,16 +1101,13 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
         const int i = tid + j * BS;
         if (i < N) TB->snap_out[(size_t)e * N + i] = make_float4(s_c[i].x, s_c[i].y, s_slp[i], act[j] ? 1.0f : 0.0f);
       }
-    } else if (wide && kTdmBlockObsLinear)
+    } else if (wide) {
       tdm_obs_block_linear<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid,
                                BS, s_alivew, *TP, s_c, s_slp);
-    else if (wide)
-      for (int j = 0; j < BPT; ++j)
-        tdm_obs_block<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N,
-                          tid + j * BS, s_alivew, *TP, s_c, s_slp);
-    else
-      MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, livem,
-                       *TP, s_c, s_slp);
+    } else {
+      tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid, livem,
+                        *TP, s_c, s_slp);
+    }
     int alive_teams = 0, last_team = -1;
     for (int t = 0; t < TP->n_teams; ++t) {
       bool any = false;

@@ -54,10 +54,7 @@ constexpr int W = 64;       // wavefront = one env's agent lanes
 // 19 waves per CU, so a 4096-env launch (16 per CU) has slack (at 16 per CU, -4% per step at M
 // and -7% in the bots closed loop; TCAP 224 fits 20 per CU but sends dense bots envs to the
 // spill step: profiles/r02/wave_levels)
-#ifndef MACM_TCAP
-#define MACM_TCAP 256
-#endif
-constexpr int TCAP = MACM_TCAP;
+constexpr int TCAP = 256;
 constexpr int DEG = 16;     // touching contacts per body
 constexpr int ICAP = W / 2; // islands with >= 1 contact (>= 2 bodies each)
 constexpr int RCH = 2;      // list chunks (of 64 entries) cached in registers
@@ -66,76 +63,25 @@ constexpr int RCH = 2;      // list chunks (of 64 entries) cached in registers
 // positions go through LDS, so a contact update waits on one LDS round trip instead of
 // three (order -> record -> bodies). Measured -3.3% per step at the metric config
 // (profiles/r01/ab2). Keeping the bodies in registers too (per-contact copies, forwarded
-// after every update) was slower: +6% at 2..3 contacts. -DMACM_REC_ISLAND=0 disables.
-#ifndef MACM_REC_ISLAND
-#define MACM_REC_ISLAND 4
-#endif
-constexpr int KREC = MACM_REC_ISLAND;
-constexpr int KRECA = KREC > 0 ? KREC : 1;
+// after every update) was slower: +6% at 2..3 contacts.
+constexpr int KREC = 4;
+constexpr int KRECA = KREC;
 // In a wave that has 2..KREC-contact islands, its single-contact islands join the same
 // register-record solve (as islands of one contact) instead of running their own register
 // loop before it: the wave then walks max-island-size x 9 updates instead of 9 more on top
 // (single-contact lanes pay the LDS round trip that the multi-contact lanes wait on anyway).
-#ifdef MACM_NO_MERGE_SINGLETONS
-constexpr bool kMergeSingletons = false;
-#else
-constexpr bool kMergeSingletons = KREC > 1;
-#endif
 // Gauss-Seidel levels (T <= 64 touching contacts): the scalar DFS also gives each contact its
 // level, 1 + the level of the last earlier contact (island order) sharing a body with it; lane k
 // holds the k-th contact's record and the wave solves a level's contacts together (they share no
-// body, so every body keeps Box2D's sequence of updates). -DMACM_NO_LEVELS: the per-island lanes.
-#ifndef MACM_LEVELS_MIN_ISLAND  // the level path runs when an island has more contacts than this
-#define MACM_LEVELS_MIN_ISLAND 4
-#endif
-#ifdef MACM_NO_LEVELS
-constexpr bool kLevels = false;
-#else
-constexpr bool kLevels = true;
-#endif
-#ifndef MACM_BRANCHFREE_WAVE_LEVELS  // A/B knob: 0 = an exec-masked branch per level step (T <= 64 levels)
-#define MACM_BRANCHFREE_WAVE_LEVELS 1
-#endif
-#ifndef MACM_WAVE_LEVEL_UNROLL  // A/B knob: level steps per loop iteration in the one-slot level path (1, 2)
-#define MACM_WAVE_LEVEL_UNROLL 2
-#endif
-#ifndef MACM_BRANCHFREE_WAVE_POS  // A/B knob: 0 = exec-masked position level steps (T <= 64 levels)
-#define MACM_BRANCHFREE_WAVE_POS 1
-#endif
-#ifndef MACM_WAVE_LEVEL_ADDR_AHEAD  // A/B knob: 0 = select a level's LDS addresses at the start of its step
-#define MACM_WAVE_LEVEL_ADDR_AHEAD 1
-#endif
-#ifndef MACM_PRIO2_T  // touching contacts from which a wave keeps priority 2 after the chain
-#define MACM_PRIO2_T 3
-#endif
-// TDM obs through the staged writer (tdm_obs.hpp): whole-line stores, 709 B per agent-step of HBM
-// traffic instead of 864, but C4 34.1 us per step instead of 28.2 (profiles/r03/abtests/tdm_obs/):
-// off, the pair tiles stay (A/B knob)
-// The mask staged in LDS and written as 16-B pieces (round 4): HBM writes -4%, but the kernel's
-// extra VGPRs spill 28 B more scratch (reads +27%): 868 -> 870 B per agent-step, time unchanged
-// (profiles/r04/tdm_mask/). Off: the pair tiles write the mask bytes (A/B knob -DMACM_TDM_MASK_STAGED).
-// TDM obs in row-block order with the transposed half staged (tdm_obs.hpp, round 4; float32 obs,
-// N <= 32: the 6 KB stage). A/B knob -DMACM_NO_TDM_ROWBLOCKS: the pair tiles as in round 3.
-#ifdef MACM_NO_TDM_ROWBLOCKS
-constexpr bool kTdmObsRowBlocks = false;
-#else
-constexpr bool kTdmObsRowBlocks = true;
-#endif
-#ifdef MACM_TDM_MASK_STAGED
-constexpr bool kTdmMaskStaged = true;
-#else
-constexpr bool kTdmMaskStaged = false;
-#endif
-#ifdef MACM_TDM_OBS_STAGED
-constexpr bool kTdmObsStaged = true;
-#else
-constexpr bool kTdmObsStaged = false;
-#endif
-#ifdef MACM_NO_CHAIN_PRIORITY  // A/B knob: no s_setprio around the serial solver chain
-constexpr bool kChainPriority = false;
-#else
-constexpr bool kChainPriority = true;
-#endif
+// body, so every body keeps Box2D's sequence of updates). The level path runs when an island has
+// more than kLevelsMinIsland contacts (the register-record islands take the rest).
+constexpr int kLevelsMinIsland = 4;
+constexpr int kPrio2T = 3;  // touching contacts from which a wave keeps priority 2 after the chain
+// TDM obs in row-block order with the transposed half staged (tdm_obs.hpp tdm_obs_rowblocks, round 4;
+// float32 obs, N <= 32: the 6 KB stage), else the pair tiles (tdm_obs_pairs). Measured and dropped
+// (round 6 removed their code; evidence kept): the staged memory-order writer, 709 B per agent-step
+// of HBM traffic instead of 864 but C4 34.1 us per step instead of 28.2 (profiles/r03/abtests/tdm_obs/);
+// the mask staged in LDS, time unchanged with more scratch (profiles/r04/tdm_mask/).
 
 // Diagnostic build only (-DMACM_STAMPS, build/libmacm_hip_stamps.so via `make stamps`):
 // lane 0 records s_memtime at phase boundaries into B.stamps[e][0..13] and per-env
@@ -165,23 +111,14 @@ constexpr bool kChainPriority = true;
 
 __device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }  // b2Min
 __device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }  // b2Max
-__device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
 // The contact solvers' clamps as single v_min_f32 / v_max_f32 instead of compare + select
 // (b2Min / b2Max): they sit on the serial Gauss-Seidel chain. For non-NaN operands the two
 // forms differ only in the sign of a zero result (b2Max(-0, +0) is +0, v_max may give -0);
 // a zero impulse or velocity of either sign leaves every later value the same, so only
 // zero signs can differ (as they already do through the angular terms).
-#ifdef MACM_EXACT_ZERO_SIGNS
-__device__ __forceinline__ float smax(float a, float b) { return bmax(a, b); }
-__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return bclamp(a, lo, hi); }
-#elif defined(MACM_NO_MED3)
-__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return fmaxf(lo, fminf(a, hi)); }
-#else
 // sclamp as one v_med3_f32: the median of (a, lo, hi) is the clamp for lo <= hi and non-NaN a.
 __device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
 __device__ __forceinline__ float sclamp(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
-#endif
 
 // b2TestOverlap
 __device__ __forceinline__ bool overlap(float4 a, float4 b) {
@@ -315,29 +252,13 @@ __device__ __forceinline__ void solve_velocity_contact_pk(pf2& vA, pf2& vB, floa
   }
 }
 
-// The chains outside the wide levels (one-slot levels, per-island lanes, single contacts) on packed
-// pairs too: A/B knob (round 5)
-#ifdef MACM_PACKED_CHAINS
-constexpr bool kPackedChains = true;
-#else
-constexpr bool kPackedChains = false;
-#endif
-#ifdef MACM_PACKED_LEVELS  // A/B knob: the one-slot level steps (T <= 64) on packed pairs
-constexpr bool kPackedLevels = true;
-#else
-constexpr bool kPackedLevels = false;
-#endif
+// The chains outside the wide levels (one-slot levels, per-island lanes, single contacts) stay on
+// scalar components: on packed pairs they measured slower (round 5, profiles/r05/abtests/).
 
 // b2ContactSolver, one circle contact (fixedRotation: no angular terms). Shared by
 // the LDS path and the single-contact register path, so both round identically.
 __device__ __forceinline__ void warm_start_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
                                                    float ny, float ln, float ltg, float mA, float mB) {
-  if constexpr (kPackedChains) {
-    pf2 a = {vAx, vAy}, b = {vBx, vBy};
-    warm_start_contact_pk(a, b, nx, ny, ln, ltg, mA, mB);
-    vAx = a.x; vAy = a.y; vBx = b.x; vBy = b.y;
-    return;
-  }
   const float tx = ny, ty = -nx;  // b2Cross(normal, 1.0f)
   const float Px = ln * nx + ltg * tx, Py = ln * ny + ltg * ty;
   vAx = vAx - mA * Px;
@@ -349,12 +270,6 @@ __device__ __forceinline__ void warm_start_contact(float& vAx, float& vAy, float
 __device__ __forceinline__ void solve_velocity_contact(float& vAx, float& vAy, float& vBx, float& vBy, float nx,
                                                        float ny, float& ln, float& ltg, float mA, float mB,
                                                        float kmass, float friction) {
-  if constexpr (kPackedChains) {
-    pf2 a = {vAx, vAy}, b = {vBx, vBy};
-    solve_velocity_contact_pk(a, b, nx, ny, ln, ltg, mA, mB, kmass, friction);
-    vAx = a.x; vAy = a.y; vBx = b.x; vBy = b.y;
-    return;
-  }
   const float tx = ny, ty = -nx;
   {  // tangent first
     const float dvx = vBx - vAx, dvy = vBy - vAy;
@@ -404,12 +319,6 @@ __device__ __forceinline__ float solve_position_contact_pk(pf2& cA, pf2& cB, flo
 // b2PositionSolverManifold + one SolvePositionConstraints contact; returns sep.
 __device__ __forceinline__ float solve_position_contact(float& cAx, float& cAy, float& cBx, float& cBy,
                                                         float radius, float mA, float mB) {
-  if constexpr (kPackedChains) {
-    pf2 a = {cAx, cAy}, b = {cBx, cBy};
-    const float sep = solve_position_contact_pk(a, b, radius, mA, mB);
-    cAx = a.x; cAy = a.y; cBx = b.x; cBy = b.y;
-    return sep;
-  }
   float nx = cBx - cAx, ny = cBy - cAy;
   normalize(nx, ny);
   const float sep = ((cBx - cAx) * nx + (cBy - cAy) * ny) - radius - radius;
@@ -439,60 +348,15 @@ struct IntC {
 // from one scalar walk in island order, so the contacts of a level share no body and every body
 // takes Box2D's sequence of updates. A level step is branch-free until its stores: every slot
 // reads its two bodies and solves (the S chains interleave), and only the slots of the current
-// level store bodies (exec-masked) and keep their impulses. -DMACM_NO_WIDE_LEVELS: the per-island
-// lanes (one lane walks each island serially through LDS, as in round 2).
-#ifdef MACM_NO_WIDE_LEVELS
-constexpr bool kWideLevels = false;
-#else
-constexpr bool kWideLevels = true;
-#endif
+// level store bodies (exec-masked) and keep their impulses.
 constexpr int kNoLevel = 0xffff;  // a slot without a contact (or whose island has left the passes)
-// One-slot level steps: the lanes outside the level on a dummy slot each (round 3). One shared slot
-// (an LDS broadcast; microbenchmark V13 278 -> 275 cycles per level step, kernel B C5 -1%) measured
-// M bots +2%, the window unchanged (profiles/r04/abtests/shared_dummy/): A/B knob
-// -DMACM_WAVE_SHARED_DUMMY. The position minima of dummy lanes stay per lane either way.
-#ifdef MACM_WAVE_SHARED_DUMMY
-constexpr bool kSharedDummy = true;
-#else
-constexpr bool kSharedDummy = false;
-#endif
-// Level order: skip a slot by its level range (a scalar test) before the exec-masked update. Measured
-// M bots 161 -> 197 us (profiles/r04/abtests/serial_prefetch/), off: A/B knob -DMACM_WIDE_RANGE_SKIP.
-#ifdef MACM_WIDE_RANGE_SKIP
-constexpr bool kWideRangeSkip = kWideLevelOrder;
-#else
-constexpr bool kWideRangeSkip = false;
-#endif
-#ifdef MACM_WIDE_PRIORITY  // A/B knob: only the wide-level waves keep priority 3 through the chain
-constexpr bool kWidePriority = true;
-#else
-constexpr bool kWidePriority = false;
-#endif
-#ifdef MACM_WIDE_ISLAND_ORDER  // A/B knob: slots in island order (round 3)
-constexpr bool kWideLevelOrder = false;
-#else
-constexpr bool kWideLevelOrder = true;
-#endif
-#ifdef MACM_PAR_DFS  // A/B knob: the scalar island walk a popped body at a time (all its edges at once)
-constexpr bool kParDfs = true;
-#else
-constexpr bool kParDfs = false;
-#endif
-#ifdef MACM_PAR_DFS_WIDE  // A/B knob: the same for more than 64 touching contacts only (converged flocks)
-constexpr bool kParDfsWide = true;
-#else
-constexpr bool kParDfsWide = false;
-#endif
-#ifdef MACM_WIDE_REGMIN  // A/B knob: the wide position passes' island minima in registers
-constexpr bool kWideRegMin = true;
-#else
-constexpr bool kWideRegMin = false;
-#endif
-#ifdef MACM_WIDE_SCALAR  // A/B knob: the wide levels' updates on scalar components (round 4)
-constexpr bool kWidePacked = false;
-#else
-constexpr bool kWidePacked = true;  // round 5: M closed loop -2.6%, metric window -0.5% (r05/abtests/wide_packed/)
-#endif
+// One-slot level steps: the lanes outside the level on a dummy slot each (round 3; one shared slot
+// measured M bots +2%, profiles/r04/abtests/shared_dummy/). The wide levels' updates run on packed
+// pairs (round 5: M closed loop -2.6%, metric window -0.5%, profiles/r05/abtests/wide_packed/).
+// Measured slower and removed in round 6 (evidence kept): skipping a wide slot by its level range
+// (M bots 161 -> 197 us, profiles/r04/abtests/serial_prefetch/), slots in island order, the island
+// walk a popped body at a time (par_dfs), the wide position minima in registers, priority 3 for the
+// wide-level waves only.
 
 // S slots per lane; REG: each slot's normal and impulses in registers (S = 2, T <= 128), else read
 // from / written to the touching-contact arrays in LDS at every level step (S = 4: registers for
@@ -560,7 +424,7 @@ struct WideLevels {
     }
 #pragma unroll
     for (int q = 0; q < S; ++q) lvis[q] |= (uint32_t)is[q] << 16;
-    if (kWideLevelOrder) reorder<S, REG>(lane, Tw, s_ord, s_tab, s_tnx, s_tny, s_tln, s_tlt, s_tmp);
+    reorder<S, REG>(lane, Tw, s_ord, s_tab, s_tnx, s_tny, s_tln, s_tlt, s_tmp);
   }
 
   // Level order (round 4): contact k of the level-sorted order moves to slot k / 64 of lane k % 64,
@@ -629,23 +493,6 @@ struct WideLevels {
     }
   }
 
-  // level order: the lowest and highest level of each slot (lane 0 and the slot's last contact;
-  // an empty slot gets an empty range)
-  template <int S>
-  __device__ __forceinline__ void slot_ranges(int* lo, int* hi) const {
-#pragma unroll
-    for (int q = 0; q < S; ++q) {
-      const unsigned long long m = __ballot(lvl(lvis[q]) != kNoLevel);
-      if (m == 0ull) {
-        lo[q] = 1;
-        hi[q] = 0;
-      } else {
-        lo[q] = lvl((uint32_t)__builtin_amdgcn_readfirstlane((int)lvis[q]));
-        hi[q] = lvl((uint32_t)__builtin_amdgcn_readlane((int)lvis[q], 63 - __clzll(m)));
-      }
-    }
-  }
-
   // warm start (pass -1) + vel_iters velocity passes, level by level; then (REG) the impulses to
   // s_tln / s_tlt
   template <int S, bool REG>
@@ -658,49 +505,18 @@ struct WideLevels {
     // than one after the other), and levels grow along the island order, so in most level steps
     // one slot is busy. The warm-start pass and the velocity passes are separate loops, so that a
     // level step has no branch before its stores.
-    // Level order (kWideLevelOrder): slot q holds levels lo[q] .. hi[q] (wave-uniform), so a level
-    // step visits only the slots whose range holds it (a scalar test). The update stays
-    // exec-masked: run branch-free (every lane on the slot, the idle ones on a dummy) it was 14%
-    // slower in the M closed loop, where 4-5 waves per SIMD share the CU's LDS.
-    int lo[S], hi[S];
-    slot_ranges<S>(lo, hi);
+    // The update stays exec-masked: run branch-free (every lane on the slot, the idle ones on a dummy)
+    // it was 14% slower in the M closed loop, where 4-5 waves per SIMD share the CU's LDS.
     auto pass = [&](auto warm) {
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {
-          if (kWideRangeSkip && (l < lo[q] || l > hi[q])) continue;  // uniform: no lane of slot q at level l
           if (lvl(lvis[q]) == l) {  // exec-masked; a slot with no contact of this level is skipped
             if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));  // LDS addresses not hoisted (VGPRs)
             float cx, cy, nl, nt;
-            if constexpr (kWidePacked) {
-              pf2* const pA = reinterpret_cast<pf2*>(s_v + ia(pw[q]));
-              pf2* const pB = reinterpret_cast<pf2*>(s_v + ib(pw[q]));
-              pf2 vA = *pA, vB = *pB;
-              if constexpr (REG) {
-                cx = nx[q];
-                cy = ny[q];
-                nl = ln[q];
-                nt = lt[q];
-              } else {
-                cx = s_tnx[it(pw[q])];
-                cy = s_tny[it(pw[q])];
-                nl = s_tln[it(pw[q])];
-                nt = s_tlt[it(pw[q])];
-              }
-              if constexpr (decltype(warm)::value) warm_start_contact_pk(vA, vB, cx, cy, nl, nt, mA, mB);
-              else solve_velocity_contact_pk(vA, vB, cx, cy, nl, nt, mA, mB, kmass, friction);
-              *pA = vA;
-              *pB = vB;
-              if constexpr (REG) {
-                ln[q] = nl;
-                lt[q] = nt;
-              } else {
-                s_tln[it(pw[q])] = nl;
-                s_tlt[it(pw[q])] = nt;
-              }
-              continue;
-            }
-            float2 vA = s_v[ia(pw[q])], vB = s_v[ib(pw[q])];
+            pf2* const pA = reinterpret_cast<pf2*>(s_v + ia(pw[q]));
+            pf2* const pB = reinterpret_cast<pf2*>(s_v + ib(pw[q]));
+            pf2 vA = *pA, vB = *pB;
             if constexpr (REG) {
               cx = nx[q];
               cy = ny[q];
@@ -712,10 +528,10 @@ struct WideLevels {
               nl = s_tln[it(pw[q])];
               nt = s_tlt[it(pw[q])];
             }
-            if constexpr (decltype(warm)::value) warm_start_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB);
-            else solve_velocity_contact(vA.x, vA.y, vB.x, vB.y, cx, cy, nl, nt, mA, mB, kmass, friction);
-            s_v[ia(pw[q])] = vA;
-            s_v[ib(pw[q])] = vB;
+            if constexpr (decltype(warm)::value) warm_start_contact_pk(vA, vB, cx, cy, nl, nt, mA, mB);
+            else solve_velocity_contact_pk(vA, vB, cx, cy, nl, nt, mA, mB, kmass, friction);
+            *pA = vA;
+            *pB = vB;
             if constexpr (REG) {
               ln[q] = nl;
               lt[q] = nt;
@@ -748,51 +564,28 @@ struct WideLevels {
                                            uint8_t* s_isolved, float mA, float mB) {
     const unsigned long long islm = nisl >= 64 ? ~0ull : ((1ull << nisl) - 1ull);
     unsigned long long done = 0ull;
-    int lo[S], hi[S];  // level order: each slot's level range, taken before islands leave (a superset after)
-    slot_ranges<S>(lo, hi);
     for (int itr = 0; itr < P.pos_iters && done != islm; ++itr) {
       if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
       // an island that has left the passes never returns: its contacts lose their level
 #pragma unroll
       for (int q = 0; q < S; ++q) lvis[q] |= ((done >> isl(lvis[q])) & 1ull) ? (uint32_t)kNoLevel : 0u;
       wave_lds_sync();
-      // kWideRegMin: each slot's pass minimum (order-preserving int keys, as the atomics) in a register,
-      // one atomic per slot after the pass instead of one per contact on the level chain
-      int kmin[S];
-#pragma unroll
-      for (int q = 0; q < S; ++q) kmin[q] = 0;  // the pass minimum starts at 0.0f (key 0)
       for (int l = 0; l < dmax; ++l) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {  // one slot at a time, busy slots only, as in the velocity passes
-          if (kWideRangeSkip && (l < lo[q] || l > hi[q])) continue;  // uniform (slot ranges, below)
           if (lvl(lvis[q]) == l) {
             if constexpr (S > 2) asm volatile("" : "+v"(pw[q]));
-            float sep;
-            if constexpr (kWidePacked) {
-              pf2* const pA = reinterpret_cast<pf2*>(s_c + ia(pw[q]));
-              pf2* const pB = reinterpret_cast<pf2*>(s_c + ib(pw[q]));
-              pf2 cA = *pA, cB = *pB;
-              sep = solve_position_contact_pk(cA, cB, P.radius, mA, mB);
-              *pA = cA;
-              *pB = cB;
-            } else {
-              float2 cA = s_c[ia(pw[q])], cB = s_c[ib(pw[q])];
-              sep = solve_position_contact(cA.x, cA.y, cB.x, cB.y, P.radius, mA, mB);
-              s_c[ia(pw[q])] = cA;
-              s_c[ib(pw[q])] = cB;
-            }
+            pf2* const pA = reinterpret_cast<pf2*>(s_c + ia(pw[q]));
+            pf2* const pB = reinterpret_cast<pf2*>(s_c + ib(pw[q]));
+            pf2 cA = *pA, cB = *pB;
+            const float sep = solve_position_contact_pk(cA, cB, P.radius, mA, mB);
+            *pA = cA;
+            *pB = cB;
             // order-preserving int of the float for atomicMin
             const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
-            if constexpr (kWideRegMin) kmin[q] = min(kmin[q], key);
-            else atomicMin(&s_pmin[isl(lvis[q])], key);
+            atomicMin(&s_pmin[isl(lvis[q])], key);
           }
         }
-        wave_lds_sync();
-      }
-      if constexpr (kWideRegMin) {
-#pragma unroll
-        for (int q = 0; q < S; ++q)
-          if (lvl(lvis[q]) != kNoLevel) atomicMin(&s_pmin[isl(lvis[q])], kmin[q]);
         wave_lds_sync();
       }
       int km = lane < nisl ? s_pmin[lane] : 0;
@@ -818,15 +611,7 @@ struct SweepState {
 // Records in flight during the sweep: record J + AH is requested while record J is tested,
 // so an LDS broadcast has AH records' worth of VALU work to arrive in (a single record's ~12
 // VALU do not cover the LDS latency with the other waves of the CU reading too).
-#ifndef MACM_SWEEP_AHEAD
-#define MACM_SWEEP_AHEAD 2
-#endif
-constexpr int kSweepAhead = MACM_SWEEP_AHEAD;
-#ifdef MACM_SWEEP_ONE_CHAIN  // A/B knob: the single-chain sweep at NCAP = 64 too
-constexpr bool kSweepTwoChains = false;
-#else
-constexpr bool kSweepTwoChains = true;
-#endif
+constexpr int kSweepAhead = 2;
 
 struct SweepRec {
   float4 fn;
@@ -1340,15 +1125,12 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     // spill step instead (HBM working set, flock_spill.hpp). Nothing has been written to global
     // memory yet, so it starts from the untouched start-of-step state; this wave returns after it.
     // (The scalar DFS of T <= 64 TMW has no degree cap: it walks bit masks.)
-#ifndef MACM_AB_NO_SPILL  // A/B knob: the fast path alone (dense envs then overflow)
     if (touch_over || (!fast_dfs && __builtin_amdgcn_ballot_w64(deg > DEG) != 0ull) || P.force_spill) {
       spill::step_env<OT, true>(P, B, e, cur, actions, obs, nbr_out, rew_out, coll_out, done_out,
                                 reinterpret_cast<unsigned char*>(&s_pool));
       return;
     }
-#endif
   } else {
-#ifndef MACM_AB_NO_SPILL
     // TDM: the same hand-over, after this step's actions, casts and deaths; the spill step does the
     // physics of the living bodies and TDM's env layer (its records in HBM: the pool is smaller)
     if (touch_over || (!fast_dfs && __builtin_amdgcn_ballot_w64(deg > DEG) != 0ull) || P.force_spill) {
@@ -1390,7 +1172,6 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
                                         reinterpret_cast<unsigned char*>(&s_pool), &TP, &TB, &F1, slot);
       return;
     }
-#endif
   }
   if (!fast_dfs && deg > DEG) {
     status |= MACM_ST_DEGREE_OVERFLOW;
@@ -1407,14 +1188,14 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   // envs with the most contacts, which set the kernel's duration (tools/timeline.py:
   // waves end at 15.5 us median, 25 us at the latest). Measured -8% per step at the metric
   // config against no priority; per-island-size or list-size priorities did no better.
-  if (kChainPriority && hasdeg) __builtin_amdgcn_s_setprio(3);
+  if (hasdeg) __builtin_amdgcn_s_setprio(3);
 
   // ---- island DFS in Box2D order (b2World::Solve), serial on lane 0 --------
   // Seeds in body-list order (reverse creation); bodies without touching
   // edges are singleton islands and contribute no contact order, so only
   // bodies in `hasdeg` are walked.
   uint32_t ordv = 0u, lvlv = 0u, kislv = 0u;  // lane k: the k-th contact in island order, its level, island
-  bool lvl_path = kLevels && fast_dfs && T <= 64;  // narrowed after the DFS (largest island)
+  bool lvl_path = fast_dfs && T <= 64;  // narrowed after the DFS (largest island)
   if (fast_dfs) {
     // Wave-uniform (scalar) DFS: bodies' edge masks and contacts' pairs are read from the
     // owning lanes' registers (v_readlane), visited sets are 64-bit masks, and the outputs
@@ -1477,101 +1258,18 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
       ++nisl;
     }
     };
-    // The same walk a popped body at a time (kParDfs, round 5): the body's unvisited edges are the set
-    // bits of one mask, so their places in the island order (the mask's bits below each contact lane),
-    // the bodies they push (lanes whose other body is not yet visited: one ballot) and those bodies'
-    // places on the stack are computed by all lanes at once and stored to LDS (s_ord, s_stack); the
-    // last push is popped next straight from registers. Same order, same pushes, same islands: a
-    // batch's contacts all touch the popped body, so no two of them reach the same other body.
-    auto pdfs = [&](auto wide) {
-      constexpr bool W2 = decltype(wide)::value;
-      // a contact's other body from the popped one: a ^ b ^ popped (one register per contact word)
-      const int cx = (int)((tabv & 0xffffu) ^ (tabv >> 16));
-      const int cx1 = (int)((tabv1 & 0xffffu) ^ (tabv1 >> 16));
-      unsigned long long vis = ~hasdeg, cvis = 0ull, cvis1 = 0ull;
-      for (unsigned long long todo = hasdeg; todo; todo = hasdeg & ~vis) {
-        const int s = 63 - __clzll(todo);
-        icv = writelane_m0(nord, nisl, icv);  // s_ic[nisl]
-        const unsigned long long before = vis;
-        vis |= 1ull << s;
-        int sp = 0, b = s;
-        for (;;) {
-          const unsigned long long m = (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_hi, b) << 32) |
-                                        (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm_lo, b)) & ~cvis;
-          cvis |= m;
-          const bool inm = (m >> lane) & 1ull;
-          const int o = cx ^ b;
-          const bool nw = inm && !((vis >> o) & 1ull);
-          const unsigned long long pm = __builtin_amdgcn_ballot_w64(nw);
-          if (inm) s_ord[nord + mbcnt64(m)] = (uint8_t)lane;
-          if (nw) s_stack[sp + mbcnt64(pm)] = (uint8_t)o;
-          int nm = __popcll(m), np = __popcll(pm);
-          unsigned long long pm1 = 0ull;
-          int o1 = 0;
-          if constexpr (W2) {
-            const unsigned long long m1 =
-                (((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_hi, b) << 32) |
-                 (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(tm1_lo, b)) & ~cvis1;
-            cvis1 |= m1;
-            const bool inm1 = (m1 >> lane) & 1ull;
-            o1 = cx1 ^ b;
-            const bool nw1 = inm1 && !((vis >> o1) & 1ull);
-            pm1 = __builtin_amdgcn_ballot_w64(nw1);
-            if (inm1) s_ord[nord + nm + mbcnt64(m1)] = (uint8_t)(64 + lane);
-            if (nw1) s_stack[sp + np + mbcnt64(pm1)] = (uint8_t)o1;
-            nm += __popcll(m1);
-            np += __popcll(pm1);
-          }
-          nord += nm;
-          if (np) {
-            // the pushed bodies: the lanes (bodies) with a pushed contact among their touching ones
-            const unsigned long long hit = (tmask & pm) | (W2 ? (tmask1 & pm1) : 0ull);
-            vis |= __builtin_amdgcn_ballot_w64(hit != 0ull);
-            sp += np - 1;  // the last push is popped next, from registers
-            b = (W2 && pm1) ? __builtin_amdgcn_readlane(o1, 63 - __clzll(pm1))
-                            : __builtin_amdgcn_readlane(o, 63 - __clzll(pm));
-          } else if (sp > 0) {
-            --sp;
-            wave_lds_sync();
-            b = __builtin_amdgcn_readfirstlane((int)s_stack[sp]);
-          } else {
-            break;
-          }
-        }
-        if (((vis & ~before) >> lane) & 1ull) islv = (uint32_t)nisl;  // s_bisl: the island's bodies
-        ++nisl;
-      }
-    };
-#ifdef MACM_AB_DFS_TWICE  // timing-only A/B knob: the walk's cost (run once more, discarded)
     if (TMW == 2 && T > 64) dfs(BoolC<true>{});
     else dfs(BoolC<false>{});
-    nord = nisl = nb = 0;
-#endif
-    const bool par = kParDfs || (kParDfsWide && TMW == 2 && T > 64);
-    if constexpr (kParDfs) {
-      if (TMW == 2 && T > 64) pdfs(BoolC<true>{});
-      else pdfs(BoolC<false>{});
-    } else if (par) {
-      pdfs(BoolC<true>{});
-    } else {
-      if (TMW == 2 && T > 64) dfs(BoolC<true>{});
-      else dfs(BoolC<false>{});
-    }
     icv = writelane_m0(nord, nisl, icv);
-    if (par) {
-      wave_lds_sync();
-      ordv = lane < nord ? (uint32_t)s_ord[lane] : 0u;  // the level paths read it from registers
-    } else {
-      ibv = writelane_m0(nb, nisl, ibv);
-      const bool wrapped = TMW == 2 && nord > 64;  // entries 0..63 in ordv1, 64.. in ordv
-      if (lane < nord) s_ord[lane] = (uint8_t)(wrapped ? ordv1 : ordv);
-      if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv;
-      if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
-    }
+    ibv = writelane_m0(nb, nisl, ibv);
+    const bool wrapped = TMW == 2 && nord > 64;  // entries 0..63 in ordv1, 64.. in ordv
+    if (lane < nord) s_ord[lane] = (uint8_t)(wrapped ? ordv1 : ordv);
+    if (TMW == 2 && 64 + lane < nord) s_ord[64 + lane] = (uint8_t)ordv;
+    if (lane < nb) s_ibodies[lane] = (uint8_t)bodv;
     if ((hasdeg >> lane) & 1ull) s_bisl[lane] = (uint8_t)islv;
     if (lane <= nisl) {
       s_ic[lane] = (uint16_t)icv;
-      if (!par) s_ib[lane] = (uint8_t)ibv;
+      s_ib[lane] = (uint8_t)ibv;
     }
     if (lane == 0) {
       s_nisl = nisl;
@@ -1654,21 +1352,18 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   // islands go through LDS in Box2D's order.
   // any 2..KREC-contact island in this wave (wave-uniform; nisl <= ICAP < W, one island per lane)
   const int lsz = lane < nisl ? s_ic[lane + 1] - s_ic[lane] : 0;
-  const bool krec_wave = kMergeSingletons && __builtin_amdgcn_ballot_w64(lsz >= 2 && lsz <= KREC) != 0ull;
+  const bool krec_wave = __builtin_amdgcn_ballot_w64(lsz >= 2 && lsz <= KREC) != 0ull;
   // levels pay off once an island is longer than the register-record path takes (KREC): islands
   // of up to KREC contacts run faster one lane each. Only then are the levels computed: a scalar
   // walk of the contacts in island order (lane b of lastv: 1 + the level of the last contact
   // touching body b).
-  const bool big_isl = __builtin_amdgcn_ballot_w64(lsz > MACM_LEVELS_MIN_ISLAND) != 0ull;
+  const bool big_isl = __builtin_amdgcn_ballot_w64(lsz > kLevelsMinIsland) != 0ull;
   lvl_path = lvl_path && big_isl;
   // More than 64 touching contacts (converged flocks: islands of 60-100 contacts, tests/gs_depth.py):
   // the same levels with S = 2 or 4 contacts per lane (WideLevels below); the per-island lanes
   // would walk such an island serially, ~470 cycles per contact update
-  const bool lvl_wide = kWideLevels && T > 64 && big_isl;
+  const bool lvl_wide = T > 64 && big_isl;
   const bool skip_isl = lvl_path || lvl_wide;  // no per-island lanes: the level paths solve every island
-  // The widest chains (T > 64 solved by levels, converged flocks) set a closed loop's step time: the
-  // other waves with contacts step down to priority 2 for the rest of the chain (A/B knob).
-  if (kWidePriority && kChainPriority && hasdeg && !lvl_wide) __builtin_amdgcn_s_setprio(2);
   // ---- integrate positions --------------------------------------------------
   float cx = p.x, cy = p.y;
   auto integrate_positions = [&]() {
@@ -1711,17 +1406,6 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     if (lvl_path) {
       const uint32_t tabv = lane < T ? s_tab[lane] : 0u;
       uint32_t lastv = 0u;
-#ifdef MACM_AB_LVL_TWICE  // timing-only A/B knob: the level walk's cost (run once more, discarded)
-      for (int k = 0; k < T; ++k) {
-        const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
-        const int a = ab & 0xffffu, bb = ab >> 16;
-        const int l = max(__builtin_amdgcn_readlane(lastv, a), __builtin_amdgcn_readlane(lastv, bb));
-        lastv = writelane_m0(l + 1, a, lastv);
-        lastv = writelane_m0(l + 1, bb, lastv);
-        lvlv = writelane_m0(l, k, lvlv);
-      }
-      lastv = 0u;
-#endif
       for (int k = 0; k < T; ++k) {
         const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane(tabv, __builtin_amdgcn_readlane(ordv, k));
         const int a = ab & 0xffffu, bb = ab >> 16;
@@ -1767,38 +1451,21 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         s_v[lb] = make_float2(vBx, vBy);
       }
     } else if (lvl_path) {
-      // the warm-start pass and the velocity passes as separate loops: no branch inside a level step
-#if MACM_BRANCHFREE_WAVE_LEVELS
-      // every lane runs every level step, the lanes outside the level on their own dummy slot in
+      // the warm-start pass and the velocity passes as separate loops: no branch inside a level step.
+      // Every lane runs every level step, the lanes outside the level on their own dummy slot in
       // s_tm (the DFS masks: dead until the next step's Collide), so a level step has no exec-mask
       // branch; only the level's lanes keep their impulses
-      float2* const pdd = reinterpret_cast<float2*>(s_tm) + (kSharedDummy ? 0 : lane);
+      float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
       float2* const pda = lhas ? s_v + la : pdd;
       float2* const pdb = lhas ? s_v + lb : pdd;
       const int mylvl = lhas ? lvl : -1;
       auto lpass = [&](auto warm) {
-#if MACM_WAVE_LEVEL_ADDR_AHEAD
         // the next level's addresses are selected while this level solves (off the read's path);
         // two level steps per iteration (no register rotation or back-edge per level, as kernel B)
         float2* pa = mylvl == 0 ? pda : pdd;
         float2* pb = mylvl == 0 ? pdb : pdd;
         auto step = [&](bool onc, bool onn) {
           float nl = lln, nt = llt;
-          if constexpr (kPackedLevels) {
-            pf2 vA = *reinterpret_cast<pf2*>(pa), vB = *reinterpret_cast<pf2*>(pb);
-            float2* const na = onn ? pda : pdd;
-            float2* const nb = onn ? pdb : pdd;
-            if constexpr (decltype(warm)::value) warm_start_contact_pk(vA, vB, lnx, lny, nl, nt, mA, mB);
-            else solve_velocity_contact_pk(vA, vB, lnx, lny, nl, nt, mA, mB, kmass, friction);
-            *reinterpret_cast<pf2*>(pa) = vA;
-            *reinterpret_cast<pf2*>(pb) = vB;
-            lln = onc ? nl : lln;
-            llt = onc ? nt : llt;
-            pa = na;
-            pb = nb;
-            level_sync();
-            return;
-          }
           const float2 vA0 = *pa, vB0 = *pb;
           float2* const na = onn ? pda : pdd;
           float2* const nb = onn ? pdb : pdd;
@@ -1814,46 +1481,12 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
           level_sync();
         };
         int l = 0;
-#if MACM_WAVE_LEVEL_UNROLL == 2
         for (; l + 1 < dmulti; l += 2) {
           step(mylvl == l, mylvl == l + 1);
           step(mylvl == l + 1, mylvl == l + 2);
         }
-#endif
         for (; l < dmulti; ++l) step(mylvl == l, mylvl == l + 1);
-#else
-        for (int l = 0; l < dmulti; ++l) {
-          const bool on = mylvl == l;
-          float2* const pa = on ? pda : pdd;
-          float2* const pb = on ? pdb : pdd;
-          const float2 vA0 = *pa, vB0 = *pb;
-          float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-          float nl = lln, nt = llt;
-          if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB);
-          else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, nl, nt, mA, mB, kmass, friction);
-          *pa = make_float2(vAx, vAy);
-          *pb = make_float2(vBx, vBy);
-          lln = on ? nl : lln;
-          llt = on ? nt : llt;
-          level_sync();
-        }
-#endif
       };
-#else
-      auto lpass = [&](auto warm) {
-        for (int l = 0; l < dmulti; ++l) {
-          if (lhas && lvl == l) {
-            const float2 vA0 = s_v[la], vB0 = s_v[lb];
-            float vAx = vA0.x, vAy = vA0.y, vBx = vB0.x, vBy = vB0.y;
-            if constexpr (decltype(warm)::value) warm_start_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB);
-            else solve_velocity_contact(vAx, vAy, vBx, vBy, lnx, lny, lln, llt, mA, mB, kmass, friction);
-            s_v[la] = make_float2(vAx, vAy);
-            s_v[lb] = make_float2(vBx, vBy);
-          }
-          level_sync();
-        }
-      };
-#endif
       if (P.warm_starting) lpass(BoolC<true>{});
       for (int it = 0; it < P.vel_iters; ++it) lpass(BoolC<false>{});
     }
@@ -1994,38 +1627,27 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         for (int it = 0; it < P.pos_iters && done != islm; ++it) {
           if (lane < nisl) s_pmin[lane] = __float_as_int(0.0f);
           level_sync();
-#if MACM_BRANCHFREE_WAVE_POS
           // branch-free level steps as in the velocity passes: the lanes outside the level (or of
           // an island that has left) correct their own dummy slot in s_tm and take their minimum
           // into its first word
           const int mylvl = (lhas && !((done >> lisl) & 1ull)) ? lvl : -1;
-          float2* const pdd = reinterpret_cast<float2*>(s_tm) + (kSharedDummy ? 0 : lane);
+          float2* const pdd = reinterpret_cast<float2*>(s_tm) + lane;
           float2* const pda = lhas ? s_c + la : pdd;
           float2* const pdb = lhas ? s_c + lb : pdd;
-          // a dummy lane's minimum: its own word (past the shared slot), atomics on one address serialise
-          int* const pmd = kSharedDummy ? reinterpret_cast<int*>(s_tm) + 2 + lane : reinterpret_cast<int*>(pdd);
+          int* const pmd = reinterpret_cast<int*>(pdd);  // a dummy lane's minimum: its own word
           int* const pmi = lhas ? s_pmin + lisl : pmd;
-#if MACM_WAVE_LEVEL_ADDR_AHEAD
           float2* pa = mylvl == 0 ? pda : pdd;
           float2* pb = mylvl == 0 ? pdb : pdd;
           int* pm = mylvl == 0 ? pmi : pmd;
           auto pstep = [&](bool onn) {
-            float sep;
             float2* const na = onn ? pda : pdd;
             float2* const nb = onn ? pdb : pdd;
             int* const nm = onn ? pmi : pmd;
-            if constexpr (kPackedLevels) {
-              pf2 cA = *reinterpret_cast<pf2*>(pa), cB = *reinterpret_cast<pf2*>(pb);
-              sep = solve_position_contact_pk(cA, cB, P.radius, mA, mB);
-              *reinterpret_cast<pf2*>(pa) = cA;
-              *reinterpret_cast<pf2*>(pb) = cB;
-            } else {
-              const float2 cA0 = *pa, cB0 = *pb;
-              float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-              sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-              *pa = make_float2(cAx, cAy);
-              *pb = make_float2(cBx, cBy);
-            }
+            const float2 cA0 = *pa, cB0 = *pb;
+            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
+            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
+            *pa = make_float2(cAx, cAy);
+            *pb = make_float2(cBx, cBy);
             // order-preserving int of the float for atomicMin
             const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
             atomicMin(pm, key);
@@ -2035,45 +1657,11 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
             level_sync();
           };
           int l = 0;
-#if MACM_WAVE_LEVEL_UNROLL == 2
           for (; l + 1 < dmulti; l += 2) {
             pstep(mylvl == l + 1);
             pstep(mylvl == l + 2);
           }
-#endif
           for (; l < dmulti; ++l) pstep(mylvl == l + 1);
-#else
-          for (int l = 0; l < dmulti; ++l) {
-            const bool on = mylvl == l;
-            float2* const pa = on ? pda : pdd;
-            float2* const pb = on ? pdb : pdd;
-            int* const pm = on ? pmi : pmd;
-            const float2 cA0 = *pa, cB0 = *pb;
-            float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-            const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-            *pa = make_float2(cAx, cAy);
-            *pb = make_float2(cBx, cBy);
-            // order-preserving int of the float for atomicMin
-            const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
-            atomicMin(pm, key);
-            level_sync();
-          }
-#endif
-#else
-          for (int l = 0; l < dmulti; ++l) {
-            if (lhas && lvl == l && !((done >> lisl) & 1ull)) {
-              const float2 cA0 = s_c[la], cB0 = s_c[lb];
-              float cAx = cA0.x, cAy = cA0.y, cBx = cB0.x, cBy = cB0.y;
-              const float sep = solve_position_contact(cAx, cAy, cBx, cBy, P.radius, mA, mB);
-              s_c[la] = make_float2(cAx, cAy);
-              s_c[lb] = make_float2(cBx, cBy);
-              // order-preserving int of the float for atomicMin
-              const int key = __float_as_int(sep) >= 0 ? __float_as_int(sep) : (__float_as_int(sep) ^ 0x7fffffff);
-              atomicMin(&s_pmin[lisl], key);
-            }
-            level_sync();
-          }
-#endif
           int km = lane < nisl ? s_pmin[lane] : 0;
           km = km >= 0 ? km : (km ^ 0x7fffffff);
           done |= __builtin_amdgcn_ballot_w64(lane < nisl && !((done >> lane) & 1ull) &&
@@ -2158,8 +1746,8 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   // After the chain a wave with touching contacts stays above the contact-free ones, and one
   // with >= 3 touching contacts (the envs that end last) above those: -2% per step against a
   // single level (profiles/r01/ab2 s24/s25; thresholds 2 and 4, or a third level, did no better).
-  if (kChainPriority && hasdeg) {
-    if (T >= MACM_PRIO2_T) __builtin_amdgcn_s_setprio(2);
+  if (hasdeg) {
+    if (T >= kPrio2T) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_s_setprio(1);
   }
   // ---- per-body sleep clock ---------------------------------------------------
@@ -2235,7 +1823,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   sw.ov_hi = 0u;
   sw.best = __builtin_inff();
   sw.bj = lane == 0 ? 1 : 0;
-  if constexpr (NCAP == 64 && !kT && kSweepTwoChains) {
+  if constexpr (NCAP == 64 && !kT) {  // two interleaved chains
     constexpr int AH2 = 2 * kSweepAhead;  // records in flight (two per step)
     SweepState2 s2;
     s2.ov_lo = 0u;
@@ -2366,27 +1954,17 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
         TB.snap_out[ag] = make_float4(c.x, c.y, ang, act ? 1.0f : 0.0f);
       }
     } else {
-    const size_t rows = (size_t)e * N * (N - 1);
-    OT* const obs_e = obs ? obs + rows * 4 : nullptr;
-    uint8_t* const mask_e = TB.mask_out ? TB.mask_out + rows : nullptr;
-    bool staged = false;
-    if constexpr (sizeof(OT) == 4 && kTdmObsStaged) {
-      staged = tdm_obs_stage_bytes(N) <= (int)sizeof(Pool);  // the contact arrays are dead here
-      if (staged)
-        tdm_obs_staged<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<unsigned char*>(&s_pool));
-    }
-    if constexpr (sizeof(OT) == 4 && kTdmObsRowBlocks) {
-      if (!staged && tdm_obs_rb_stage_bytes(N) <= (int)sizeof(Pool)) {  // the contact arrays are dead here
-        tdm_obs_rowblocks<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<float4*>(&s_pool));
-        staged = true;
+      const size_t rows = (size_t)e * N * (N - 1);
+      OT* const obs_e = obs ? obs + rows * 4 : nullptr;
+      uint8_t* const mask_e = TB.mask_out ? TB.mask_out + rows : nullptr;
+      bool staged = false;
+      if constexpr (sizeof(OT) == 4) {
+        if (tdm_obs_rb_stage_bytes(N) <= (int)sizeof(Pool)) {  // the contact arrays are dead here
+          tdm_obs_rowblocks<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<float4*>(&s_pool));
+          staged = true;
+        }
       }
-    }
-    if (!staged) {
-      if (kTdmMaskStaged && N * (N - 1) <= (int)sizeof(Pool))  // the contact arrays are dead here
-        tdm_obs_pairs_smask<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang, reinterpret_cast<uint8_t*>(&s_pool));
-      else
-        MACM_TDM_OBS<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang);
-    }
+      if (!staged) tdm_obs_pairs<OT>(obs_e, mask_e, N, lane, livem, TP, s_c, s_ang);
     }
   }
   STAMP(12);
@@ -2465,8 +2043,6 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
 }
 
 #ifdef MACM_ROLLOUT_TU
-hipError_t launch_wait_count(const unsigned long long* ctr, unsigned long long target, uint32_t* host_status,
-                             hipStream_t s);  // flock_step_wg.hip
 
 // nsteps consecutive steps of env blockIdx.x in one launch (macm_world_rollout): actions of step k
 // at actions + k * astride bytes ([K, E, N, A]), outputs overwritten each step (the last step's
@@ -2478,10 +2054,8 @@ hipError_t launch_wait_count(const unsigned long long* ctr, unsigned long long t
 // (flock_rollout_w64.hip, -mllvm -disable-machine-licm): with the step inside a loop, machine
 // LICM hoists the f64 polynomial constants of the trig and atan2 code out of it and the
 // register allocator spills them (327 VGPRs of spills; none without the hoisting).
-#ifndef MACM_ROLL_OPAQUE_LANE  // A/B knob: 0 none, 1 TDM rollouts, 2 TDM and Flock rollouts
-#define MACM_ROLL_OPAQUE_LANE 1
-#endif
-constexpr bool kRollOpaqueLaneTdm = MACM_ROLL_OPAQUE_LANE >= 1, kRollOpaqueLaneFlock = MACM_ROLL_OPAQUE_LANE >= 2;
+// The lane index is made opaque to the compiler in TDM rollouts only (Flock rollouts: measured no
+// better, round 4).
 template <typename OT>
 struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   StepParams P;
@@ -2503,8 +2077,12 @@ struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   // trajectory form: every output (and, in the closed loop, the bot's actions: [K + 1, E, N, A],
   // step k reading row k and writing row k + 1) advances one row per step
   int traj;
-  int sched_off;  // a balanced launch steps envs order[sched_off + blockIdx.x] (solo split, below)
-  unsigned long long* solo_started;  // SOLO: the start counter (SoloLaunch::started)
+  // A balanced launch steps envs order[sched_off + blockIdx.x]; sched_off is 0 since the solo split
+  // was removed (round 6), and kept with `reserved` so the kernel's argument layout (and with it its
+  // register allocation) stays the measured one: without them the driver window ran 1.1% slower, with
+  // them 0.3% (in noise) against the library before the removal (profiles/r06/abtests/cleanup/).
+  int sched_off;
+  unsigned long long* reserved;
 };
 
 // [K, ...] row k of an output (trajectory form); NULL stays NULL
@@ -2524,16 +2102,7 @@ __device__ __forceinline__ T* traj_row(T* p, size_t k, size_t per_step) {
 // costs ~6 us per launch (+0.3 us per step of a 20-step rollout, no gain there), so rollouts shorter
 // than kRollBalanceMinSteps keep wave b on env b. Claiming envs by SIMD id at the wave's start
 // (3 device-scope atomics per wave on two counters) balanced as well but cost ~50 us per launch.
-// A/B knob -DMACM_NO_ROLL_BALANCE: wave b steps env b.
-#ifdef MACM_NO_ROLL_BALANCE
-constexpr bool kRollBalance = false;
-#else
-constexpr bool kRollBalance = true;
-#endif
-#ifndef MACM_ROLL_BALANCE_MIN_STEPS
-#define MACM_ROLL_BALANCE_MIN_STEPS 32
-#endif
-constexpr int kRollBalanceMinSteps = MACM_ROLL_BALANCE_MIN_STEPS;
+constexpr int kRollBalanceMinSteps = 32;
 constexpr int kSchedMaxSize = 4095;
 
 // order[0..E): the envs by descending contact-list size (ccount, clamped to C); one workgroup.
@@ -2564,25 +2133,12 @@ __global__ __launch_bounds__(1024) void rollout_sched(const uint32_t* __restrict
   for (int e = tid; e < E; e += BS) order[atomicAdd(&s_h[max(0, min((int)ccount[e], C))], 1u)] = (uint32_t)e;
 }
 
-// Solo waves (round 5). Two heavy envs that share a SIMD slow each other's latency-bound chains, and
-// the balanced order alone still co-schedules the heaviest envs with three other waves (M closed
-// loop: ~500 cycles per level step shared, ~290 alone). A balanced rollout of at least
-// kRollBalanceMinSteps therefore launches its `solo` heaviest envs (order[0 .. solo)) in a kernel
-// instance whose waves own their SIMD — SOLO clobbers an accumulation register, so the register
-// file of a SIMD holds one such wave (512 of its registers allocated) — on a high-priority stream
-// forked from the caller's, and the other envs (order[solo ..)) in the ordinary instance. Which SIMD
-// a wave gets never changes an env's arithmetic; if the ordinary launch happened to be dispatched
-// first, the solo waves would only wait for free SIMDs (no wave waits on another).
-template <int MODE, int NCAP, typename OT, bool SCAL = false, bool SOLO = false>
-__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : 4))) void env_rollout_w64(
-    RolloutArgs<OT> A0) {
-  if constexpr (SOLO) {
-    asm volatile("" ::: "a255");  // one wave per SIMD (occupancy 1)
-    if (threadIdx.x == 0)  // this wave holds its SIMD: the ordinary launch may be dispatched
-      __hip_atomic_fetch_add(A0.solo_started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+// A balanced rollout's heaviest envs in waves that own their SIMD, on a stream of their own ("solo"
+// waves, round 5), measured slower and were removed in round 6 (profiles/r05/abtests/).
+template <int MODE, int NCAP, typename OT, bool SCAL = false>
+__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_rollout_w64(RolloutArgs<OT> A0) {
   const int nsteps = A0.nsteps;
-  const bool bal = kRollBalance && A0.B.sched && nsteps >= kRollBalanceMinSteps;  // as in launch_roll
+  const bool bal = A0.B.sched && nsteps >= kRollBalanceMinSteps;  // as in launch_roll
   const int env = bal ? (int)A0.B.sched[A0.sched_off + blockIdx.x] : (int)blockIdx.x;
   for (int k = 0; k < nsteps; ++k) {
     // each step reads its parameters from the kernel arguments afresh, through a pointer the
@@ -2611,7 +2167,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : 4)
     // mask of the step is hoisted out of it and held across all K steps. The TDM step then ran out
     // of its 128 VGPRs and kept 7 of them in scratch, re-read every step (rollout: 28 B per lane).
     int sl = (int)threadIdx.x;
-    if (MODE == kTdm ? kRollOpaqueLaneTdm : kRollOpaqueLaneFlock) asm volatile("" : "+v"(sl));
+    if constexpr (MODE == kTdm) asm volatile("" : "+v"(sl));
     step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, TB, A.cur ^ (k & 1),
                                         pol_in ? pol_in : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
                                         obs, traj_row(A.nbr_out, kr, EN), traj_row(A.rew_out, kr, EN),
@@ -2639,11 +2195,10 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : 4)
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
 static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStream_t s, const StepParams& P,
                         const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
-                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
-                        SoloLaunch* solo = nullptr) {
+                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
-  const bool bal = kRollBalance && B.sched && nsteps >= kRollBalanceMinSteps;
+  const bool bal = B.sched && nsteps >= kRollBalanceMinSteps;
   if (bal) {
     // list sizes above kSchedMaxSize share the top bucket (any order among them is a valid order;
     // the histogram stays within 16 KB of LDS whatever max_contacts a world was given)
@@ -2652,41 +2207,7 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
                        reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, CB, nullptr);
     if (hipPeekAtLastError() != hipSuccess) return;  // no rollout on a stale order (the caller reports it)
   }
-  RolloutArgs<OT> A{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol, traj, 0,
-                    solo ? solo->started : nullptr};
-  int H = 0;
-  if constexpr (MODE == kFlock && NCAP == 64 && sizeof(OT) == 4) {
-    if (bal && solo && solo->stream && solo->started && solo->n > 0) H = solo->n < P.n_envs ? solo->n : 0;
-  }
-  if (H > 0) {
-    if constexpr (MODE == kFlock && NCAP == 64 && sizeof(OT) == 4) {
-      if (hipEventRecord(solo->fork, s) != hipSuccess || hipStreamWaitEvent(solo->stream, solo->fork, 0) != hipSuccess)
-        return;
-      hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL, true>), dim3(H), dim3(W), 0, solo->stream, A);
-      // the watcher (flock_step_wg.hip wait_count) is launched only behind a solo launch that was
-      // accepted: its H waves start (they wait for nothing) and end it
-      A.sched_off = H;
-      if (hipPeekAtLastError() != hipSuccess) {  // solo launch refused: the error stays for the caller
-        (void)hipEventRecord(solo->join, solo->stream);
-        (void)hipStreamWaitEvent(s, solo->join, 0);
-        return;
-      }
-      solo->expected += (unsigned long long)H;
-      // a watcher that cannot be launched (its error is consumed here): the ordinary instance runs
-      // after the solo one instead of beside it, so every env is still stepped
-      const bool watched = launch_wait_count(solo->started, solo->expected, B.host_status, s) == hipSuccess;
-      if (!watched) {
-        (void)hipEventRecord(solo->join, solo->stream);
-        (void)hipStreamWaitEvent(s, solo->join, 0);
-      }
-      hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs - H), dim3(W), 0, s, A);
-      if (watched) {  // joined (no unjoined work on the solo stream)
-        (void)hipEventRecord(solo->join, solo->stream);
-        (void)hipStreamWaitEvent(s, solo->join, 0);
-      }
-    }
-    return;
-  }
+  RolloutArgs<OT> A{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol, traj, 0, nullptr};
   hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s, A);
 }
 
@@ -2700,7 +2221,7 @@ hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int 
 
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
-                              int nsteps, unsigned long long astride, int traj, SoloLaunch* solo) {
+                              int nsteps, unsigned long long astride, int traj) {
   const TdmParams TP{};
   const TdmBuffers TB{};
   const bool small = P.n_agents <= 32;
@@ -2714,10 +2235,9 @@ hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cu
       launch_roll<kFlock, 32, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
     else if (P.n_envs >= kScalarSweepMinEnvs)
       launch_roll<kFlock, 64, float, true>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll,
-                                           done, solo);
+                                           done);
     else
-      launch_roll<kFlock, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done,
-                                     solo);
+      launch_roll<kFlock, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nbr, rew, coll, done);
   }
   return hipGetLastError();
 }
@@ -2906,7 +2426,7 @@ __global__ __launch_bounds__(W) void tdm_init_w64(StepParams P, WorldBuffers B, 
   const unsigned long long livem = __ballot(act);
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
-  MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+  tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
                    s_p, s_a);
   if (lane == 0) {
     B.ccount[cur][e] = total;
@@ -2941,7 +2461,7 @@ __global__ __launch_bounds__(W) void tdm_observe_w64(StepParams P, WorldBuffers 
   const unsigned long long livem = __ballot(live);
   __syncthreads();
   const size_t rows = (size_t)e * N * (N - 1);
-  MACM_TDM_OBS<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
+  tdm_obs_pairs<OT>(obs ? obs + rows * 4 : nullptr, TB.mask_out ? TB.mask_out + rows : nullptr, N, lane, livem, TP,
                    s_p, s_a);
 }
 

@@ -35,14 +35,9 @@ hipError_t launch_env_order(const uint32_t* ccount, uint32_t* order, int E, int 
 // steps env order[b]. Kernels A and C take several dispatch rounds (more workgroups than fit the
 // chip at once), so the heaviest envs start in the first round instead of ending a late one, and
 // kernel B's heaviest waves start one per SIMD. Any order gives the same results: every env is
-// stepped by exactly one workgroup of each kernel. A/B knob -DMACM_NO_WG_ENV_ORDER: b steps env b.
-#ifdef MACM_NO_WG_ENV_ORDER
-constexpr bool kWgEnvOrder = false;
-#else
-constexpr bool kWgEnvOrder = true;
-#endif
+// stepped by exactly one workgroup of each kernel.
 __device__ __forceinline__ int wg_env(const WorldBuffers& B) {
-  return (kWgEnvOrder && B.sched) ? (int)B.sched[blockIdx.x] : (int)blockIdx.x;
+  return B.sched ? (int)B.sched[blockIdx.x] : (int)blockIdx.x;
 }
 
 // ---- the B -> C handoff (flock_common.hpp Handoff) -------------------------------------------------
@@ -125,66 +120,20 @@ constexpr int kNewSlots = 8;  // kernel C, all-pairs sweep: new partners kept pe
 // first (union-find over the touching contacts, in parallel), each gets its contact and body
 // ranges from its size and seed order, and then one thread walks each island, all islands at
 // once, with the serial walk's code: the same order, levels and records as one thread walking
-// them all in turn. -DMACM_NO_ISLAND_DFS: thread 0 walks every island. Islands of more than
-// kBigIsland contacts get a whole wave each (the dense path's wave-parallel walk).
-#ifndef MACM_BIG_ISLAND
-#define MACM_BIG_ISLAND 48
-#endif
-constexpr int kBigIsland = MACM_BIG_ISLAND;
-#ifdef MACM_NO_ISLAND_DFS
-constexpr bool kIslandDfs = false;
-#else
-constexpr bool kIslandDfs = true;
-#endif
-#ifdef MACM_NO_DFS_PRIORITY
-constexpr bool kDfsPriority = false;
-#else
-constexpr bool kDfsPriority = true;
-#endif
+// them all in turn. Islands of more than kBigIsland contacts get a whole wave each (the dense
+// path's wave-parallel walk). The walks run at issue priority 3.
+constexpr int kBigIsland = 48;
 // Dense envs (the wave-parallel walk: average touching degree >= 4, e.g. C5) take the island DFS,
 // the Gauss-Seidel levels and the level-ordered records in their own kernel (flock_dfs_wg: one wave
 // per env, ~45 KB of LDS, so 3 envs share a CU), instead of in kernel A, whose 78 KB block would
-// hold a CU while one of its 16 waves walks. -DMACM_NO_DFS_KERNEL: kernel A walks them.
-#ifdef MACM_NO_DFS_KERNEL
-constexpr bool kDfsKernel = false;
-#else
-constexpr bool kDfsKernel = true;
-#endif
-// Issue priority 3 for the island-first walks (sparse worlds, kIslandDfs). -DMACM_NO_ISL_PRIORITY: off.
-#ifdef MACM_NO_ISL_PRIORITY
-constexpr bool kIslPriority = false;
-#else
-constexpr bool kIslPriority = true;
-#endif
-// Kernel B: issue priority by the env's Gauss-Seidel depth (round 4). Off since the packed level
-// steps (round 5: C3 window -1.3 / -1.7%, C3 closed loop -1.9%, C5 even; profiles/r05/abtests/
-// solve_priority). -DMACM_SOLVE_PRIORITY: on.
-#ifdef MACM_SOLVE_PRIORITY
-constexpr bool kSolvePriority = true;
-#else
-constexpr bool kSolvePriority = false;
-#endif
+// hold a CU while one of its 16 waves walks.
+// Kernel B's issue priority by the env's Gauss-Seidel depth (round 4) was dropped with the packed
+// level steps (round 5: C3 window -1.3 / -1.7%, C3 closed loop -1.9%, C5 even without it;
+// profiles/r05/abtests/solve_priority).
 constexpr int kDfsPending = -2;  // x_nisl: the env's DFS is flock_dfs_wg's
-#ifndef MACM_SERIAL_PREFETCH  // A/B knob: kernel A's one-thread island walks read the next edge ahead
-#define MACM_SERIAL_PREFETCH 1
-#endif
-constexpr bool kSerialPrefetch = MACM_SERIAL_PREFETCH != 0;
-// Kernel B's level steps: the idle lanes share one dummy slot (an LDS broadcast; A/B knob
-// -DMACM_LANE_DUMMY: a slot per lane, round 3); their position minima keep a word each.
-#ifdef MACM_LANE_DUMMY
-constexpr bool kSharedDummy = false;
-#else
-constexpr bool kSharedDummy = true;
-#endif
-#ifndef MACM_SWEEP_PIPE  // A/B knob: kernel C's strip-cell candidate loop: entries read ahead (1), entries
-                         // and AABBs read ahead (2), in order (0)
-#define MACM_SWEEP_PIPE 1
-#endif
-constexpr bool kSweepPipe = MACM_SWEEP_PIPE != 0, kSweepPipe2 = MACM_SWEEP_PIPE == 2;
-#ifndef MACM_DFS_BATCH  // A/B knob: contacts per lane whose loads flock_dfs_wg's record pass issues together
-#define MACM_DFS_BATCH 8
-#endif
-constexpr int kDfsBatch = MACM_DFS_BATCH;
+// Kernel B's level steps: the idle lanes share one dummy slot (an LDS broadcast; a slot per lane,
+// round 3, was slower); their position minima keep a word each.
+constexpr int kDfsBatch = 8;  // contacts per lane whose loads flock_dfs_wg's record pass issues together
 
 // Diagnostic build only (-DMACM_STAMPS): thread 0 records s_memtime after the
 // block barrier that closes each phase into B.stamps[e][0..12] (tools/phase_profile.py
@@ -204,22 +153,14 @@ constexpr int kDfsBatch = MACM_DFS_BATCH;
 
 __device__ __forceinline__ float bmin(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float bmax(float a, float b) { return a > b ? a : b; }
-__device__ __forceinline__ float bclamp(float a, float lo, float hi) { return bmax(lo, bmin(a, hi)); }
 // The contact solvers' clamps as single v_min_f32 / v_max_f32 instead of compare + select
 // (b2Min / b2Max): they sit on the serial Gauss-Seidel chain. For non-NaN operands the two
 // forms differ only in the sign of a zero result (b2Max(-0, +0) is +0, v_max may give -0);
 // a zero impulse or velocity of either sign leaves every later value the same, so only
 // zero signs can differ (as they already do through the angular terms).
-#ifdef MACM_EXACT_ZERO_SIGNS
-__device__ __forceinline__ float smax(float a, float b) { return bmax(a, b); }
-__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return bclamp(a, lo, hi); }
-#elif defined(MACM_NO_MED3)
-__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ float sclamp(float a, float lo, float hi) { return fmaxf(lo, fminf(a, hi)); }
-#else  // one v_med3_f32 (as in flock_step_w64.hip)
+// sclamp as one v_med3_f32 (as in flock_step_w64.hip)
 __device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
 __device__ __forceinline__ float sclamp(float a, float lo, float hi) { return __builtin_amdgcn_fmed3f(a, lo, hi); }
-#endif
 __device__ __forceinline__ bool overlap(float4 a, float4 b) {  // b2TestOverlap
   const float d1x = b.x - a.z, d1y = b.y - a.w;
   const float d2x = a.x - b.z, d2y = a.y - b.w;
@@ -420,10 +361,7 @@ __global__ __launch_bounds__(1024) void flock_observe_wg(StepParams P, WorldBuff
 // touching contact), so an island walk reads an edge and its other body in one LDS round trip
 // instead of two (edge, then the contact's pair). Above it (78 KB of LDS at N = 1024, two blocks
 // per CU) the walks read the pair.
-#ifndef MACM_OTH_MAX_AGENTS  // A/B knob
-#define MACM_OTH_MAX_AGENTS 512
-#endif
-constexpr int kOthMaxAgents = MACM_OTH_MAX_AGENTS;
+constexpr int kOthMaxAgents = 512;
 struct WgLayoutA {
   int c, deg, csr_off, todo, ord, ib, ibod, stk, ic, scan, misc, tab, adj, oth, total;
 };
@@ -679,12 +617,8 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   WSTAMP(19);
 
   // ---- island DFS in Box2D order (as in flock_step_wg) ---------------------------------
-#ifdef MACM_AB_PAR_DFS_ALWAYS
-  const bool par_dfs = true;
-#else
   const bool par_dfs = 2 * T >= 4 * N;
-#endif
-  if (kDfsKernel && par_dfs) {
+  if (par_dfs) {
     // the touching contacts, the CSR offsets and every edge with its other body to HBM; the
     // integrated velocities as after the walk; flock_dfs_wg does the rest of this kernel
     const int IS = wg_isl_stride(N);
@@ -835,22 +769,15 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       // the next edge and its other body are read one edge ahead (the edges are not written
       // during the walk): an edge then costs one dependent LDS round trip (its other body's word)
       int tn = 0, on = 0;
-      if (kSerialPrefetch && e0 < e1) {
+      if (e0 < e1) {
         tn = s_adj[e0];
         on = edge_other(HO, e0, tn, b);
       }
       for (int q = e0; q < e1; ++q) {
-        int t, o;
-        if (kSerialPrefetch) {
-          t = tn;
-          o = on;
-          const int qn = min(q + 1, e1 - 1);
-          tn = s_adj[qn];
-          on = edge_other(HO, qn, tn, b);
-        } else {
-          t = s_adj[q];
-          o = edge_other(HO, q, t, b);
-        }
+        const int t = tn, o = on;
+        const int qn = min(q + 1, e1 - 1);
+        tn = s_adj[qn];
+        on = edge_other(HO, qn, tn, b);
         const int so = s_last[o];
         const int oe0 = s_off[o], oe1 = s_off[o + 1];
         if (so & kPopped) continue;
@@ -872,7 +799,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
   };
 #define MACM_WALK(f, ...) (s_oth ? f(std::true_type{}, __VA_ARGS__) : f(std::false_type{}, __VA_ARGS__))
   // Sparse worlds: islands first, then one thread per island (see kIslandDfs).
-  const bool isl_dfs = kIslandDfs && !par_dfs && 2 * tcap >= 4 * N;
+  const bool isl_dfs = !par_dfs && 2 * tcap >= 4 * N;
   if (isl_dfs) {
     // Union-find labels, hooking the lower root under the higher and jumping to the roots after
     // every round, so each component's root is its highest body: the seed the serial walk would
@@ -962,7 +889,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     __syncthreads();
     // the walks are latency chains while other blocks' waves share the SIMDs: issue priority, as
     // for the serial walk below
-    if (kIslPriority) __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(3);
     if (wid < nbw) {
       const int sd = (int)job.x;
       int nord = (int)(job.y & 0xffffu), nb = (int)(job.y >> 16), dmax = 0;
@@ -976,12 +903,12 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
       MACM_WALK(serial_walk, seed, nord, nb, dmax);
       atomicMax(&s_misc[1], dmax);
     }
-    if (kIslPriority) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   }
   // The DFS is one latency chain on one wave while the block's other waves wait at the barrier
   // and other blocks' waves share the SIMD: raise its issue priority for the walk (as the wave
   // kernel does for its chain).
-  if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(3);
+  if (tid < W) __builtin_amdgcn_s_setprio(3);
   if (!par_dfs && !isl_dfs && tid == 0) {  // -DMACM_NO_ISLAND_DFS: one thread walks every island
     int nord = 0, nisl = 0, nb = 0, dmax = 0;
     for (int w = (N + 63) / 64 - 1; w >= 0;) {
@@ -1028,7 +955,7 @@ __global__ __launch_bounds__(1024) void flock_step_wg_a(StepParams P, WorldBuffe
     }
   }
 #undef MACM_WALK
-  if (kDfsPriority && tid < W) __builtin_amdgcn_s_setprio(0);
+  if (tid < W) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   const int nisl = s_misc[0];
   WSTAMP(20);
@@ -1188,7 +1115,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
     if (lane == 0) s_has[w] = m;
   }
   __syncthreads();
-  if (kDfsPriority) __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(3);
   // s_last[b]: 1 + the level of the last walked contact touching b (bits 0..13; levels <= tcap <
   // 2^14), b pushed (bit 15), b popped (bit 14). One LDS read of the other body's word gives the
   // three things an edge needs: the contact was walked iff its other body was popped (the first of
@@ -1210,7 +1137,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
       s_ic[nisl] = (uint16_t)nord;
-      st_wt(xib + nisl, (uint16_t)nb);  // kernel C's (write-through: a fused B hands it over, see solve_wg)
+      st_wt(xib + nisl, (uint16_t)nb);  // kernel C reads it (stored write-through)
     }
     // the body to pop next with its CSR range and level: the seed (never touched yet: level 0), then
     // the last push of the previous pop (in registers; its stack slot is dropped), else the stack's
@@ -1278,7 +1205,7 @@ __device__ __forceinline__ void dfs_env(const StepParams& P, const WorldBuffers&
     s_ic[nisl] = (uint16_t)nord;
     st_wt(xib + nisl, (uint16_t)nb);
   }
-  if (kDfsPriority) __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_s_setprio(0);
   // this wave's x_dfs stores are read back below (workgroup scope: this CU, this XCD's L2)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __syncthreads();
@@ -1384,127 +1311,73 @@ namespace wg {
 // fixedRotation bodies): the fused kernel's arithmetic.
 // Kernel B's contact updates on packed (x, y) pairs (v_pk_mul_f32 / v_pk_add_f32, each lane of a pair
 // the scalar form's IEEE operation, no contraction: bit-identical). Round 5: C5 -1.2%, C3 even
-// (profiles/r05/abtests/wg_packed); -DMACM_WG_SCALAR restores the scalar form.
-#ifdef MACM_WG_SCALAR
-constexpr bool kWgPacked = false;
-#else
-constexpr bool kWgPacked = true;
-#endif
+// (profiles/r05/abtests/wg_packed).
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void gs_velocity(float2& va, float2& vb, float nx, float ny, float& ln, float& ltg,
                                             float mA, float mB, float kmass, float friction) {
-  if constexpr (kWgPacked) {
-    pf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
-    const pf2 n = {nx, ny}, t = {ny, -nx};
-    {
-      const pf2 pr = (vB - vA) * t;
-      const float vt = pr.x + pr.y;
-      float lambda = kmass * (-vt);
-      const float maxf = friction * ln;
-      const float ni = sclamp(ltg + lambda, -maxf, maxf);
-      lambda = ni - ltg;
-      ltg = ni;
-      const pf2 Pv = lambda * t;
-      vA = vA - mA * Pv;
-      vB = vB + mB * Pv;
-    }
-    {
-      const pf2 pr = (vB - vA) * n;
-      const float vn = pr.x + pr.y;
-      float lambda = -kmass * (vn - 0.0f);
-      const float ni = smax(ln + lambda, 0.0f);
-      lambda = ni - ln;
-      ln = ni;
-      const pf2 Pv = lambda * n;
-      vA = vA - mA * Pv;
-      vB = vB + mB * Pv;
-    }
-    va = make_float2(vA.x, vA.y);
-    vb = make_float2(vB.x, vB.y);
-    return;
-  }
-  const float tx = ny, ty = -nx;
+  pf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
+  const pf2 n = {nx, ny}, t = {ny, -nx};
   {
-    const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-    const float vt = dvx * tx + dvy * ty;
+    const pf2 pr = (vB - vA) * t;
+    const float vt = pr.x + pr.y;
     float lambda = kmass * (-vt);
     const float maxf = friction * ln;
     const float ni = sclamp(ltg + lambda, -maxf, maxf);
     lambda = ni - ltg;
     ltg = ni;
-    const float Px = lambda * tx, Py = lambda * ty;
-    va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-    vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+    const pf2 Pv = lambda * t;
+    vA = vA - mA * Pv;
+    vB = vB + mB * Pv;
   }
   {
-    const float dvx = vb.x - va.x, dvy = vb.y - va.y;
-    const float vn = dvx * nx + dvy * ny;
+    const pf2 pr = (vB - vA) * n;
+    const float vn = pr.x + pr.y;
     float lambda = -kmass * (vn - 0.0f);
     const float ni = smax(ln + lambda, 0.0f);
     lambda = ni - ln;
     ln = ni;
-    const float Px = lambda * nx, Py = lambda * ny;
-    va.x = va.x - mA * Px; va.y = va.y - mA * Py;
-    vb.x = vb.x + mB * Px; vb.y = vb.y + mB * Py;
+    const pf2 Pv = lambda * n;
+    vA = vA - mA * Pv;
+    vB = vB + mB * Pv;
   }
+  va = make_float2(vA.x, vA.y);
+  vb = make_float2(vB.x, vB.y);
 }
 
 __device__ __forceinline__ void gs_warm(float2& va, float2& vb, float nx, float ny, float ln, float lt, float mA,
                                         float mB) {
-  if constexpr (kWgPacked) {
-    const pf2 n = {nx, ny}, t = {ny, -nx};
-    const pf2 Pv = ln * n + lt * t;
-    pf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
-    vA = vA - mA * Pv;
-    vB = vB + mB * Pv;
-    va = make_float2(vA.x, vA.y);
-    vb = make_float2(vB.x, vB.y);
-    return;
-  }
-  const float tx = ny, ty = -nx;
-  const float Px = ln * nx + lt * tx, Py = ln * ny + lt * ty;
-  va.x = va.x - mA * Px;
-  va.y = va.y - mA * Py;
-  vb.x = vb.x + mB * Px;
-  vb.y = vb.y + mB * Py;
+  const pf2 n = {nx, ny}, t = {ny, -nx};
+  const pf2 Pv = ln * n + lt * t;
+  pf2 vA = {va.x, va.y}, vB = {vb.x, vb.y};
+  vA = vA - mA * Pv;
+  vB = vB + mB * Pv;
+  va = make_float2(vA.x, vA.y);
+  vb = make_float2(vB.x, vB.y);
 }
 
 // b2PositionSolverManifold + one position-constraint correction; returns the separation.
 // KPOS: K = mA + mB is known to be > 0 (else the impulse is 0, b2ContactSolver's K > 0 test).
 template <bool KPOS = false>
 __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radius, float mA, float mB) {
-  if constexpr (kWgPacked) {
-    const pf2 cA = {ca.x, ca.y}, cB = {cb.x, cb.y};
-    const pf2 d = cB - cA;
-    const pf2 d2 = d * d;
-    const float len = sqrt_rn(d2.x + d2.y);
-    const pf2 n = len < kEps ? d : d * rcp_rn(len);
-    const pf2 pr = d * n;
-    const float sep = (pr.x + pr.y) - radius - radius;
-    const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
-    const float K = mA + mB;
-    const float imp = KPOS ? div_by_invariant(-Cc, K) : K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
-    const pf2 Pv = imp * n;
-    const pf2 nA = cA - mA * Pv, nB = cB + mB * Pv;
-    ca = make_float2(nA.x, nA.y);
-    cb = make_float2(nB.x, nB.y);
-    return sep;
-  }
-  float nx = cb.x - ca.x, ny = cb.y - ca.y;
-  normalize(nx, ny);
-  const float sep = ((cb.x - ca.x) * nx + (cb.y - ca.y) * ny) - radius - radius;
+  const pf2 cA = {ca.x, ca.y}, cB = {cb.x, cb.y};
+  const pf2 d = cB - cA;
+  const pf2 d2 = d * d;
+  const float len = sqrt_rn(d2.x + d2.y);
+  const pf2 n = len < kEps ? d : d * rcp_rn(len);
+  const pf2 pr = d * n;
+  const float sep = (pr.x + pr.y) - radius - radius;
   const float Cc = sclamp(kBaumgarte * (sep + kLinearSlop), -kMaxLinearCorrection, 0.0f);
   const float K = mA + mB;
   const float imp = KPOS ? div_by_invariant(-Cc, K) : K > 0.0f ? div_by_invariant(-Cc, K) : 0.0f;
-  const float Px = imp * nx, Py = imp * ny;
-  ca.x = ca.x - mA * Px; ca.y = ca.y - mA * Py;
-  cb.x = cb.x + mB * Px; cb.y = cb.y + mB * Py;
+  const pf2 Pv = imp * n;
+  const pf2 nA = cA - mA * Pv, nB = cB + mB * Pv;
+  ca = make_float2(nA.x, nA.y);
+  cb = make_float2(nB.x, nB.y);
   return sep;
 }
 
 }  // namespace wg
-
 
 // Kernel B: one wave per env solves all its islands together, level by level (kernel A's
 // Gauss-Seidel levels): a level's contacts touch disjoint bodies, so lanes solve them at once
@@ -1518,9 +1391,6 @@ __device__ __forceinline__ float gs_position(float2& ca, float2& cb, float radiu
 // level solves. Level steps are issue- and latency-bound (one wave per SIMD pair at C5:
 // tools/ubench_level.hip), so the loops run two levels per iteration (no register rotation or
 // back-edge per level) and the position passes keep no uniform K > 0 branch inside the loop.
-#ifndef MACM_LEVEL_UNROLL  // A/B knob: level steps per loop iteration (1 or 2)
-#define MACM_LEVEL_UNROLL 2
-#endif
 __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffers& B, int tcap, int e,
                                           unsigned char* lds) {
   using namespace wg;
@@ -1535,14 +1405,6 @@ __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffer
   const int nisl = B.x_nisl[e];
   if (nisl < 0) return;  // stepped whole by the spill step in kernel A
   const int nc = nisl > 0 ? (int)B.x_ic[(size_t)e * IS + nisl] : 0;
-  if (kSolvePriority) {
-    // The kernel ends with its deepest envs (C3 closed loop: 72 levels per pass on average, up to
-    // ~200): the waves with the longest level chains take the SIMD's issue first
-    const int nlvl = B.x_nlvl[e];
-    if (nlvl >= 128) __builtin_amdgcn_s_setprio(3);
-    else if (nlvl >= 64) __builtin_amdgcn_s_setprio(2);
-    else if (nlvl >= 32) __builtin_amdgcn_s_setprio(1);
-  }
   const int nch = (nc + W - 1) / W;
   const float4* cst = B.x_cst + (size_t)e * tcap;
   float2* cimp = B.x_cimp + (size_t)e * tcap;
@@ -1595,7 +1457,6 @@ __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffer
   auto level_loop = [&](int lv0, int lv1, int mylv, auto&& step) {
     bool on = mylv == lv0;
     int lv = lv0;
-#if MACM_LEVEL_UNROLL == 2
     for (; lv < lv1; lv += 2) {
       step(lv, on, mylv == lv + 1);
       level_sync();
@@ -1607,14 +1468,6 @@ __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffer
       step(lv, on, false);
       level_sync();
     }
-#else
-    for (; lv <= lv1; ++lv) {
-      const bool nx = mylv == lv + 1;
-      step(lv, on, nx);
-      on = nx;
-      level_sync();
-    }
-#endif
   };
 
   // Warm start and velocity passes. last: the final impulses go straight to list order (g_lam).
@@ -1636,7 +1489,7 @@ __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffer
       // exec-mask branch per level); only the level's lanes keep their impulses
       float2* const pa0 = s_v + a;
       float2* const pb0 = s_v + b;
-      float2* const pd = s_dum + (kSharedDummy ? 0 : lane);  // shared: an LDS broadcast for the idle lanes
+      float2* const pd = s_dum + 0;  // shared: an LDS broadcast for the idle lanes
       float2* pa = mylv == lv0 ? pa0 : pd;
       float2* pb = mylv == lv0 ? pb0 : pd;
       level_loop(lv0, lv1, mylv, [&](int, bool onc, bool onn) {
@@ -1710,9 +1563,9 @@ __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffer
         const bool live = !s_done[I];
         // branch-free level steps as in the velocity passes; the dummy slots are in s_v (dead after
         // the position integration), a dummy lane's minimum goes to its slot's first word
-        float2* const pdd = s_v + (kSharedDummy ? 0 : lane);
+        float2* const pdd = s_v + 0;
         // a dummy lane's minimum stays in a word of its own (atomics on one address serialise)
-        float* const pmd = reinterpret_cast<float*>(s_v + (kSharedDummy ? 1 + lane : lane));
+        float* const pmd = reinterpret_cast<float*>(s_v + 1 + lane);
         const int mylvp = live ? mylv : -1;
         float2* const pca = s_c + a;
         float2* const pcb = s_c + b;
@@ -1759,274 +1612,14 @@ __device__ __forceinline__ void solve_env(const StepParams& P, const WorldBuffer
   for (int i = lane; i < N; i += W) st_wt(B.x_cout + en + i, s_c[i]);
 }
 
-// Kernel B, and with FUSED the dense envs' DFS first in the same wave (kernel A2 + B: one launch, an
-// env's solve starting as soon as its own walk ends instead of after the slowest env's walk; the
-// walk's records reach the solve through this wave's own global stores, ordered by a
-// workgroup-scope fence; the LDS is the larger of the two layouts, 8 waves per CU either way at C5).
-template <bool FUSED>
+// Kernel B: one wave per env. Measured slower and removed in round 6 (evidence kept,
+// profiles/r05/abtests/): the dense envs' DFS fused into this kernel (handoff_fused), and two envs per
+// wave (solve_pair).
 __global__ __launch_bounds__(64) void flock_solve_wg(StepParams P, WorldBuffers B, int tcap, Handoff H) {
   extern __shared__ __align__(16) unsigned char lds[];
   const int e = wg_env(B);
   const HandoffPublish publish(H, e);  // to kernel C when this body ends (any return)
-  if constexpr (FUSED) {
-    dfs_env(P, B, tcap, e, lds);
-    // the walk's records, counts and island ranges reach the solve through this wave's own global
-    // stores (this CU's L1, this XCD's L2); kernel C, which may run on another XCD beside this kernel
-    // (the handoff), reads the island outputs it needs write-through (dfs_env stores them so)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __syncthreads();
-  }
   solve_env(P, B, tcap, e, lds);
-}
-
-// ---- kernel B with two envs per wave (round 5) -----------------------------------------------------
-// A level step issues the same ~45 VALU however few of its lanes are on the level, and with four
-// waves per SIMD (C3: 4096 envs) the level steps of the SIMD's waves queue for its issue slots
-// (tools/ubench_level.hip: 387 cycles per level step at four waves per SIMD, 288 at two, 278 alone).
-// Here each half of the wave (32 lanes) solves an env of its own, each half on its own levels: the
-// same instructions step two envs, and the launch has half the waves. Envs b and b + 1 of the env
-// order (similar list sizes, so similar depths) share a wave. Each env's arithmetic, its order of
-// updates and its LDS bodies are exactly those of solve_env; only the chunks are 32 records.
-constexpr int kPairLanes = 32;  // lanes per env (half a wave)
-__host__ __device__ inline int wg_solve_lds_env(int N) { return (wg_solve_lds(N) + 15) & ~15; }
-
-__device__ __forceinline__ void solve_env_pair(const StepParams& P, const WorldBuffers& B, int tcap,
-                                               int ev0, int ev1, unsigned char* lds) {
-  using namespace wg;
-  constexpr int GW = kPairLanes;
-  const int lane = threadIdx.x, N = P.n_agents;
-  const int h = lane / GW, hl = lane % GW;  // this lane's half (env) and its lane in the half
-  const int IS = wg_isl_stride(N);
-  // per env (wave-uniform): island count (< 0: no solve: the spill step's, or no env), contacts
-  const int nisl0 = ev0 >= 0 ? B.x_nisl[ev0] : -1, nisl1 = ev1 >= 0 ? B.x_nisl[ev1] : -1;
-  const int nc0 = nisl0 > 0 ? (int)B.x_ic[(size_t)ev0 * IS + nisl0] : 0;
-  const int nc1 = nisl1 > 0 ? (int)B.x_ic[(size_t)ev1 * IS + nisl1] : 0;
-  if (nisl0 < 0 && nisl1 < 0) return;
-  if (kSolvePriority) {
-    int nlvl = 0;
-    if (nisl0 >= 0) nlvl = B.x_nlvl[ev0];
-    if (nisl1 >= 0) nlvl = max(nlvl, B.x_nlvl[ev1]);
-    if (nlvl >= 128) __builtin_amdgcn_s_setprio(3);
-    else if (nlvl >= 64) __builtin_amdgcn_s_setprio(2);
-    else if (nlvl >= 32) __builtin_amdgcn_s_setprio(1);
-  }
-  const int nch0 = (nc0 + GW - 1) / GW, nch1 = (nc1 + GW - 1) / GW;
-  const int nchw = max(nch0, nch1);
-  // this lane's env
-  const int nisl_h = h ? nisl1 : nisl0;
-  const bool hv = nisl_h >= 0;
-  const int e = hv ? (h ? ev1 : ev0) : (nisl0 >= 0 ? ev0 : ev1);  // an inactive half reads a live env's rows
-  const int nisl = hv ? nisl_h : 0, nc = hv ? (h ? nc1 : nc0) : 0;
-  unsigned char* base = lds + h * wg_solve_lds_env(N);
-  float2* s_v = (float2*)base;
-  float2* s_c = s_v + N;
-  float* s_mins = (float*)(s_c + N);
-  uint8_t* s_done = (uint8_t*)s_mins + wg_solve_mins_bytes(N);
-  float2* s_dum = (float2*)s_mins;
-  const size_t en = (size_t)e * N;
-  const float4* cst = B.x_cst + (size_t)e * tcap;
-  float2* cimp = B.x_cimp + (size_t)e * tcap;
-  const uint16_t* xord = B.x_ord + (size_t)e * tcap;
-  float2* g_lam = B.scratch + (size_t)e * tcap;
-  if (hv)
-    for (int i = hl; i < N; i += GW) {
-      s_c[i] = B.pos[en + i];
-      s_v[i] = B.x_vmid[en + i];
-    }
-  for (int I = hl; I < nisl; I += GW) s_done[I] = 0;
-  __syncthreads();
-  const float mA = P.inv_mass, mB = P.inv_mass;
-  const float kmass = (mA + mB) > 0.0f ? 1.0f / (mA + mB) : 0.0f;
-  const float friction = P.friction;
-  auto level_sync = [&]() { wave_lds_sync(); };
-  auto wait_vm = [&]() { __builtin_amdgcn_s_waitcnt(0x0f70); };  // vmcnt(0)
-  struct Slot {
-    float4 r;
-    float2 m;
-    int o;
-  };
-  auto load = [&](int c, Slot& x) {
-    const int k = max(0, min(c * GW + hl, nc - 1));
-    x.r = cst[k];
-    x.m = cimp[k];
-    x.o = xord[k];
-  };
-  // a lane's level relative to its half's first level in the chunk (0x7fff: no record), and the
-  // chunk's number of level steps: the larger of the two halves' level spans
-  auto chunk_levels = [&](int c, const Slot& x, int& rel, int& nsteps) {
-    const bool valid = c * GW + hl < nc;
-    const int mylv = valid ? __float_as_int(x.r.w) >> 16 : 0x7fff;
-    const int cnt0 = min(GW, nc0 - c * GW), cnt1 = min(GW, nc1 - c * GW);  // this chunk's records per env
-    const int lv00 = __builtin_amdgcn_readlane(mylv, 0), lv01 = __builtin_amdgcn_readlane(mylv, GW);
-    const int lv10 = __builtin_amdgcn_readlane(mylv, max(cnt0, 1) - 1);
-    const int lv11 = __builtin_amdgcn_readlane(mylv, GW + max(cnt1, 1) - 1);
-    const int span0 = (nisl0 >= 0 && cnt0 > 0) ? lv10 - lv00 + 1 : 0;
-    const int span1 = (nisl1 >= 0 && cnt1 > 0) ? lv11 - lv01 + 1 : 0;
-    rel = valid ? mylv - (h ? lv01 : lv00) : 0x7fff;
-    nsteps = max(span0, span1);
-  };
-  // level steps 0..nsteps-1 of a chunk (uniform), lane on at step rel; two steps per iteration
-  auto level_loop = [&](int nsteps, int rel, auto&& step) {
-    bool on = rel == 0;
-    int i = 0;
-    for (; i + 1 < nsteps; i += 2) {
-      step(on, rel == i + 1);
-      level_sync();
-      step(rel == i + 1, rel == i + 2);
-      level_sync();
-      on = rel == i + 2;
-    }
-    if (i + 1 == nsteps) {
-      step(on, false);
-      level_sync();
-    }
-  };
-  auto vel_pass = [&](auto warm_c, bool last) {
-    constexpr bool warm = decltype(warm_c)::value;
-    if (nchw == 0) return;
-    Slot cur, nxt;
-    load(0, cur);
-    wait_vm();
-    for (int c = 0; c < nchw; ++c) {
-      load(c + 1, nxt);
-      int rel, nsteps;
-      chunk_levels(c, cur, rel, nsteps);
-      const uint32_t ab = __float_as_uint(cur.r.x);
-      const int a = ab & 0xffffu, b = ab >> 16;
-      float2 im = cur.m;
-      float2* const pa0 = s_v + a;
-      float2* const pb0 = s_v + b;
-      float2* const pd = s_dum + (kSharedDummy ? 0 : hl);
-      float2* pa = rel == 0 ? pa0 : pd;
-      float2* pb = rel == 0 ? pb0 : pd;
-      level_loop(nsteps, rel, [&](bool onc, bool onn) {
-        float2 va = *pa, vb = *pb;
-        float2* const na = onn ? pa0 : pd;
-        float2* const nb = onn ? pb0 : pd;
-        float lx = im.x, ly = im.y;
-        if constexpr (warm) gs_warm(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB);
-        else gs_velocity(va, vb, cur.r.y, cur.r.z, lx, ly, mA, mB, kmass, friction);
-        *pa = va;
-        *pb = vb;
-        im.x = onc ? lx : im.x;
-        im.y = onc ? ly : im.y;
-        pa = na;
-        pb = nb;
-      });
-      const int k = c * GW + hl;
-      if (!warm && k < nc) {
-        if (last) st_wt(g_lam + cur.o, im);
-        else cimp[k] = im;
-      }
-      wait_vm();
-      cur = nxt;
-    }
-  };
-  if (P.warm_starting) vel_pass(std::true_type{}, false);
-  for (int it = 0; it < P.vel_iters; ++it) vel_pass(std::false_type{}, it + 1 == P.vel_iters);
-  if (P.vel_iters == 0)
-    for (int k = hl; k < nc; k += GW) st_wt(g_lam + xord[k], cimp[k]);
-
-  if (hv)
-    for (int i = hl; i < N; i += GW) {
-      const float2 vv = s_v[i];
-      float vx = vv.x, vy = vv.y;
-      const float tx = P.dt * vx, ty = P.dt * vy;
-      if (tx * tx + ty * ty > kMaxTranslation * kMaxTranslation) {
-        const float ratio = kMaxTranslation / sqrtf(tx * tx + ty * ty);
-        vx = vx * ratio;
-        vy = vy * ratio;
-      }
-      const float2 c = s_c[i];
-      s_c[i] = make_float2(c.x + P.dt * vx, c.y + P.dt * vy);
-      st_wt(B.x_vout + en + i, make_float2(vx, vy));
-    }
-  __syncthreads();
-
-  auto pos_passes = [&](auto kpos_c) {
-    constexpr bool kpos = decltype(kpos_c)::value;
-    for (int it = 0; it < P.pos_iters; ++it) {
-      for (int I = hl; I < nisl; I += GW) s_mins[I] = 0.0f;
-      __syncthreads();
-      Slot cur, nxt;
-      if (nchw > 0) load(0, cur);
-      wait_vm();
-      for (int c = 0; c < nchw; ++c) {
-        load(c + 1, nxt);
-        int rel, nsteps;
-        chunk_levels(c, cur, rel, nsteps);
-        const int I = __float_as_int(cur.r.w) & 0xffff;
-        const uint32_t ab = __float_as_uint(cur.r.x);
-        const int a = ab & 0xffffu, b = ab >> 16;
-        const bool live = hv && nc > 0 && !s_done[min(I, max(nisl - 1, 0))];
-        float2* const pdd = s_v + (kSharedDummy ? 0 : hl);
-        float* const pmd = reinterpret_cast<float*>(s_v + (kSharedDummy ? 1 + hl : hl));
-        const int relp = live ? rel : 0x7fff;
-        float2* const pca = s_c + a;
-        float2* const pcb = s_c + b;
-        float* const pmi = s_mins + I;
-        float2* pa = relp == 0 ? pca : pdd;
-        float2* pb = relp == 0 ? pcb : pdd;
-        float* pm = relp == 0 ? pmi : pmd;
-        level_loop(nsteps, relp, [&](bool, bool onn) {
-          float2 ca = *pa, cb = *pb;
-          float2* const na = onn ? pca : pdd;
-          float2* const nb = onn ? pcb : pdd;
-          float* const nm = onn ? pmi : pmd;
-          const float sep = gs_position<kpos>(ca, cb, P.radius, mA, mB);
-          *pa = ca;
-          *pb = cb;
-          __hip_atomic_fetch_min(pm, sep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          pa = na;
-          pb = nb;
-          pm = nm;
-        });
-        wait_vm();
-        cur = nxt;
-      }
-      __syncthreads();
-      bool open = false;
-      for (int I = hl; I < nisl; I += GW) {
-        if (s_done[I]) continue;
-        if (s_mins[I] >= -3.0f * kLinearSlop) s_done[I] = 1;
-        else open = true;
-      }
-      const bool any_open = __ballot(open) != 0ull;
-      __syncthreads();
-      if (!any_open) break;
-    }
-  };
-  if (mA + mB > 0.0f) pos_passes(std::true_type{});
-  else pos_passes(std::false_type{});
-  if (!hv) return;
-  uint8_t* isolv = B.x_isolv + (size_t)e * IS;
-  for (int I = hl; I < nisl; I += GW) st_wt(isolv + I, s_done[I]);
-  for (int i = hl; i < N; i += GW) st_wt(B.x_cout + en + i, s_c[i]);
-}
-
-// Kernel B, two envs per wave: envs order[2 b], order[2 b + 1] (one when E is odd). With the handoff,
-// the wave counts both envs as started and publishes both when it ends.
-__global__ __launch_bounds__(64) void flock_solve_wg_pair(StepParams P, WorldBuffers B, int tcap, Handoff H) {
-  extern __shared__ __align__(16) unsigned char lds[];
-  const int b0 = 2 * (int)blockIdx.x, b1 = b0 + 1;
-  const bool ord = kWgEnvOrder && B.sched;
-  const int ev0 = ord ? (int)B.sched[b0] : b0;
-  const int ev1 = b1 < P.n_envs ? (ord ? (int)B.sched[b1] : b1) : -1;
-  const int nv = ev1 >= 0 ? 2 : 1;
-  if (H.q && threadIdx.x == 0)
-    __hip_atomic_fetch_add(H.b_started, (unsigned long long)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  solve_env_pair(P, B, tcap, ev0, ev1, lds);
-  if (H.q) {
-    __builtin_amdgcn_s_waitcnt(0);
-    if (threadIdx.x == 0) {
-      const unsigned slot = __hip_atomic_fetch_add(&H.ctr[0], (unsigned)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&H.q[slot], ((unsigned long long)H.tag << 32) | (unsigned)ev0, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      if (nv == 2)
-        __hip_atomic_store(&H.q[slot + 1], ((unsigned long long)H.tag << 32) | (unsigned)ev1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 template <typename OT>
@@ -2065,8 +1658,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   uint16_t* s_bjv = (uint16_t*)(lds + L.bjv);
   const float2* g_lam = B.scratch + (size_t)e * tcap;
   const int IS = wg_isl_stride(N);
-  // With the handoff, a fused kernel B may have walked this env's islands (flock_solve_wg<true>) on
-  // another XCD while this kernel runs: its island outputs are read write-through, as B's solve outputs
+  // with the handoff, the island count and B's solve outputs are read write-through (flock_dfs_wg
+  // stores the count so)
   const bool hwt = H.q != nullptr;
   const int nisl = hwt ? ld_wt(B.x_nisl + e) : B.x_nisl[e];
   if (nisl < 0) {  // stepped whole by the spill step in kernel A (its observation is written)
@@ -2191,11 +1784,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   int bj = tid == 0 ? 1 : 0;
   // strip cells from N = 256 (grid::kCellsMinAgents): with per-strip extent pruning (round 4) they
   // walk ~290 of C5's 1024 bodies per body and beat the all-pairs sweep at C3 too
-#ifdef MACM_AB_ALL_PAIRS
-  const bool cells = false;
-#else
   const bool cells = P.sweep == 1 || (P.sweep == 0 && N >= grid::kCellsMinAgents);
-#endif
   const bool gok = cells && grid::build(G, act, make_float2(cx, cy), fn);
   WSTAMP(4);
   // Thread t sweeps the body of strip-sorted entry t (flock_grid.hpp): body i, its wave's tile of
@@ -2252,46 +1841,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           np2 = nw ? (np2 << 10) | (uint32_t)j : np2;
           nc += nw ? 1 : 0;
         };
-        if (kSweepPipe2) {
-          // entries two candidates ahead and AABBs one ahead: every read has a whole candidate's
-          // test to arrive in (the loop-carried copies at the back edge find their loads done)
-          if (q0 < q1) {
-            const int ql = q1 - 1;
-            float4 Ea = G.ent[q0], Eb = G.ent[min(q0 + 1, ql)];
-            float4 Fa = s_fn[__float_as_int(Ea.z)];
-            for (int q = q0;; q += 2) {
-              const float4 Fb = s_fn[__float_as_int(Eb.z)];
-              const float4 Ec = G.ent[min(q + 2, ql)];
-              cand(Ea, Fa);
-              if (q + 1 >= q1) break;
-              const float4 Fc = s_fn[__float_as_int(Ec.z)];
-              const float4 Ed = G.ent[min(q + 3, ql)];
-              cand(Eb, Fb);
-              if (q + 2 >= q1) break;
-              Ea = Ec;
-              Fa = Fc;
-              Eb = Ed;
-            }
-          }
-        } else if (kSweepPipe) {
-          // two candidates per iteration, each entry read one candidate ahead (into the register
-          // pair the other candidate is not using, so the loop carries no copies that would wait
-          // for the loads): an entry's read hides under the previous candidate's test
-          if (q0 < q1) {
-            float4 Ea = G.ent[q0];
-            for (int q = q0;; q += 2) {
-              const float4 Eb = G.ent[min(q + 1, q1 - 1)];
-              cand(Ea, s_fn[__float_as_int(Ea.z)]);
-              if (q + 1 >= q1) break;
-              Ea = G.ent[min(q + 2, q1 - 1)];
-              cand(Eb, s_fn[__float_as_int(Eb.z)]);
-              if (q + 2 >= q1) break;
-            }
-          }
-        } else {
-          for (int q = q0; q < q1; ++q) {
-            const float4 Eq = G.ent[q];
-            cand(Eq, s_fn[__float_as_int(Eq.z)]);
+        // two candidates per iteration, each entry read one candidate ahead (into the register
+        // pair the other candidate is not using, so the loop carries no copies that would wait
+        // for the loads): an entry's read hides under the previous candidate's test
+        if (q0 < q1) {
+          float4 Ea = G.ent[q0];
+          for (int q = q0;; q += 2) {
+            const float4 Eb = G.ent[min(q + 1, q1 - 1)];
+            cand(Ea, s_fn[__float_as_int(Ea.z)]);
+            if (q + 1 >= q1) break;
+            Ea = G.ent[min(q + 2, q1 - 1)];
+            cand(Eb, s_fn[__float_as_int(Eb.z)]);
+            if (q + 2 >= q1) break;
           }
         }
       }
@@ -2347,26 +1908,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     // this body's slots of an LDS scratch (the cells' entry array, unused on this path), so the
     // list build below writes them back in descending order without a second sweep.
     uint16_t* np = (uint16_t*)(lds + L.gent) + tid * kNewSlots;
-#ifdef MACM_WG_PACKED_SWEEP
-    // the AABB separations and the distance as packed pairs (v_pk_add / v_pk_mul: each lane of a
-    // packed op rounds as the scalar op)
-    typedef float fv2 __attribute__((ext_vector_type(2)));
-    const fv2 flo = {fn.x, fn.y}, fhi = {fn.z, fn.w}, cc2 = {cx, cy};
-#endif
 #pragma unroll 2
     for (int j = 0; j < N; ++j) {
       const float4 rfn = s_fn[j];
       const float2 rc = s_c[j];
-#ifdef MACM_WG_PACKED_SWEEP
-      const fv2 s1 = (fv2){rfn.x, rfn.y} - fhi, s2 = flo - (fv2){rfn.z, rfn.w};
-      const bool ovn = !(fmaxf(fmaxf(s1.x, s1.y), fmaxf(s2.x, s2.y)) > 0.0f);
-      const fv2 dv = (fv2){rc.x, rc.y} - cc2, dq = dv * dv;
-      const float d2 = dq.x + dq.y;
-#else
       const bool ovn = !(sep_max(fn, rfn) > 0.0f);
       const float dx = rc.x - cx, dy = rc.y - cy;
       const float d2 = dx * dx + dy * dy;
-#endif
       const bool other = j != tid;
       coll |= other && ovn;
       if (other && d2 < best) {
@@ -2574,32 +2122,6 @@ int wg_lds_bytes(int N, int tcap) {
 // Raise the dynamic-LDS limit of the workgroup kernels (world creation). The limit is a property of
 // the kernel, not of a world: it only ever grows (per device), so creating a world of fewer agents
 // after a larger one cannot make the larger world's launches fail.
-// kernel B with the dense envs' DFS in the same wave (flock_solve_wg<true>): the larger LDS layout
-static int wg_fused_lds(int N, int tcap) {
-  const int d = wg::wg_layout_d(N, tcap).total, b = wg_solve_lds(N);
-  return d > b ? d : b;
-}
-// MACM_FUSE_DFS overrides the default (A/B sessions)
-#ifndef MACM_FUSE_DFS_DEFAULT
-#define MACM_FUSE_DFS_DEFAULT 0
-#endif
-static bool fuse_dfs() {
-  const char* x = getenv("MACM_FUSE_DFS");
-  return wg::kDfsKernel && (x ? atoi(x) : MACM_FUSE_DFS_DEFAULT) != 0;
-}
-
-// Kernel B with two envs per wave (flock_solve_wg_pair) where waves would otherwise queue for their
-// SIMDs' issue: many envs of up to kPairMaxAgents agents. MACM_SOLVE_PAIR=0/1 overrides (A/B sessions).
-#ifndef MACM_SOLVE_PAIR_DEFAULT
-#define MACM_SOLVE_PAIR_DEFAULT 0
-#endif
-constexpr int kPairMaxAgents = 512, kPairMinEnvs = 1024;
-static bool solve_pairs(const StepParams& P) {
-  const char* x = getenv("MACM_SOLVE_PAIR");
-  const bool on = x ? atoi(x) != 0 : MACM_SOLVE_PAIR_DEFAULT != 0;
-  return on && P.n_agents <= kPairMaxAgents && P.n_envs >= kPairMinEnvs;
-}
-
 hipError_t wg_configure(int N, int tcap) {
   static std::mutex mu;
   static std::map<int, int> high;  // device -> the largest N configured
@@ -2614,18 +2136,15 @@ hipError_t wg_configure(int N, int tcap) {
   for (const void* f : fi)
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, wg_init_lds_bytes(N));
   const void* fsplit[] = {(const void*)flock_step_wg_a<float>, (const void*)flock_step_wg_a<double>,
-                          (const void*)flock_solve_wg<false>, (const void*)flock_step_wg_c<float>,
-                          (const void*)flock_step_wg_c<double>, (const void*)flock_solve_wg<true>};
+                          (const void*)flock_solve_wg, (const void*)flock_step_wg_c<float>,
+                          (const void*)flock_step_wg_c<double>};
   const int la = wg_a_lds_bytes(N, tcap), lc = wg_layout_c(N).total;
-  const int lsplit[] = {la, la, wg_solve_lds(N), lc, lc, wg_fused_lds(N, tcap)};
-  for (int i = 0; i < 6; ++i)
+  const int lsplit[] = {la, la, wg_solve_lds(N), lc, lc};
+  for (int i = 0; i < 5; ++i)
     if (e == hipSuccess) e = hipFuncSetAttribute(fsplit[i], hipFuncAttributeMaxDynamicSharedMemorySize, lsplit[i]);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)flock_dfs_wg, hipFuncAttributeMaxDynamicSharedMemorySize,
                             wg::wg_layout_d(N, tcap).total);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)flock_solve_wg_pair, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            2 * wg_solve_lds_env(N));
   return e;
 }
 
@@ -2638,11 +2157,11 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
                           hipStream_t s, HandoffStream* HS, uint8_t* bot_act) {
   dim3 grid(P.n_envs), block(wg_block(P.n_agents));
   Handoff H{nullptr, nullptr, nullptr, 0u};
-  if (HS && kWgEnvOrder && B.sched) {
+  if (HS && B.sched) {
     if (++HS->tag == 0u) HS->tag = 1u;  // 0 never tags a step (zeroed queue entries)
     H = Handoff{HS->b_started, HS->ctr, HS->q, HS->tag};
   }
-  if (kWgEnvOrder && B.sched) {
+  if (B.sched) {
     const hipError_t oe = launch_env_order(reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs,
                                            P.max_contacts, s, H.q ? H.ctr : nullptr);
     if (oe != hipSuccess) return oe;
@@ -2666,22 +2185,9 @@ hipError_t launch_step_wg(const StepParams& P, const WorldBuffers& B, int cur, i
   // the watcher's clock starts only once kernel B's dependencies have finished: HS->stream
   // waits for this event, recorded on `s` right before B, so work queued on the caller's stream ahead
   // of the step (a policy update, another world's launches) cannot run the watcher out of time
-  bool pre_b = false;
-  auto record_pre_b = [&]() {
-    if (H.q) pre_b = hipEventRecord(HS->pre_b, s) == hipSuccess;
-  };
-  if (fuse_dfs()) {
-    record_pre_b();
-    hipLaunchKernelGGL(flock_solve_wg<true>, grid, dim3(64), wg_fused_lds(N, tcap), s, P, B, tcap, H);
-  } else {
-    if (wg::kDfsKernel) hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
-    record_pre_b();
-    if (solve_pairs(P))
-      hipLaunchKernelGGL(flock_solve_wg_pair, dim3((P.n_envs + 1) / 2), dim3(64), 2 * wg_solve_lds_env(N), s, P, B,
-                         tcap, H);
-    else
-      hipLaunchKernelGGL(flock_solve_wg<false>, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
-  }
+  hipLaunchKernelGGL(flock_dfs_wg, grid, dim3(64), ld, s, P, B, tcap);
+  const bool pre_b = H.q && hipEventRecord(HS->pre_b, s) == hipSuccess;
+  hipLaunchKernelGGL(flock_solve_wg, grid, dim3(64), wg_solve_lds(N), s, P, B, tcap, H);
   if (!H.q) {
     launch_c(s);
     return hipGetLastError();

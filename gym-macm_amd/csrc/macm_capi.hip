@@ -20,7 +20,7 @@ hipError_t launch_step_w64(const StepParams& P, const WorldBuffers& B, int cur, 
                            bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s);
 hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cur, const void* actions, void* obs,
                               bool obs_f64, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done, hipStream_t s,
-                              int nsteps, unsigned long long astride, int traj, SoloLaunch* solo);
+                              int nsteps, unsigned long long astride, int traj);
 hipError_t launch_init_w64(const StepParams& P, const WorldBuffers& B, int cur, void* obs, bool obs_f64,
                            int32_t* nbr, const uint8_t* mask, hipStream_t s);
 hipError_t launch_observe_w64(const StepParams& P, const WorldBuffers& B, void* obs, bool obs_f64, int32_t* nbr,
@@ -99,7 +99,6 @@ struct macm_world {
   // workgroup-path rollouts: env slices on streams of their own (created on first use)
   std::vector<hipStream_t> slice_streams;
   std::vector<hipEvent_t> slice_events;  // [0] fork, [1 + s] join of slice s
-  SoloLaunch solo{0, nullptr, nullptr, nullptr, nullptr, 0ull};  // wave path: the balanced rollout's solo split
   HandoffStream* ho = nullptr;  // workgroup path: kernel C as kernel B's consumer (handoff_for)
   bool ho_tried = false;
   int slots_alloc = 0;  // spill working-set slots allocated (== E: one per env)
@@ -215,10 +214,6 @@ static void free_handoff(HandoffStream*& h) {
 
 void free_world(macm_world* w) {
   free_handoff(w->ho);
-  if (w->solo.stream) (void)hipStreamDestroy(w->solo.stream);
-  if (w->solo.fork) (void)hipEventDestroy(w->solo.fork);
-  if (w->solo.started) (void)hipFree(w->solo.started);
-  if (w->solo.join) (void)hipEventDestroy(w->solo.join);
   for (hipStream_t st : w->slice_streams) (void)hipStreamDestroy(st);
   for (hipEvent_t ev : w->slice_events) (void)hipEventDestroy(ev);
   w->slice_streams.clear();
@@ -270,16 +265,10 @@ struct Capacity {
   int64_t C;
   int64_t slots;  // == E: one slot per env
 };
-// The solo split of balanced wave-kernel rollouts (flock_step_w64.hip, env_rollout_w64<..., SOLO>):
-// how many of the heaviest envs run in waves that own their SIMD. MACM_SOLO_ENVS overrides it
-// (A/B sessions; 0 = one launch).
-#ifndef MACM_SOLO_ENVS_DEFAULT
-#define MACM_SOLO_ENVS_DEFAULT 0
-#endif
 // Kernel dispatches run one at a time: HIP's serialisation switches, or a profiler collecting counters
-// (rocprofv3 --pmc serialises dispatches to attribute counters to them). The two producer/consumer
-// launches (the solo split, the B -> C handoff) need their consumer to run BESIDE the producer: under
-// serialisation the consumer's wait would time out and the step be left incomplete, so they are off.
+// (rocprofv3 --pmc serialises dispatches to attribute counters to them). The producer/consumer
+// launch pair of the B -> C handoff needs its consumer to run BESIDE the producer: under
+// serialisation the consumer's wait would time out and the step be left incomplete, so it is off.
 static bool serialized_dispatch() {
   for (const char* k : {"AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "CUDA_LAUNCH_BLOCKING"}) {
     const char* v = getenv(k);
@@ -287,12 +276,6 @@ static bool serialized_dispatch() {
   }
   const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
   return pmc && *pmc && strcmp(pmc, "0") != 0 && strcasecmp(pmc, "false") != 0;
-}
-
-static int solo_envs() {
-  const char* v = getenv("MACM_SOLO_ENVS");
-  const int n = v ? atoi(v) : MACM_SOLO_ENVS_DEFAULT;
-  return (n > 0 && !serialized_dispatch()) ? n : 0;
 }
 
 // The most agents per env (Flock and TDM): one workgroup of 1024 threads, up to 4 bodies per thread
@@ -435,7 +418,6 @@ int macm_world_create(const macm_config* cfg, const int32_t* targets_idx, int32_
   w->tidx = tidx;
   w->wave = N <= 64;
   w->big = N > 1024;  // flock_big.hip: the spill step with several bodies per thread
-  w->solo.n = w->wave ? solo_envs() : 0;
   {
     const int bs = N <= 64 ? 64 : wg_block(N);
     const int want = N <= 64 ? 256 : 5 * bs;  // register staging holds 5 records per thread
@@ -673,10 +655,7 @@ static int overflow_error(uint32_t st) {
 // The workgroup step's B -> C handoff (flock_common.hpp Handoff), created at the first step that can
 // use it: the workgroup path, when kHandoffDefault or MACM_HANDOFF=1 (A/B; MACM_HANDOFF=0 off). Env
 // slices (rollout_wg_slices) run without it. NULL: kernel C launched after B on the same stream.
-#ifndef MACM_HANDOFF_DEFAULT
-#define MACM_HANDOFF_DEFAULT 1  // round 5: C5 window 5.35 -> 4.99 ms (profiles/r05/abtests/handoff_fused/)
-#endif
-static constexpr bool kHandoffDefault = MACM_HANDOFF_DEFAULT != 0;
+static constexpr bool kHandoffDefault = true;  // round 5: C5 window 5.35 -> 4.99 ms (profiles/r05/abtests/handoff_fused/)
 static HandoffStream* handoff_for(macm_world* w) {
   if (w->wave || w->big || w->ho_tried) return w->ho;
   w->ho_tried = true;
@@ -774,10 +753,7 @@ static macm_outputs step_outputs(const macm_world* w, const macm_outputs* out, i
 // 481 with 3, but 744 with 4: with the caller's stream that is more streams than the process's 4
 // hardware queues (GPU_MAX_HW_QUEUES), and two slices sharing a queue serialise each other's
 // launches. C5 (N = 1024, 2048 envs) gained nothing (profiles/r02/rollout/).
-#ifndef MACM_SLICE_MAX_AGENTS  // A/B knob
-#define MACM_SLICE_MAX_AGENTS 512
-#endif
-static constexpr int kSlices = 3, kSliceMinEnvs = 1024, kSliceMaxAgents = MACM_SLICE_MAX_AGENTS;
+static constexpr int kSlices = 3, kSliceMinEnvs = 1024, kSliceMaxAgents = 512;
 // MACM_WG_SLICES=n: n env slices (0: none, the handoff instead; A/B sessions), kSlices by default
 static int n_slices() {
   const char* v = getenv("MACM_WG_SLICES");
@@ -873,19 +849,9 @@ static int world_rollout(macm_world* w, const void* actions, int n_steps, const 
   const unsigned long long astride =
       bots ? 0ull
            : (unsigned long long)w->P.n_envs * w->P.n_agents * (mode == 0 ? 3 * sizeof(uint8_t) : 2 * sizeof(float));
-  if (w->wave) {  // one launch (two with the solo split); astride 0: the closed-loop form of the rollout kernel
-    if (w->solo.n > 0 && !w->solo.stream) {  // created at the first rollout that can use it
-      int lo = 0, hi = 0;
-      HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIP_TRY(hipStreamCreateWithPriority(&w->solo.stream, hipStreamNonBlocking, hi));
-      HIP_TRY(hipEventCreateWithFlags(&w->solo.fork, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&w->solo.join, hipEventDisableTiming));
-      HIP_TRY(hipMalloc(&w->solo.started, sizeof(unsigned long long)));
-      HIP_TRY(hipMemset(w->solo.started, 0, sizeof(unsigned long long)));
-    }
+  if (w->wave) {  // one launch; astride 0: the closed-loop form of the rollout kernel
     HIP_TRY(launch_rollout_w64(w->P, w->B, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->nbr_id, out->reward,
-                               out->collided, out->done, s, n_steps, astride, traj ? 1 : 0,
-                               w->solo.started ? &w->solo : nullptr));
+                               out->collided, out->done, s, n_steps, astride, traj ? 1 : 0));
     if (n_steps & 1) w->cur ^= 1;
     return MACM_OK;
   }
@@ -1460,14 +1426,7 @@ int macm_tdm_reset_envs(macm_tdm* w, const uint8_t* env_mask, const macm_tdm_out
 // Below kTdmSplitMaxEnvs envs by default; MACM_TDM_SPLIT_OBS=0/1 overrides
 // (tests, A/B). The closed loop (the bots read each step's observation inside the launch) and the
 // workgroup step (N > 64) keep the fused form.
-#ifndef MACM_TDM_SPLIT_MAX_ENVS
-#define MACM_TDM_SPLIT_MAX_ENVS 1024
-#endif
-static constexpr int kTdmSplitMaxEnvs = MACM_TDM_SPLIT_MAX_ENVS;
-#ifndef MACM_TDM_SPLIT_CHUNK
-#define MACM_TDM_SPLIT_CHUNK 8
-#endif
-static constexpr int kTdmSplitChunk = MACM_TDM_SPLIT_CHUNK;
+static constexpr int kTdmSplitMaxEnvs = 1024, kTdmSplitChunk = 8;
 
 static bool tdm_split_obs(const macm_tdm* w) {
   if (!w->wave) return false;

@@ -165,141 +165,6 @@ __device__ __forceinline__ void tdm_obs_pairs(OT* __restrict__ obs, uint8_t* __r
   }
 }
 
-// The pair tiles with the mask staged in LDS (stage: N (N - 1) bytes, the dead contact arrays) and
-// written out as whole 16-B pieces after the tiles: the tiles' 8-byte mask runs left most of the
-// env's mask lines partly written, so L2 wrote them back piece by piece (round 3 PMC: ~25 MB of HBM
-// writes per C4 step above the algorithmic bytes). The obs slots are the pair tiles'.
-template <typename OT>
-__device__ __forceinline__ void tdm_obs_pairs_smask(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N,
-                                                    int lane, unsigned long long livem, const TdmParams& TP,
-                                                    const float2* sc, const float* sa, uint8_t* stage) {
-  tdm_obs_pairs<OT>(obs, mask ? stage : nullptr, N, lane, livem, TP, sc, sa);
-  if (!mask) return;
-  wave_lds_sync();  // the stage's bytes (written by other lanes) before the copy reads them
-  const int nb = N * (N - 1);
-  if ((nb & 15) == 0) {  // 16-B pieces (N = 32: 62 lanes, one store instruction)
-    for (int k = lane; 16 * k < nb; k += 64)
-      reinterpret_cast<uint4*>(mask)[k] = reinterpret_cast<const uint4*>(stage)[k];
-  } else {  // 64 consecutive bytes per store instruction
-    for (int k = lane; k < nb; k += 64) mask[k] = stage[k];
-  }
-}
-
-// The same slots in memory order: lane q of each pass writes slot q of the env's [N, N-1] block,
-// so one store instruction covers 64 consecutive slots (1 KB: whole 128-B lines; an env's block is
-// N (N-1) 16 B, a multiple of 128 B for N = 32) and the mask 64 consecutive bytes. Each slot
-// computes its own atan2 (no sharing between the two directions of a pair).
-template <typename OT>
-__device__ __forceinline__ void tdm_obs_linear(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
-                                               unsigned long long livem, const TdmParams& TP, const float2* sc,
-                                               const float* sa) {
-  const int S = N - 1, ns = N * S;
-  int i = lane / S, k = lane - i * S;  // slot q = i * S + k, advanced by 64 per pass
-  for (int q = lane; q < ns; q += 64) {
-    const int j = k < i ? k : k + 1;
-    const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
-    double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
-    if (m) {
-      const float2 ci = sc[i], cj = sc[j];
-      const float rx = cj.x - ci.x, ry = cj.y - ci.y;
-      r = obs_sqrt<OT>(rx * rx + ry * ry);
-      t = wrap_pi(obs_atan2((double)ry, (double)rx) - (double)sa[i]);
-      p = wrap_pi((double)sa[j] - (double)sa[i]);
-      ty = tdm_team_of(TP, j) == tdm_team_of(TP, i) ? 1.0 : 0.0;
-    }
-    if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
-    if (mask) mask[q] = m ? 1 : 0;
-    k += 64;
-    while (k >= S) {
-      k -= S;
-      ++i;
-    }
-  }
-}
-
-// The pair computation of tdm_obs_pairs with the stores of tdm_obs_linear: pass 1 evaluates, for
-// every unordered pair {i, j} (i < j) whose agents are both alive, the shared part of its two slots
-// (r and atan2's reduction and polynomial, obs_atan2_core) into LDS; pass 2 writes the slots in
-// memory order, lane q slot q, each finishing its own quadrant, "- angle" and wraps from the staged
-// core. Every value is bit-identical to tdm_obs_pairs (the same expressions on the same operands);
-// a store instruction covers 64 consecutive slots, so the env's block leaves L2 as whole lines
-// (the pair tiles' 8-slot runs straddle lines: rows are 496 B at N = 32). float32 obs only; stage:
-// 12 B per pair (N <= 32 in the wave kernel's 6 KB of contact arrays, dead by then).
-__host__ __device__ constexpr int tdm_obs_stage_bytes(int N) { return 12 * (N * (N - 1) / 2); }
-
-template <typename OT>
-__device__ __forceinline__ void tdm_obs_staged(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
-                                               unsigned long long livem, const TdmParams& TP, const float2* sc,
-                                               const float* sa, unsigned char* stage) {
-  static_assert(sizeof(OT) == 4, "the staged writer keeps r as float32");
-  const int S = N - 1, P = N * S / 2;
-  double* s_core = reinterpret_cast<double*>(stage);
-  float* s_r = reinterpret_cast<float*>(stage + 8 * P);
-  // pair (i < j) -> its stage index (row-major over i < j)
-  auto pidx = [N](int i, int j) { return ((i * (2 * N - i - 1)) >> 1) + (j - i - 1); };
-  auto stage_pair = [&](int i, int j) {
-    if ((livem >> i) & (livem >> j) & 1ull) {
-      const float2 ci = sc[i], cj = sc[j];
-      const float rx = cj.x - ci.x, ry = cj.y - ci.y;
-      const int pp = pidx(i, j);
-      s_r[pp] = (float)obs_sqrt<OT>(rx * rx + ry * ry);
-      s_core[pp] = obs_atan2_core(fabs((double)rx), fabs((double)ry));
-    }
-  };
-  {  // pass 1 over the pair tiles of tdm_obs_pairs (uniform loops)
-    const int nb = (N + 7) >> 3;
-    const int a = lane >> 3, b = lane & 7;
-    for (int I = 0; I < nb; ++I) {
-      const int i = 8 * I + a;
-      for (int J = I + 1; J < nb; ++J) {
-        const int j = 8 * J + b;
-        if (i < N && j < N) stage_pair(i, j);
-      }
-    }
-    const int k = lane & 31;
-    int r = 0, rem = k;
-    while (r < 7 && rem >= 7 - r) {
-      rem -= 7 - r;
-      ++r;
-    }
-    const int c = r + 1 + rem;
-    for (int D0 = 0; D0 < nb; D0 += 2) {
-      const int D = D0 + (lane >> 5);
-      const int i = 8 * D + r, j = 8 * D + c;
-      if (k < 28 && D < nb && j < N) stage_pair(i, j);
-    }
-  }
-  __syncthreads();
-  const int ns = N * S;
-  const float invS = 1.0f / (float)S;
-  for (int q = lane; q < ns; q += 64) {
-    int i = (int)((float)q * invS);  // q / S, then one exact correction
-    int k = q - i * S;
-    if (k < 0) {
-      --i;
-      k += S;
-    } else if (k >= S) {
-      ++i;
-      k -= S;
-    }
-    const int j = k < i ? k : k + 1;
-    const bool m = ((livem >> i) & (livem >> j) & 1ull) != 0ull;
-    double r = 0.0, t = 0.0, p = 0.0, ty = 0.0;
-    if (m) {
-      const int pp = i < j ? pidx(i, j) : pidx(j, i);
-      const float2 ci = sc[i], cj = sc[j];
-      const float rx = cj.x - ci.x, ry = cj.y - ci.y;  // other.position - agent.position
-      const float ai = sa[i], aj = sa[j];
-      r = (double)s_r[pp];
-      t = wrap_pi(obs_atan2_finish(s_core[pp], (double)ry, (double)rx) - (double)ai);
-      p = wrap_pi((double)aj - (double)ai);
-      ty = tdm_team_nb(TP, j) == tdm_team_nb(TP, i) ? 1.0 : 0.0;
-    }
-    if (obs) store4<OT>(obs + (size_t)q * 4, r, t, p, ty);
-    if (mask) mask[q] = m ? 1 : 0;
-  }
-}
-
 // Row-block order (round 4): the pair tiles of tdm_obs_pairs (each unordered pair once, both
 // directions from one atan2 core), but taken row block by row block so that every 128-B line of
 // the env's [N, N-1, 4] block is written within one short stretch. Row block R (rows 8R .. 8R+7,
@@ -377,10 +242,5 @@ __device__ __forceinline__ void tdm_obs_rowblocks(OT* __restrict__ obs, uint8_t*
   }
 }
 
-#ifdef MACM_TDM_OBS_LINEAR
-#define MACM_TDM_OBS tdm_obs_linear
-#else
-#define MACM_TDM_OBS tdm_obs_pairs
-#endif
 
 }  // namespace macm

@@ -58,13 +58,13 @@ def test_tdm_algorithmic_bytes(bench):
 def test_pmc_summary_matches_the_rollout_kernel(tmp_path):
     pmc = load("pmc_summary_mod", "tools/pmc_summary.py")
     p = tmp_path / "run_counter_collection.csv"
-    rows = [("void macm::env_rollout_w64<0, 64, float, true, false>(macm::RolloutArgs<float>)", "1", "FETCH_SIZE", "10"),
-            ("void macm::env_rollout_w64<0, 64, float, true, false>(macm::RolloutArgs<float>)", "2", "FETCH_SIZE", "30"),
-            ("void macm::env_rollout_w64<0, 64, float, false, false>(macm::RolloutArgs<float>)", "3", "FETCH_SIZE", "99")]
+    rows = [("void macm::env_rollout_w64<0, 64, float, true>(macm::RolloutArgs<float>)", "1", "FETCH_SIZE", "10"),
+            ("void macm::env_rollout_w64<0, 64, float, true>(macm::RolloutArgs<float>)", "2", "FETCH_SIZE", "30"),
+            ("void macm::env_rollout_w64<0, 64, float, false>(macm::RolloutArgs<float>)", "3", "FETCH_SIZE", "99")]
     with open(p, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["Kernel_Name", "Dispatch_Id", "Counter_Name", "Counter_Value"])
         w.writerows(rows)
-    k = "env_rollout_w64<0, 64, float, true, false>"
+    k = "env_rollout_w64<0, 64, float, true>"
     assert pmc.kernel_means(str(p), k)["FETCH_SIZE"] == 20.0
     assert pmc.kernel_means(str(p), k, last=True)["FETCH_SIZE"] == 30.0

@@ -229,40 +229,6 @@ def test_balanced_rollout_equals_per_step(E, N, K, kw):
     assert b.status() == 0
 
 
-@pytest.mark.parametrize("solo,E,N,K,kw", [
-    (16, 600, 64, 40, {"start_spread": 6}),
-    (64, 2100, 64, 32, {"start_spread": 12}),                    # the scalar-sweep instantiation (>= 2048 envs)
-    (5, 70, 40, 33, {"reward_mode": "linear", "coord": "cartesian"}),
-    (8, 8, 64, 32, {}),                                          # solo >= envs: one launch
-])
-def test_solo_split_rollout_equals_per_step(monkeypatch, solo, E, N, K, kw):
-    """The solo split of a balanced rollout (env_rollout_w64<..., SOLO>: the `solo` heaviest envs in
-    waves that own their SIMD, on a second stream, the rest in the ordinary launch) equals per-step
-    launches, open and closed loop, with the reward sums."""
-    from gym_macm.bots import flock_actions as bot_actions
-    monkeypatch.setenv("MACM_SOLO_ENVS", str(solo))
-    b = FlockVec(E, n_agents=[N], seed=29, device="cuda:0", **kw)
-    monkeypatch.delenv("MACM_SOLO_ENVS")
-    a = FlockVec(E, n_agents=[N], seed=29, device="cuda:0", **kw)
-    acts = flock_actions(K, E, N, 31)
-    for k in range(K):
-        a.step(acts[k])
-    b.rollout(acts)
-    assert_same(a, b, "solo open-loop rollout")
-    act_a = bot_actions(a.obs)
-    act_b = act_a.clone()
-    for _ in range(K):
-        a.step(act_a)
-        bot_actions(a.obs, out=act_a)
-    b.rollout_bots(act_b, K)
-    assert_same(a, b, "solo closed-loop rollout")
-    assert torch.equal(act_a, act_b), "the bot's next actions"
-    pa, ta = a.reward_sums()
-    pb, tb = b.reward_sums()
-    np.testing.assert_array_equal(pa, pb)
-    assert ta == tb and b.status() == 0
-
-
 @pytest.mark.parametrize("E,N,K,kw", [
     (40, 100, 12, {"start_spread": 12}),
     (24, 300, 8, {"reward_mode": "linear"}),
@@ -326,73 +292,6 @@ def test_handoff_after_a_long_backlog_on_the_callers_stream(monkeypatch):
     assert b.world.uses_handoff()
     assert b.status() == 0, b.status()
     assert_same(a, b, "handoff behind a backlog")
-
-
-@pytest.mark.parametrize("E,N,K,kw", [
-    (6, 1024, 6, {}),                                   # C5-shaped: every env takes the DFS kernel's walk
-    (12, 300, 8, {"start_spread": 8}),                  # dense and sparse envs mixed
-    (40, 100, 10, {"reward_mode": "linear"}),
-])
-@pytest.mark.parametrize("handoff", ["0", "1"])
-def test_fused_dfs_solve_equals_split(monkeypatch, E, N, K, kw, handoff):
-    """Kernel B with the dense envs' DFS in the same wave (MACM_FUSE_DFS=1, flock_solve_wg<true>) gives the
-    split kernels' results bit for bit, with and without the B -> C handoff."""
-    monkeypatch.setenv("MACM_HANDOFF", handoff)
-    monkeypatch.setenv("MACM_FUSE_DFS", "1")
-    b = FlockVec(E, n_agents=[N], seed=3 * E + N, device="cuda:0", **kw)
-    a = FlockVec(E, n_agents=[N], seed=3 * E + N, device="cuda:0", **kw)
-    acts = flock_actions(K, E, N, 13)
-    for k in range(K):
-        monkeypatch.setenv("MACM_FUSE_DFS", "0")
-        a.step(acts[k])
-        monkeypatch.setenv("MACM_FUSE_DFS", "1")
-        b.step(acts[k])
-    assert_same(a, b, "fused DFS + solve")
-    pa, _ = a.reward_sums()
-    pb, _ = b.reward_sums()
-    np.testing.assert_array_equal(pa, pb)
-
-
-@pytest.mark.parametrize("E,N,K,kw", [
-    (1031, 100, 6, {}),                                  # odd env count: the last wave holds one env
-    (1024, 256, 8, {"targets": [i * 4 // 256 for i in range(256)]}),   # C3-shaped
-    (1026, 300, 4, {"start_spread": 8}),                 # dense and sparse envs, the spill step beside
-    (1024, 120, 6, {"reward_mode": "linear", "obs_dtype": torch.float64}),
-])
-@pytest.mark.parametrize("handoff", ["0", "1"])
-def test_solve_pairs_equal_single(monkeypatch, E, N, K, kw, handoff):
-    """Kernel B with two envs per wave (MACM_SOLVE_PAIR=1, flock_solve_wg_pair) gives the one-env-per-wave
-    kernel's results bit for bit: state, lists, outputs, counters and reward sums, with and without the
-    B -> C handoff."""
-    monkeypatch.setenv("MACM_HANDOFF", handoff)
-    b = FlockVec(E, n_agents=[N], seed=7 * E + N, device="cuda:0", **kw)
-    a = FlockVec(E, n_agents=[N], seed=7 * E + N, device="cuda:0", **kw)
-    acts = flock_actions(K, E, N, 17)
-    for k in range(K):
-        monkeypatch.setenv("MACM_SOLVE_PAIR", "0")
-        a.step(acts[k])
-        monkeypatch.setenv("MACM_SOLVE_PAIR", "1")
-        b.step(acts[k])
-    assert_same(a, b, "paired solve")
-    pa, ta = a.reward_sums()
-    pb, tb = b.reward_sums()
-    np.testing.assert_array_equal(pa, pb)
-    assert ta == tb and b.status() == 0
-
-
-def test_solve_pairs_in_slices(monkeypatch):
-    """The sliced rollout (3 slices of >= 1024 envs) with paired solves equals one-env-per-wave steps."""
-    E, N, K = 3100, 80, 5
-    b = FlockVec(E, n_agents=[N], seed=3, device="cuda:0")
-    a = FlockVec(E, n_agents=[N], seed=3, device="cuda:0")
-    acts = flock_actions(K, E, N, 19)
-    monkeypatch.setenv("MACM_SOLVE_PAIR", "0")
-    for k in range(K):
-        a.step(acts[k])
-    monkeypatch.setenv("MACM_SOLVE_PAIR", "1")
-    monkeypatch.setenv("MACM_WG_SLICES", "3")
-    b.rollout(acts)
-    assert_same(a, b, "paired solve in slices")
 
 
 def test_handoff_is_off_under_serialized_dispatch():
