@@ -35,6 +35,9 @@ B_ALG = 107  # bytes per agent-step: state r+w 2x40, action 3, obs 20, reward 4 
 # dependent VALU chain, one wave alone on its SIMD (tools/ubench_level.hip V3 / V14 on the MI355X,
 # profiles/r05/ubench/), and the shader clock those cycles run at (V0: 278.1 cycles = 117.1 ns)
 C_VEL_LEVEL, C_POS_LEVEL, SHADER_GHZ = 208.0, 236.5, 2.375
+# the same chains on packed (x, y) pairs (V5 / V16, profiles/r05/ubench/): the form kernel B, the spill
+# step and the wave kernel's wide levels run; roofline.chain_frac_packed prices against these
+C_VEL_LEVEL_PK, C_POS_LEVEL_PK = 155.4, 224.1
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 SCALAR_SWEEP_MIN_ENVS = 2048  # = kScalarSweepMinEnvs in gym-macm_amd/csrc/flock_step_w64.hip
 
@@ -126,7 +129,7 @@ def cpu_baseline(n_agents, seed, budget_s=15.0, n_envs=4096, warmup=5, steps=20,
     return base, lv
 
 
-def chain_floor(levels, rollout, vel_iters=8, pos_iters=3):
+def chain_floor(levels, rollout, vel_iters=8, pos_iters=3, c_vel=C_VEL_LEVEL, c_pos=C_POS_LEVEL):
     """The Gauss-Seidel chain floor of the timed window, per step: every velocity and position pass
     steps each level of an env's island order once ((1 + vel_iters) x C_VEL_LEVEL + pos_iters x
     C_POS_LEVEL cycles per level, the dependent VALU floors of one wave alone on its SIMD), and a
@@ -137,11 +140,11 @@ def chain_floor(levels, rollout, vel_iters=8, pos_iters=3):
     K = L.shape[0]
     per_launch, pipelined = int(L.max(axis=1).sum()), int(L.sum(axis=0).max())
     lv = pipelined if rollout else per_launch
-    cyc = (1 + vel_iters) * C_VEL_LEVEL + pos_iters * C_POS_LEVEL
+    cyc = (1 + vel_iters) * c_vel + pos_iters * c_pos
     ms = lv * cyc / (SHADER_GHZ * 1e9) * 1e3 / K
     return ms, {"levels_per_step_deepest": [int(x) for x in L.max(axis=1)], "levels_mean": float(L.mean()),
                 "sum_k_max_e": per_launch, "max_e_sum_k": pipelined, "steps_sampled": K,
-                "cycles_per_level": cyc, "c_vel": C_VEL_LEVEL, "c_pos": C_POS_LEVEL, "ghz": SHADER_GHZ}
+                "cycles_per_level": cyc, "c_vel": c_vel, "c_pos": c_pos, "ghz": SHADER_GHZ}
 
 
 def b_alg_tdm(n_agents, obs_f64=False):
@@ -629,6 +632,9 @@ def main():
                     out["roofline"]["chain_floor_ms"] = fl_ms
                     out["roofline"]["chain_frac"] = fl_ms / kernel_ms
                     out["roofline"]["chain_floor"] = fl
+                    fp_ms, _ = chain_floor(lv, rollout and N <= 64, c_vel=C_VEL_LEVEL_PK, c_pos=C_POS_LEVEL_PK)
+                    out["roofline"]["chain_floor_packed_ms"] = fp_ms
+                    out["roofline"]["chain_frac_packed"] = fp_ms / kernel_ms
             else:
                 out["cpu_baseline"] = cpu_baseline_tdm(teams, args.seed, args.cpu_budget, E, W, K)
         else:
