@@ -1171,28 +1171,33 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       ncoll += block_scan_excl(act[j] && coll[j] ? 1 : 0, dummy, s_scan);  // also orders the B.pos reads
       npos += block_scan_excl(act[j] && rew[j] > 0.0f ? 1 : 0, dummy, s_scan);  // before the write-back
     }
-    double rsum;  // thread 0: the step's reward sum in agent-slot order (flock_common.hpp)
-    if constexpr (BPT == 1) {
-      rsum = block_pairwise_sum((double)rew[0], reinterpret_cast<double*>(s_scan));
-    } else {
-      double* s_grp = reinterpret_cast<double*>(s_slp);  // the sleep clocks are dead: 64-body group sums
-      const int gw = BS / W;
+    // thread 0: the step's reward sum in agent-slot order (flock_common.hpp); linear rewards only, a
+    // binary step sums to npos - ncoll exactly (macm_world_reward_sums)
+    double rsum = 0.0;
+    const bool lin = P.reward_mode == MACM_REWARD_LINEAR;
+    if (lin) {
+      if constexpr (BPT == 1) {
+        rsum = block_pairwise_sum((double)rew[0], reinterpret_cast<double*>(s_scan));
+      } else {
+        double* s_grp = reinterpret_cast<double*>(s_slp);  // the sleep clocks are dead: 64-body group sums
+        const int gw = BS / W;
 #pragma unroll
-      for (int j = 0; j < BPT; ++j) {
-        const double g = wave_pairwise_sum((double)rew[j]);
-        if ((tid & (W - 1)) == 0) s_grp[j * gw + tid / W] = g;
+        for (int j = 0; j < BPT; ++j) {
+          const double g = wave_pairwise_sum((double)rew[j]);
+          if ((tid & (W - 1)) == 0) s_grp[j * gw + tid / W] = g;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          const int ng = BPT * gw;
+          int n2 = 1;
+          while (n2 < ng) n2 <<= 1;
+          for (int q = ng; q < n2; ++q) s_grp[q] = 0.0;
+          for (int h = 1; h < n2; h <<= 1)
+            for (int q = 0; q + h < n2; q += 2 * h) s_grp[q] = s_grp[q] + s_grp[q + h];
+          rsum = s_grp[0];
+        }
+        __syncthreads();
       }
-      __syncthreads();
-      if (tid == 0) {
-        const int ng = BPT * gw;
-        int n2 = 1;
-        while (n2 < ng) n2 <<= 1;
-        for (int q = ng; q < n2; ++q) s_grp[q] = 0.0;
-        for (int h = 1; h < n2; h <<= 1)
-          for (int q = 0; q + h < n2; q += 2 * h) s_grp[q] = s_grp[q] + s_grp[q + h];
-        rsum = s_grp[0];
-      }
-      __syncthreads();
     }
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
@@ -1221,7 +1226,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
       ec[1] += (unsigned long long)ncoll;
       ec[2] += (unsigned long long)npos;
       ec[3] += (unsigned long long)dn;
-      add_reward_sum(B, e, rsum);
+      if (lin) add_reward_sum(B, e, rsum);
       if (B.spill_count) B.spill_count[e] += 1u;
     }
     SSTAMP(11);

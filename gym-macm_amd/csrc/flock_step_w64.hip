@@ -1977,7 +1977,8 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
   if constexpr (!kT) {
     c1 = __popcll(__ballot(act && coll));        // collided agent-steps
     c2 = __popcll(__ballot(act && rew > 0.0f));  // positive-reward agent-steps
-    rsum = wave_pairwise_sum((double)rew);  // lanes >= N: rew = +0.0
+    // linear rewards only: a binary step sums to c2 - c1 exactly (macm_world_reward_sums)
+    if (P.reward_mode == MACM_REWARD_LINEAR) rsum = wave_pairwise_sum((double)rew);  // lanes >= N: rew = +0.0
   } else {
     c1 = __popcll(att_m);               // melee attacks
     c2 = __popcll(alive0_m & ~livem);   // deaths
@@ -2018,7 +2019,9 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     ulonglong2* ec = reinterpret_cast<ulonglong2*>(B.env_counters + (size_t)e * 4);
     ec[0] = make_ulonglong2(ctr[0] + c0, ctr[1] + c1);
     ec[1] = make_ulonglong2(ctr[2] + c2, ctr[3] + (unsigned long long)dn);
-    if constexpr (!kT) add_reward_sum(B, e, rsum);
+    if constexpr (!kT) {
+      if (P.reward_mode == MACM_REWARD_LINEAR) add_reward_sum(B, e, rsum);
+    }
   }
   STAMP(13);
 #ifdef MACM_TIMELINE

@@ -2064,7 +2064,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   int dummy;  // both counts in one scan (collided in the low half, rewarded in the high)
   const int cp = block_scan_excl((act && coll ? 1 : 0) | (act && rew > 0.0f ? 0x10000 : 0), dummy, s_scan);
   const int ncoll = cp & 0xffff, npos = cp >> 16;
-  const double rsum = block_pairwise_sum((double)rew, reinterpret_cast<double*>(s_scan));  // thread 0
+  const bool lin = P.reward_mode == MACM_REWARD_LINEAR;  // binary steps: c2 - c1 (macm_world_reward_sums)
+  const double rsum = lin ? block_pairwise_sum((double)rew, reinterpret_cast<double*>(s_scan)) : 0.0;  // thread 0
   if (status) atomicOr(&s_misc[1], status);
   __syncthreads();
   WSTAMP(8);
@@ -2089,7 +2090,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     ec[1] += (unsigned long long)ncoll;
     ec[2] += (unsigned long long)npos;
     ec[3] += (unsigned long long)dn;
-    add_reward_sum(B, e, rsum);
+    if (lin) add_reward_sum(B, e, rsum);
   }
   WSTAMP(9);
 #ifdef MACM_STAMPS

@@ -1055,13 +1055,25 @@ int macm_world_reset_counters(macm_world* w, void* stream) {
 // Per-env reward sums (flock_common.hpp: each step's float32 rewards as float64, pairwise over the
 // agent slots, added to the env's total in step order) and their sum over envs in env order, starting
 // from +0.0: a fixed order throughout, so the total is bit-stable for any launch form or env slicing.
+// Binary rewards are -1, 0 or +1, so every partial sum in that order is an exact integer and an env's
+// total is exactly (positive-reward agent-steps) - (collided agent-steps), its counters 2 and 1: the
+// kernels accumulate env_rsum for linear rewards only (a binary world's per-step sum and atomic add
+// cost 2.5% of the steady-state step, profiles/r06/abtests/rsum/).
 int macm_world_reward_sums(macm_world* w, double* per_env, double* total, void* stream) {
   if (!w || (!per_env && !total)) return fail(MACM_E_INVALID, "NULL argument");
   DeviceGuard g(w->device);
   std::vector<double> h((size_t)w->P.n_envs);
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemcpyAsync(h.data(), w->B.env_rsum, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (w->P.reward_mode == MACM_REWARD_LINEAR) {
+    HIP_TRY(hipMemcpyAsync(h.data(), w->B.env_rsum, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else {
+    std::vector<unsigned long long> c(h.size() * 4);
+    HIP_TRY(hipMemcpyAsync(c.data(), w->B.env_counters, c.size() * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (size_t e = 0; e < h.size(); ++e) h[e] = (double)((long long)c[e * 4 + 2] - (long long)c[e * 4 + 1]);
+  }
   if (per_env) memcpy(per_env, h.data(), h.size() * sizeof(double));
   if (total) {
     double acc = 0.0;

@@ -421,7 +421,9 @@ int macm_world_reset_counters(macm_world* w, void* stream);  /* also zeroes the 
  * in a fixed order so that it is bit-stable (ABI 8): each step's float32 rewards are summed as
  * float64 pairwise over the agent slots 0 .. P-1 (P = 64 * 2^ceil(log2(ceil(N / 64))), +0.0 past N:
  * ((r0 + r1) + (r2 + r3)) + ...), that sum is added to the env's total in step order, and `total`
- * is the envs' totals summed in env order from +0.0. per_env: host double [E] or NULL; total: host
+ * is the envs' totals summed in env order from +0.0. Binary rewards (-1, 0, +1) make every partial sum
+ * an exact integer, so a binary world's env total is read as counter 2 - counter 1 (the same bits; the
+ * kernels accumulate the float64 sums for linear rewards only). per_env: host double [E] or NULL; total: host
  * double or NULL (not both NULL). Accumulated by every step since creation or reset_counters;
  * synchronises `stream`. Multi-GPU: gather the per-env totals and sum them in global env order
  * (gym_macm.dist.reduce_reward_sums), which gives the single-process total at any rank count.

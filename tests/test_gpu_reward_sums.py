@@ -9,7 +9,10 @@ count, so the linear mode — values like 1 - d/35 — is what tests the order) 
 and step path: the wave kernel per step and in one rollout launch, the workgroup path with a
 number of waves that is not a power of two, the env slices on their own streams, the spill step,
 the trajectory form at the metric size (self-consistency with the rewards it returns) and the
-closed loop. Every tests/ rollout through test_gpu_parity.check_rollout checks the sums too."""
+closed loop. Every tests/ rollout through test_gpu_parity.check_rollout checks the sums too, in
+binary mode as well, where the library reads an env's total from its counters (positive-reward minus
+collided agent-steps: the same bits, every partial sum of -1 / 0 / +1 values being an exact integer)
+instead of accumulating it in the kernels."""
 import numpy as np
 import pytest
 import torch
