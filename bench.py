@@ -405,6 +405,7 @@ def main():
             policy()
     rollout = args.launch == "rollout"
     traj = world_h.trajectory_buffers(K) if use_traj else None
+    traj_out = world_h.traj_outputs(traj) if use_traj else None  # the C-ABI struct, built outside the timing
     rname = ("macm_world_rollout" if args.env == "flock" else "macm_tdm_rollout") + ("_traj" if traj is not None else "")
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}, "
         f"{'one rollout launch' if rollout else 'one launch per step'}")
@@ -432,12 +433,12 @@ def main():
         if launched:
             dist.barrier()
         torch.cuda.synchronize(dev)
+        ev0.record(stream)  # on the idle stream: its timestamp falls just before t0
         t0 = time.perf_counter()
-        ev0.record(stream)
         if roll and args.policy == "bots":
             world_h.rollout_bots_raw(loop_ptr, K, sh)
         elif roll and traj is not None:
-            world_h.rollout_traj_raw(base + W * stride, K, traj, sh)
+            world_h.rollout_traj_raw(base + W * stride, K, traj_out, sh)
         elif roll:
             world_h.rollout_raw(base + W * stride, K, sh)
         else:

@@ -198,10 +198,14 @@ class TdmWorld:
                              "world's device")
         return self._traj_call(self.L.macm_tdm_rollout_bots_traj, "macm_tdm_rollout_bots_traj", actions, K, traj)
 
-    def rollout_traj_raw(self, actions_ptr: int, n_steps: int, traj: dict, stream_handle: int) -> None:
+    def traj_outputs(self, traj: dict):
+        """The C-ABI outputs struct of trajectory buffers, built once for repeated rollout_traj_raw calls."""
+        return _abi.MacmTdmOutputs(*[_ptr(traj.get(k)) for k in self._TRAJ_KEYS])
+
+    def rollout_traj_raw(self, actions_ptr: int, n_steps: int, traj, stream_handle: int) -> None:
         """Minimal-overhead trajectory rollout for timed loops (no validation); ``traj`` from
-        trajectory_buffers(n_steps)."""
-        out = _abi.MacmTdmOutputs(*[_ptr(traj.get(k)) for k in self._TRAJ_KEYS])
+        trajectory_buffers(n_steps), or its traj_outputs(traj)."""
+        out = traj if isinstance(traj, _abi.MacmTdmOutputs) else self.traj_outputs(traj)
         self.L.macm_tdm_rollout_traj(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(out),
                                      ctypes.c_void_p(stream_handle))
 
