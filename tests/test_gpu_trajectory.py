@@ -188,3 +188,42 @@ def test_trajectory_buffers_are_checked_before_the_launch():
         with pytest.raises(ValueError):
             w.rollout_traj(ta, t)
     w.rollout_traj(ta, tg)
+
+
+def test_raw_trajectory_launch_forms_agree():
+    """bench.py's timed launch: rollout_traj_launcher (ctypes arguments and the outputs struct built
+    before the timed region) writes what rollout_traj_raw and the checked rollout write."""
+    E, N, K = 96, 64, 7
+    a = FlockVec(E, n_agents=[N], seed=21, device="cuda:0")
+    b = FlockVec(E, n_agents=[N], seed=21, device="cuda:0")
+    c = FlockVec(E, n_agents=[N], seed=21, device="cuda:0")
+    acts = flock_actions(K, E, N, 17)
+    ref = a.rollout(acts, trajectory=True)
+    sh = torch.cuda.current_stream().cuda_stream
+    buf_b = b.world.trajectory_buffers(K)
+    b.world.rollout_traj_raw(acts.data_ptr(), K, buf_b, sh)
+    buf_c = c.world.trajectory_buffers(K)
+    go = c.world.rollout_traj_launcher(acts.data_ptr(), K, c.world.traj_outputs(buf_c), sh)
+    go()
+    torch.cuda.synchronize()
+    assert_traj(ref, buf_b, "rollout_traj_raw")
+    assert_traj(ref, buf_c, "rollout_traj_launcher")
+    for v in (b, c):
+        sa, sv = a.world.get_state(), v.world.get_state()
+        for k in sa:
+            np.testing.assert_array_equal(sa[k], sv[k], err_msg=f"state[{k}]")
+
+
+def test_raw_tdm_trajectory_launch_forms_agree():
+    E, teams, K = 40, [16, 16], 6
+    a, b = tdm_pair(teams, E)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(4)
+    acts = torch.randint(0, 3, (K, E, 32, 4), dtype=torch.uint8, device="cuda:0", generator=g)
+    ref = a.rollout_traj(acts)
+    buf = b.trajectory_buffers(K)
+    go = b.rollout_traj_launcher(acts.data_ptr(), K, b.traj_outputs(buf), torch.cuda.current_stream().cuda_stream)
+    go()
+    torch.cuda.synchronize()
+    assert_traj(ref, buf, "TDM rollout_traj_launcher")
+    assert_tdm_state(a, b)
