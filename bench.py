@@ -528,13 +528,25 @@ def main():
                         f", from reset (seed {args.seed:#x})")
         # MACM_LAUNCH_SPLIT_OBS: every TDM step / rollout but the closed-loop rollout (its bot reads each
         # step's observation inside the launch)
-        split = (args.env == "tdm" and N <= 64 and bool(world_h.launch_flags() & 2)
+        lflags = world_h.launch_flags() if args.env == "tdm" else 0
+        split = (args.env == "tdm" and N <= 64 and bool(lflags & 2)
                  and not (rollout and args.policy == "bots"))
+        # MACM_LAUNCH_TAIL_OBS: the trajectory rollout observes in the tail of its own launch (TailObs)
+        tail = (args.env == "tdm" and N <= 64 and bool(lflags & 4) and rollout and traj is not None
+                and args.policy == "random")
+        if tail:
+            split = False
         slices = world_h.rollout_slices() if (args.env == "flock" and N > 64) else 0
         if split:  # TDM below 1024 envs: pose snapshots, the observation in a kernel of its own
             kname += " + tdm_observe_snap<" + ("double" if args.obs_f64 else "float") + ">"
+        if tail:
+            kname += " (tail observation)"
         if rollout and N <= 64:
-            if split and traj is not None:
+            if tail:
+                launch_desc = (f"one {rname} launch for the K timed steps: each env's wave steps its K steps writing "
+                               "pose snapshots, then the finished waves and one observe-only wave per env observe "
+                               "the (step, env) rows beside the remaining envs' physics")
+            elif split and traj is not None:
                 launch_desc = (f"{rname}: the K timed steps in rollout launches of 8 steps that write pose "
                                "snapshots, each chunk's observation (tdm_observe_snap) on a second stream beside "
                                "the next chunk's physics")

@@ -136,6 +136,19 @@ __device__ __forceinline__ float2 ld_wt(const float2* p) {
       __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return make_float2(__uint_as_float((unsigned int)w), __uint_as_float((unsigned int)(w >> 32)));
 }
+// The tail observation's control words (flock_step_w64.hip TailObs): per launch-tag parity kTailQ row
+// counters, each in a 128-B line of its own, then one ready word per env
+constexpr int kTailQ = 16, kTailLine = 16;
+__host__ __device__ constexpr size_t tail_ctl_words(int n_envs) { return 2 * kTailQ * kTailLine + (size_t)n_envs; }
+
+__device__ __forceinline__ void st_wt4(float4* p, float4 v) {
+  st_wt(reinterpret_cast<float2*>(p), make_float2(v.x, v.y));
+  st_wt(reinterpret_cast<float2*>(p) + 1, make_float2(v.z, v.w));
+}
+__device__ __forceinline__ float4 ld_wt4(const float4* p) {
+  const float2 a = ld_wt(reinterpret_cast<const float2*>(p)), b = ld_wt(reinterpret_cast<const float2*>(p) + 1);
+  return make_float4(a.x, a.y, b.x, b.y);
+}
 __device__ __forceinline__ void st_wt(uint8_t* p, uint8_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

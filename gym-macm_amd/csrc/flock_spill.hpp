@@ -1099,7 +1099,7 @@ __device__ __forceinline__ void step_env(const StepParams& P, const WorldBuffers
 #pragma unroll
       for (int j = 0; j < BPT; ++j) {
         const int i = tid + j * BS;
-        if (i < N) TB->snap_out[(size_t)e * N + i] = make_float4(s_c[i].x, s_c[i].y, s_slp[i], act[j] ? 1.0f : 0.0f);
+        if (i < N) st_wt4(TB->snap_out + (size_t)e * N + i, make_float4(s_c[i].x, s_c[i].y, s_slp[i], act[j] ? 1.0f : 0.0f));
       }
     } else if (wide) {
       tdm_obs_block_linear<OT>(obs ? obs + rows * 4 : nullptr, TB->mask_out ? TB->mask_out + rows : nullptr, N, tid,

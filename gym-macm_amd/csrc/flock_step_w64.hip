@@ -758,6 +758,105 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
   return total;
 }
 
+// ---- the tail observation (round 6) -----------------------------------------------------------------
+// A TDM trajectory rollout whose envs all fit the chip at once. The fused form observes inside each
+// env's wave after every step (55% of a wave's cycles at 2 x 16), so the launch ends with the heaviest
+// env's K physics steps plus its K observations. Here every wave steps its env's K steps writing
+// only pose snapshots (write-through, st_wt4) and, each step, the number of its steps whose snapshots
+// have drained (its ready word); a wave that has finished its own steps then observes (step, env) rows
+// in step-major order from a shared counter, each once its env's ready word covers the step, until
+// all K x E rows are taken. Extra blocks (blockIdx.x >= E) only observe. The observations of the envs
+// that end first run beside the heaviest envs' physics. A wait that does not end within ~1 s (never
+// expected: every env's wave is resident, macm_capi checks the occupancy, and never waits) reports
+// MACM_ST_HANDOFF and ends the worker. Each row is the fused form's observation of the same snapshot
+// values (tdm_obs_rowblocks / tdm_obs_pairs), bit for bit.
+struct TailObs {
+  unsigned long long* ctl;  // tail_ctl_words(E) words (flock_common.hpp): row counters, then ready words
+  unsigned int tag;         // this launch's tag (> 0); the ready word of env e holds tag << 32 | steps stored
+  int nsteps;               // K
+  int k;                    // physics: the step this call takes (steps 0 .. k - 1 are complete)
+  bool worker;              // this call observes one claimed row instead of stepping
+  bool more;                // worker: false once every row is taken (or a wait gave up)
+  int q, left;              // worker: the sub-queue it claims from, sub-queues not yet found empty
+  int r, r_end;             // worker: the rows of its current claim (sub-queue-local, step-major)
+};
+// The rows are split into kTailQ sub-queues by env range (a single counter, one device-scope atomic
+// per row, serialised at ~9 ns per claim: 81,920 rows of C4 cost more than the observation saved); a
+// worker starts on sub-queue blockIdx % kTailQ and takes kTailChunk rows per claim, moving on when its
+// sub-queue is empty.
+constexpr int kTailChunk = 2;
+constexpr unsigned kTailSpins = 1u << 20;
+
+__device__ __forceinline__ unsigned long long* tail_counter(const TailObs& tl, int q) {
+  return tl.ctl + (size_t)(((tl.tag & 1u) * kTailQ + q) * kTailLine);
+}
+
+template <typename OT>
+__device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
+                                             const TdmBuffers& TB, OT* obs, TailObs& tl, int lane, float2* s_c,
+                                             float* s_ang, float4* stage, bool staged) {
+  const int E = P.n_envs, N = P.n_agents;
+  auto env0 = [E](int q) { return (int)(((long long)E * q) / kTailQ); };
+  while (tl.r >= tl.r_end) {  // claim kTailChunk rows of the current sub-queue, else move on
+    if (tl.left == 0) {
+      tl.more = false;
+      return;
+    }
+    const int ne = env0(tl.q + 1) - env0(tl.q);
+    const int nrows = tl.nsteps * ne;
+    int c = 0;
+    if (lane == 0 && ne > 0)
+      c = (int)__hip_atomic_fetch_add(tail_counter(tl, tl.q), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c = __builtin_amdgcn_readfirstlane(c);
+    if (ne == 0 || (long long)c * kTailChunk >= nrows) {
+      tl.q = tl.q + 1 == kTailQ ? 0 : tl.q + 1;
+      --tl.left;
+      continue;
+    }
+    tl.r = c * kTailChunk;
+    tl.r_end = min(tl.r + kTailChunk, nrows);
+  }
+  const int e0 = env0(tl.q), ne = env0(tl.q + 1) - e0;
+  const int i = tl.r++;
+  const int k = i / ne, e = e0 + (i - k * ne);
+  int ok = 1;
+  if (lane == 0) {
+    ok = 0;
+    for (unsigned it = 0; it < kTailSpins; ++it) {
+      const unsigned long long v = __hip_atomic_load(tl.ctl + 2 * kTailQ * kTailLine + e, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(v >> 32) == tl.tag && (unsigned)v > (unsigned)k) {
+        ok = 1;
+        break;
+      }
+      if (it < 16) __builtin_amdgcn_s_sleep(2);
+      else __builtin_amdgcn_s_sleep(32);  // a long wait: poll ~1 us apart
+    }
+    if (!ok) report_status(B, MACM_ST_HANDOFF);
+  }
+  if (!__builtin_amdgcn_readfirstlane(ok)) {
+    tl.more = false;
+    return;
+  }
+  const size_t row = ((size_t)k * E + e) * N;  // the snapshot row: [K, E, N]
+  float4 sn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (lane < N) sn = ld_wt4(TB.snap_out + row + lane);
+  s_c[lane] = make_float2(sn.x, sn.y);
+  s_ang[lane] = sn.z;
+  const unsigned long long livem = __ballot(lane < N && sn.w != 0.0f);
+  __syncthreads();
+  const size_t slots = row * (N - 1);
+  OT* const obs_r = obs ? obs + slots * 4 : nullptr;
+  uint8_t* const mask_r = TB.mask_out ? TB.mask_out + slots : nullptr;
+  if constexpr (sizeof(OT) == 4) {
+    if (staged) tdm_obs_rowblocks<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang, stage);
+    else tdm_obs_pairs<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang);
+  } else {
+    tdm_obs_pairs<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang);
+  }
+  __syncthreads();  // the next row's snapshot overwrites s_c, s_ang and the stage
+}
+
 // MODE kFlock: Flock.step. MODE kTdm: TDM.step (combat.py:104-184) — the same
 // physics with alive masks, plus melee ray casts, health, deaths and the full
 // relative observation; `TP`/`TB` are unused for Flock.
@@ -770,7 +869,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     const StepParams& P, const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur,
     const void* __restrict__ actions, OT* __restrict__ obs, int32_t* __restrict__ nbr_out,
     float* __restrict__ rew_out, uint8_t* __restrict__ coll_out, uint8_t* __restrict__ done_out,
-    const int e = blockIdx.x, const int lane = threadIdx.x) {
+    const int e = blockIdx.x, const int lane = threadIdx.x, TailObs* tl = nullptr) {
   constexpr bool kT = MODE == kTdm;
 #ifdef MACM_TIMELINE
   const unsigned long long tl_rt0 = __builtin_amdgcn_s_memrealtime(), tl_c0 = __builtin_amdgcn_s_memtime();
@@ -835,6 +934,13 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
 #ifdef MACM_STAMPS
   __shared__ int s_stat_maxisl;
 #endif
+  if constexpr (kT) {
+    if (tl && tl->worker) {  // the tail observation: one (step, env) row instead of a step
+      tdm_tail_row<OT>(P, B, TP, TB, obs, *tl, lane, s_c, s_ang, reinterpret_cast<float4*>(&s_pool),
+                       tdm_obs_rb_stage_bytes(N) <= (int)sizeof(Pool));
+      return;
+    }
+  }
 
   // ---- every global load the step needs, issued up front ---------------------
   const uint32_t* cab = B.cab[cur] + (size_t)e * C;
@@ -1341,6 +1447,17 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
 
   __syncthreads();
   STAMP(4);
+  if constexpr (kT) {
+    // the tail observation: steps 0 .. k - 1 are complete and their write-through snapshot stores
+    // drained by now (waiting here costs nothing: this step has stored nothing yet), so the ready word
+    // can say k
+    if (tl && tl->ctl && tl->k > 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      if (lane == 0)
+        __hip_atomic_store(tl->ctl + 2 * kTailQ * kTailLine + e, ((unsigned long long)tl->tag << 32) | (unsigned)tl->k,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 
   const int nisl = s_nisl;
   const float mA = P.inv_mass, mB = P.inv_mass;
@@ -1951,7 +2068,7 @@ __device__ __attribute__((always_inline)) inline void step_w64_body(
     if (TB.snap_out) {  // the split observation: the pose snapshot tdm_observe_snap observes
       if (lane < N) {
         const float2 c = s_c[lane];
-        TB.snap_out[ag] = make_float4(c.x, c.y, ang, act ? 1.0f : 0.0f);
+        st_wt4(TB.snap_out + ag, make_float4(c.x, c.y, ang, act ? 1.0f : 0.0f));  // write-through: the tail observation
       }
     } else {
       const size_t rows = (size_t)e * N * (N - 1);
@@ -2085,7 +2202,10 @@ struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   // register allocation) stays the measured one: without them the driver window ran 1.1% slower, with
   // them 0.3% (in noise) against the library before the removal (profiles/r06/abtests/cleanup/).
   int sched_off;
-  unsigned long long* reserved;
+  // the tail observation (TailObs; TDM trajectory rollouts, macm_capi tdm_tail_obs): its counters and
+  // ready words, and this launch's tag (0: off; blocks beyond n_envs then do not exist)
+  unsigned long long* tail_ctl;
+  unsigned int tail_tag;
 };
 
 // [K, ...] row k of an output (trajectory form); NULL stays NULL
@@ -2142,8 +2262,13 @@ template <int MODE, int NCAP, typename OT, bool SCAL = false>
 __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env_rollout_w64(RolloutArgs<OT> A0) {
   const int nsteps = A0.nsteps;
   const bool bal = A0.B.sched && nsteps >= kRollBalanceMinSteps;  // as in launch_roll
-  const int env = bal ? (int)A0.B.sched[A0.sched_off + blockIdx.x] : (int)blockIdx.x;
-  for (int k = 0; k < nsteps; ++k) {
+  // TDM tail observation: blocks beyond the envs only observe (TailObs)
+  const bool phys = MODE != kTdm || (int)blockIdx.x < A0.P.n_envs;
+  const int env = bal && phys ? (int)A0.B.sched[A0.sched_off + blockIdx.x] : (int)blockIdx.x;
+  // (the body gets &tl itself in TDM, never a select of it, so that tl stays in registers; ctl NULL = off)
+  TailObs tl{A0.tail_tag ? A0.tail_ctl : nullptr, A0.tail_tag, nsteps, 0, false, true, (int)(blockIdx.x % kTailQ), kTailQ, 0, 0};
+  const int ksteps = phys ? nsteps : 0;
+  for (int k = 0; k < ksteps; ++k) {
     // each step reads its parameters from the kernel arguments afresh, through a pointer the
     // compiler cannot see through, so nothing derived from them stays live across the loop
     const __attribute__((address_space(4))) RolloutArgs<OT>* ka =
@@ -2171,11 +2296,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     // of its 128 VGPRs and kept 7 of them in scratch, re-read every step (rollout: 28 B per lane).
     int sl = (int)threadIdx.x;
     if constexpr (MODE == kTdm) asm volatile("" : "+v"(sl));
+    tl.k = k;
     step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, TB, A.cur ^ (k & 1),
                                         pol_in ? pol_in : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
                                         obs, traj_row(A.nbr_out, kr, EN), traj_row(A.rew_out, kr, EN),
                                         traj_row(A.coll_out, kr, EN), traj_row(A.done_out, kr, (size_t)A.P.n_envs),
-                                        env, sl);
+                                        env, sl, MODE == kTdm ? &tl : nullptr);
     // the next step reads only what this wave wrote: workgroup scope (this CU's L1 and its XCD's L2)
     // suffices; agent scope would write back and invalidate the L2 every step (5x slower, measured)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -2193,12 +2319,48 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       __syncthreads();
     }
   }
+  if constexpr (MODE == kTdm) {
+    if (tl.ctl) {  // the tail observation: publish the last step, then observe rows until none is left
+      if (phys) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (threadIdx.x == 0)
+          __hip_atomic_store(tl.ctl + 2 * kTailQ * kTailLine + env, ((unsigned long long)tl.tag << 32) | (unsigned)nsteps,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (blockIdx.x == 0 && threadIdx.x < kTailQ)  // the next launch's row counters (not this launch's)
+        __hip_atomic_store(tl.ctl + (size_t)((((tl.tag + 1u) & 1u) * kTailQ + threadIdx.x) * kTailLine), 0ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tl.worker = true;
+      int sl = (int)threadIdx.x;
+      asm volatile("" : "+v"(sl));
+      while (tl.more)
+        step_w64_body<MODE, NCAP, OT, SCAL>(A0.P, A0.B, A0.TP, A0.TB, A0.cur, nullptr, A0.obs, nullptr, nullptr, nullptr,
+                                            nullptr, env, sl, &tl);
+    }
+  }
+}
+
+// Resident blocks of the TDM rollout kernel on this device (the tail observation needs every block
+// of a launch resident at once: a worker waits for envs whose waves must be running)
+int tdm_rollout_resident_blocks(int n_agents, bool obs_f64) {
+  const void* k = n_agents <= 32 ? (obs_f64 ? (const void*)env_rollout_w64<kTdm, 32, double>
+                                            : (const void*)env_rollout_w64<kTdm, 32, float>)
+                                 : (obs_f64 ? (const void*)env_rollout_w64<kTdm, 64, double>
+                                            : (const void*)env_rollout_w64<kTdm, 64, float>);
+  int per = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, W, 0) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return per * cus;
 }
 
 template <int MODE, int NCAP, typename OT, bool SCAL = false>
 static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStream_t s, const StepParams& P,
                         const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
-                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done) {
+                        void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
+                        unsigned long long* tail_ctl = nullptr, unsigned tail_tag = 0u, int tail_workers = 0) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
   const bool bal = B.sched && nsteps >= kRollBalanceMinSteps;
@@ -2210,8 +2372,10 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
                        reinterpret_cast<const uint32_t*>(B.ccount[cur]), B.sched, P.n_envs, CB, nullptr);
     if (hipPeekAtLastError() != hipSuccess) return;  // no rollout on a stale order (the caller reports it)
   }
-  RolloutArgs<OT> A{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol, traj, 0, nullptr};
-  hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(P.n_envs), dim3(W), 0, s, A);
+  RolloutArgs<OT> A{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol, traj, 0,
+                    tail_ctl, tail_tag};
+  const int blocks = P.n_envs + (tail_tag ? tail_workers : 0);
+  hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(blocks), dim3(W), 0, s, A);
 }
 
 // the same instantiation choice as launch_step_w64 / launch_tdm_step_w64
@@ -2247,22 +2411,23 @@ hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cu
 
 hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
-                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride, int traj) {
+                                  uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride, int traj,
+                                  unsigned long long* tail_ctl, unsigned tail_tag, int tail_workers) {
   const bool small = P.n_agents <= 32;
   if (obs_f64) {
     if (small)
       launch_roll<kTdm, 32, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                    nullptr, done);
+                                    nullptr, done, tail_ctl, tail_tag, tail_workers);
     else
       launch_roll<kTdm, 64, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                    nullptr, done);
+                                    nullptr, done, tail_ctl, tail_tag, tail_workers);
   } else {
     if (small)
       launch_roll<kTdm, 32, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                   nullptr, done);
+                                   nullptr, done, tail_ctl, tail_tag, tail_workers);
     else
       launch_roll<kTdm, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                   nullptr, done);
+                                   nullptr, done, tail_ctl, tail_tag, tail_workers);
   }
   return hipGetLastError();
 }

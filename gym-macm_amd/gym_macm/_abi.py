@@ -78,6 +78,7 @@ class MacmState(Structure):
 
 LAUNCH_HANDOFF = 1  # macm_world_info.launch_flags
 LAUNCH_SPLIT_OBS = 2  # macm_tdm_launch_flags
+LAUNCH_TAIL_OBS = 4  # macm_tdm_launch_flags: trajectory rollouts take the tail observation
 
 
 class MacmWorldInfo(Structure):

@@ -315,7 +315,8 @@ class TdmWorld:
 
     def launch_flags(self) -> int:
         """MACM_LAUNCH_* of the next step / rollout (macm_tdm_launch_flags): LAUNCH_SPLIT_OBS when the
-        observation is written by its own kernel from pose snapshots (fewer than 1024 envs)."""
+        observation is written by its own kernel from pose snapshots (fewer than 1024 envs),
+        LAUNCH_TAIL_OBS when trajectory rollouts take the tail observation (fewer than 2048 envs)."""
         f = self.L.macm_tdm_launch_flags(self.h)
         _abi.check(min(f, 0), "macm_tdm_launch_flags")
         return int(f)

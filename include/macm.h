@@ -279,6 +279,11 @@ typedef struct macm_world_info {
 #define MACM_LAUNCH_SPLIT_OBS 2 /* TDM (macm_tdm_launch_flags, ABI 9): the step writes pose snapshots and
                                    tdm_observe_snap observes them in a launch of its own (fewer than
                                    1024 envs, N <= 64; MACM_TDM_SPLIT_OBS overrides); same results */
+#define MACM_LAUNCH_TAIL_OBS 4  /* TDM trajectory rollouts (macm_tdm_rollout_traj): the tail observation,
+                                   each env's wave steps its K steps writing pose snapshots, then the
+                                   finished waves and observe-only waves observe the (step, env) rows
+                                   (fewer than 2048 envs, N <= 64, the launch resident at once;
+                                   MACM_TDM_TAIL_OBS overrides); same results */
 
 typedef struct macm_world macm_world;
 

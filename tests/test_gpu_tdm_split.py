@@ -5,7 +5,12 @@ counters) through every entry point that takes it: per-step launches, the overwr
 trajectory rollout in chunks (K = 19: chunks of 8, 8 and 3 on two snapshot halves), float32 and
 float64 observations, deaths, and envs that take the spill step (MACM_DEBUG_FORCE_SPILL). The fused
 form itself is pinned to the oracle by test_gpu_tdm.py; the split form is the default below 1024 envs,
-so those tests run it too. MACM_TDM_SPLIT_OBS=0/1 selects the form per call."""
+so those tests run it too. MACM_TDM_SPLIT_OBS=0/1 selects the form per call.
+
+The tail observation (round 6, flock_step_w64.hip TailObs; the default for trajectory rollouts below
+2048 envs): every env's wave steps its K steps writing write-through snapshots and publishing them, and
+the finished waves plus observe-only waves observe the (step, env) rows from sub-queues; the same bits
+as the fused form (test_tail_equals_fused; MACM_TDM_TAIL_OBS=0/1 and MACM_TDM_TAIL_WORKERS select)."""
 import numpy as np
 import pytest
 import torch
@@ -86,15 +91,62 @@ def test_split_equals_fused(monkeypatch, E, teams, kw, debug):
         assert b.spilled() > 0
 
 
-def test_split_is_the_default_below_1024_envs(monkeypatch):
-    """The launch form the library picks itself equals the forced fused form at 512 envs (C4's shard),
-    in the trajectory rollout the benchmark times."""
+def test_default_form_below_1024_envs(monkeypatch):
+    """The launch form the library picks itself (the tail observation for trajectory rollouts below 1024
+    envs) equals the forced fused form at 512 envs (C4's shard), in the trajectory rollout the
+    benchmark times."""
     E, teams, K = 512, [16, 16], 20
     monkeypatch.delenv("MACM_TDM_SPLIT_OBS", raising=False)
+    monkeypatch.delenv("MACM_TDM_TAIL_OBS", raising=False)
     a, b = pair(monkeypatch, E, teams, 77)
+    assert b.launch_flags() & _abi.LAUNCH_TAIL_OBS
     acts = actions(K, E, 32, 5)
-    ta = call(monkeypatch, False, a.rollout_traj, acts)
+    ta = call_env(monkeypatch, FUSED, a.rollout_traj, acts)
     tb = b.rollout_traj(acts)  # default
     for key in ta:
         assert torch.equal(ta[key], tb[key]), key
     same_state(a, b, "default form")
+
+
+def call_env(monkeypatch, env, fn, *args):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    r = fn(*args)
+    for k in env:
+        monkeypatch.delenv(k)
+    return r
+
+
+FUSED = {"MACM_TDM_SPLIT_OBS": "0", "MACM_TDM_TAIL_OBS": "0"}
+
+
+@pytest.mark.parametrize("E,teams,kw,debug,K,workers", [
+    (512, [16, 16], {}, 0, 20, None),                        # C4's shard, observe-only blocks
+    (512, [16, 16], {}, 0, 20, "0"),                         # the physics waves alone observe
+    (4096, [16, 16], {}, 0, 20, None),                       # C4 on one GPU: every slot an env
+    (37, [16, 16], {"obs_f64": True}, 0, 19, "3"),           # float64 obs (the pair tiles)
+    (24, [32, 32], {}, 0, 9, None),                          # N = 64
+    (64, [3, 3, 3], {"fresh_raycast": True}, 0, 33, None),   # >= 32 steps: the balanced env order
+    (16, [8, 8], {"world_width": 8.0, "world_height": 8.0}, 0, 25, None),  # deaths
+    (12, [16, 16], {}, _abi.DEBUG_FORCE_SPILL, 7, None),     # the spill step's snapshots
+])
+def test_tail_equals_fused(monkeypatch, E, teams, kw, debug, K, workers):
+    """The tail observation (flock_step_w64.hip TailObs): each env's wave steps its K steps writing
+    snapshots and publishing them; finished waves (and observe-only blocks) observe the (step, env)
+    rows. Bit for bit the fused form's trajectory, state and counters, twice in a row (the second
+    launch's tag and row counter)."""
+    N = sum(teams)
+    a, b = pair(monkeypatch, E, teams, 500 + E + N, debug, **kw)
+    acts = actions(2 * K, E, N, 3 * E + N)
+    env = {"MACM_TDM_SPLIT_OBS": "0", "MACM_TDM_TAIL_OBS": "1"}
+    if workers is not None:
+        env["MACM_TDM_TAIL_WORKERS"] = workers
+    for r in range(2):
+        ta = call_env(monkeypatch, FUSED, a.rollout_traj, acts[r * K:(r + 1) * K])
+        tb = call_env(monkeypatch, env, b.rollout_traj, acts[r * K:(r + 1) * K])
+        for key in ta:
+            assert torch.equal(ta[key], tb[key]), f"launch {r}: {key}"
+        same_state(a, b, f"launch {r}")
+    assert a.status() == 0 and b.status() == 0
+    if debug:
+        assert b.spilled() > 0
