@@ -805,8 +805,15 @@ __device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuf
     const int ne = env0(tl.q + 1) - env0(tl.q);
     const int nrows = tl.nsteps * ne;
     int c = 0;
-    if (lane == 0 && ne > 0)
-      c = (int)__hip_atomic_fetch_add(tail_counter(tl, tl.q), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && ne > 0) {
+      // a load first: the waves leaving find every sub-queue empty, and a load of an exhausted counter
+      // does not queue behind the other waves' atomics on it
+      unsigned long long* const ctr = tail_counter(tl, tl.q);
+      const unsigned long long seen = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c = seen * kTailChunk >= (unsigned long long)nrows
+              ? (int)seen
+              : (int)__hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     c = __builtin_amdgcn_readfirstlane(c);
     if (ne == 0 || (long long)c * kTailChunk >= nrows) {
       tl.q = tl.q + 1 == kTailQ ? 0 : tl.q + 1;
