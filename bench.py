@@ -405,6 +405,8 @@ def main():
             policy()
     rollout = args.launch == "rollout"
     traj = world_h.trajectory_buffers(K) if use_traj else None
+    if args.env == "tdm":  # the tail observation's snapshots for the longer of the two rollouts, ahead
+        world_h.reserve(max(W, K))
     traj_out = world_h.traj_outputs(traj) if use_traj else None  # the C-ABI struct, built outside the timing
     rname = ("macm_world_rollout" if args.env == "flock" else "macm_tdm_rollout") + ("_traj" if traj is not None else "")
     log(f"rank {rank}/{world}: {E} envs x {N} agents, warmup {W}, timed {K}, "

@@ -138,7 +138,7 @@ __device__ __forceinline__ float2 ld_wt(const float2* p) {
 }
 // The tail observation's control words (flock_step_w64.hip TailObs): per launch-tag parity kTailQ row
 // counters, each in a 128-B line of its own, then one ready word per env
-constexpr int kTailQ = 16, kTailLine = 16;
+constexpr int kTailQ = 64, kTailLine = 16;
 __host__ __device__ constexpr size_t tail_ctl_words(int n_envs) { return 2 * kTailQ * kTailLine + (size_t)n_envs; }
 
 __device__ __forceinline__ void st_wt4(float4* p, float4 v) {

@@ -773,17 +773,20 @@ __device__ __forceinline__ int write_new_pairs(int lane, unsigned long long newm
 struct TailObs {
   unsigned long long* ctl;  // tail_ctl_words(E) words (flock_common.hpp): row counters, then ready words
   unsigned int tag;         // this launch's tag (> 0); the ready word of env e holds tag << 32 | steps stored
-  int nsteps;               // K
-  int k;                    // physics: the step this call takes (steps 0 .. k - 1 are complete)
+  int nsteps;               // the steps observed in the tail: the launch's last nsteps (k0 = K - nsteps)
+  int k;                    // physics: the tail step this call takes (tail steps 0 .. k - 1 are complete;
+                            // negative: a step before the tail, observed in the step itself)
   bool worker;              // this call observes one claimed row instead of stepping
   bool more;                // worker: false once every row is taken (or a wait gave up)
   int q, left;              // worker: the sub-queue it claims from, sub-queues not yet found empty
   int r, r_end;             // worker: the rows of its current claim (sub-queue-local, step-major)
+  int nq;                   // sub-queues in use: min(kTailQ, blocks of the launch), each with a wave
 };
 // The rows are split into kTailQ sub-queues by env range (a single counter, one device-scope atomic
 // per row, serialised at ~9 ns per claim: 81,920 rows of C4 cost more than the observation saved); a
-// worker starts on sub-queue blockIdx % kTailQ and takes kTailChunk rows per claim, moving on when its
-// sub-queue is empty.
+// worker takes kTailChunk rows per claim from sub-queue blockIdx % kTailQ only and ends when it is
+// empty (moving on to the other sub-queues cost every leaving wave kTailQ accesses to the same few
+// lines: ~5 us per step at 4096 envs).
 constexpr int kTailChunk = 2;
 constexpr unsigned kTailSpins = 1u << 20;
 
@@ -796,7 +799,8 @@ __device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuf
                                              const TdmBuffers& TB, OT* obs, TailObs& tl, int lane, float2* s_c,
                                              float* s_ang, float4* stage, bool staged) {
   const int E = P.n_envs, N = P.n_agents;
-  auto env0 = [E](int q) { return (int)(((long long)E * q) / kTailQ); };
+  const int nq = tl.nq > 0 ? tl.nq : 1;
+  auto env0 = [E, nq](int q) { return (int)(((long long)E * q) / nq); };
   while (tl.r >= tl.r_end) {  // claim kTailChunk rows of the current sub-queue, else move on
     if (tl.left == 0) {
       tl.more = false;
@@ -816,7 +820,7 @@ __device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuf
     }
     c = __builtin_amdgcn_readfirstlane(c);
     if (ne == 0 || (long long)c * kTailChunk >= nrows) {
-      tl.q = tl.q + 1 == kTailQ ? 0 : tl.q + 1;
+      tl.q = tl.q + 1 == nq ? 0 : tl.q + 1;
       --tl.left;
       continue;
     }
@@ -826,6 +830,11 @@ __device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuf
   const int e0 = env0(tl.q), ne = env0(tl.q + 1) - e0;
   const int i = tl.r++;
   const int k = i / ne, e = e0 + (i - k * ne);
+  if (k >= tl.nsteps || e >= E || e < 0) {  // never: a row outside the launch ends the worker, not a fault
+    if (lane == 0) report_status(B, MACM_ST_HANDOFF);
+    tl.more = false;
+    return;
+  }
   int ok = 1;
   if (lane == 0) {
     ok = 0;
@@ -845,9 +854,10 @@ __device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuf
     tl.more = false;
     return;
   }
-  const size_t row = ((size_t)k * E + e) * N;  // the snapshot row: [K, E, N]
+  const size_t srow = ((size_t)k * E + e) * N;  // the snapshot row: [nsteps, E, N]
   float4 sn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (lane < N) sn = ld_wt4(TB.snap_out + row + lane);
+  if (lane < N) sn = ld_wt4(TB.snap_out + srow + lane);
+  const size_t row = ((size_t)(tl.k + k) * E + e) * N;  // the observation row of launch step k0 + k (tl.k: k0)
   s_c[lane] = make_float2(sn.x, sn.y);
   s_ang[lane] = sn.z;
   const unsigned long long livem = __ballot(lane < N && sn.w != 0.0f);
@@ -2213,6 +2223,7 @@ struct RolloutArgs {  // the kernel's only argument (kernarg offset 0)
   // ready words, and this launch's tag (0: off; blocks beyond n_envs then do not exist)
   unsigned long long* tail_ctl;
   unsigned int tail_tag;
+  int tail_k0;  // the first step observed in the tail (0: all); the steps before observe in the step
 };
 
 // [K, ...] row k of an output (trajectory form); NULL stays NULL
@@ -2273,7 +2284,19 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
   const bool phys = MODE != kTdm || (int)blockIdx.x < A0.P.n_envs;
   const int env = bal && phys ? (int)A0.B.sched[A0.sched_off + blockIdx.x] : (int)blockIdx.x;
   // (the body gets &tl itself in TDM, never a select of it, so that tl stays in registers; ctl NULL = off)
-  TailObs tl{A0.tail_tag ? A0.tail_ctl : nullptr, A0.tail_tag, nsteps, 0, false, true, (int)(blockIdx.x % kTailQ), kTailQ, 0, 0};
+  const int nq = gridDim.x < (unsigned)kTailQ ? (int)gridDim.x : kTailQ;
+  TailObs tl{};  // every field named: an initializer list in declaration order hid a misplaced field once
+  tl.ctl = A0.tail_tag ? A0.tail_ctl : nullptr;
+  tl.tag = A0.tail_tag;
+  tl.nsteps = nsteps - A0.tail_k0;
+  tl.k = 0;
+  tl.worker = false;
+  tl.more = true;
+  tl.q = (int)(blockIdx.x % nq);
+  tl.left = 1;
+  tl.r = 0;
+  tl.r_end = 0;
+  tl.nq = nq;
   const int ksteps = phys ? nsteps : 0;
   for (int k = 0; k < ksteps; ++k) {
     // each step reads its parameters from the kernel arguments afresh, through a pointer the
@@ -2293,7 +2316,10 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       TB.health_out = traj_row(TB.health_out, kr, EN);
       TB.alive_out = traj_row(TB.alive_out, kr, EN);
       TB.winner_out = traj_row(TB.winner_out, kr, (size_t)A.P.n_envs);
-      TB.snap_out = traj_row(TB.snap_out, kr, EN);
+      // the tail observation: snapshots of the last nsteps - tail_k0 steps only ([K - k0, E, N]); the
+      // steps before observe in the step (snap_out NULL)
+      TB.snap_out = A.tail_tag ? (k >= A.tail_k0 ? traj_row(TB.snap_out, (size_t)(k - A.tail_k0), EN) : nullptr)
+                               : traj_row(TB.snap_out, kr, EN);
     }
     const size_t abytes = MODE == kTdm ? 4 : 3;  // closed loop: uint8 actions per agent
     uint8_t* const pol_in = A.policy_act ? A.policy_act + kr * EN * abytes : nullptr;
@@ -2303,7 +2329,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
     // of its 128 VGPRs and kept 7 of them in scratch, re-read every step (rollout: 28 B per lane).
     int sl = (int)threadIdx.x;
     if constexpr (MODE == kTdm) asm volatile("" : "+v"(sl));
-    tl.k = k;
+    tl.k = k - A0.tail_k0;
     step_w64_body<MODE, NCAP, OT, SCAL>(A.P, A.B, A.TP, TB, A.cur ^ (k & 1),
                                         pol_in ? pol_in : static_cast<const unsigned char*>(A.actions) + (size_t)k * A.astride,
                                         obs, traj_row(A.nbr_out, kr, EN), traj_row(A.rew_out, kr, EN),
@@ -2331,13 +2357,14 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(4))) void env
       if (phys) {
         __builtin_amdgcn_s_waitcnt(0);
         if (threadIdx.x == 0)
-          __hip_atomic_store(tl.ctl + 2 * kTailQ * kTailLine + env, ((unsigned long long)tl.tag << 32) | (unsigned)nsteps,
+          __hip_atomic_store(tl.ctl + 2 * kTailQ * kTailLine + env, ((unsigned long long)tl.tag << 32) | (unsigned)tl.nsteps,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (blockIdx.x == 0 && threadIdx.x < kTailQ)  // the next launch's row counters (not this launch's)
         __hip_atomic_store(tl.ctl + (size_t)((((tl.tag + 1u) & 1u) * kTailQ + threadIdx.x) * kTailLine), 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       tl.worker = true;
+      tl.k = A0.tail_k0;  // the worker's row offset: tail step k is launch step k0 + k
       int sl = (int)threadIdx.x;
       asm volatile("" : "+v"(sl));
       while (tl.more)
@@ -2367,7 +2394,8 @@ template <int MODE, int NCAP, typename OT, bool SCAL = false>
 static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStream_t s, const StepParams& P,
                         const WorldBuffers& B, const TdmParams& TP, const TdmBuffers& TB, int cur, const void* actions,
                         void* obs, int32_t* nbr, float* rew, uint8_t* coll, uint8_t* done,
-                        unsigned long long* tail_ctl = nullptr, unsigned tail_tag = 0u, int tail_workers = 0) {
+                        unsigned long long* tail_ctl = nullptr, unsigned tail_tag = 0u, int tail_workers = 0,
+                        int tail_k0 = 0) {
   // astride == 0: closed loop, `actions` is the bots' action buffer (macm_world_rollout_bots)
   uint8_t* pol = astride == 0 ? static_cast<uint8_t*>(const_cast<void*>(actions)) : nullptr;
   const bool bal = B.sched && nsteps >= kRollBalanceMinSteps;
@@ -2380,7 +2408,7 @@ static void launch_roll(int nsteps, unsigned long long astride, int traj, hipStr
     if (hipPeekAtLastError() != hipSuccess) return;  // no rollout on a stale order (the caller reports it)
   }
   RolloutArgs<OT> A{P, B, TP, TB, actions, (OT*)obs, nbr, rew, coll, done, astride, cur, nsteps, pol, traj, 0,
-                    tail_ctl, tail_tag};
+                    tail_ctl, tail_tag, tail_tag ? tail_k0 : 0};
   const int blocks = P.n_envs + (tail_tag ? tail_workers : 0);
   hipLaunchKernelGGL((env_rollout_w64<MODE, NCAP, OT, SCAL>), dim3(blocks), dim3(W), 0, s, A);
 }
@@ -2419,22 +2447,23 @@ hipError_t launch_rollout_w64(const StepParams& P, const WorldBuffers& B, int cu
 hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
                                   uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride, int traj,
-                                  unsigned long long* tail_ctl, unsigned tail_tag, int tail_workers) {
+                                  unsigned long long* tail_ctl, unsigned tail_tag, int tail_workers,
+                                  int tail_k0) {
   const bool small = P.n_agents <= 32;
   if (obs_f64) {
     if (small)
       launch_roll<kTdm, 32, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                    nullptr, done, tail_ctl, tail_tag, tail_workers);
+                                    nullptr, done, tail_ctl, tail_tag, tail_workers, tail_k0);
     else
       launch_roll<kTdm, 64, double>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                    nullptr, done, tail_ctl, tail_tag, tail_workers);
+                                    nullptr, done, tail_ctl, tail_tag, tail_workers, tail_k0);
   } else {
     if (small)
       launch_roll<kTdm, 32, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                   nullptr, done, tail_ctl, tail_tag, tail_workers);
+                                   nullptr, done, tail_ctl, tail_tag, tail_workers, tail_k0);
     else
       launch_roll<kTdm, 64, float>(nsteps, astride, traj, s, P, B, TP, TB, cur, actions, obs, nullptr, nullptr,
-                                   nullptr, done, tail_ctl, tail_tag, tail_workers);
+                                   nullptr, done, tail_ctl, tail_tag, tail_workers, tail_k0);
   }
   return hipGetLastError();
 }

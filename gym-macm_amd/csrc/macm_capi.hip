@@ -38,7 +38,8 @@ hipError_t launch_tdm_step_w64(const StepParams& P, const WorldBuffers& B, const
 hipError_t launch_tdm_rollout_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                   const TdmBuffers& TB, int cur, const void* actions, void* obs, bool obs_f64,
                                   uint8_t* done, hipStream_t s, int nsteps, unsigned long long astride, int traj,
-                                  unsigned long long* tail_ctl = nullptr, unsigned tail_tag = 0u, int tail_workers = 0);
+                                  unsigned long long* tail_ctl = nullptr, unsigned tail_tag = 0u, int tail_workers = 0,
+                                  int tail_k0 = 0);
 int tdm_rollout_resident_blocks(int n_agents, bool obs_f64);
 hipError_t launch_tdm_init_w64(const StepParams& P, const WorldBuffers& B, const TdmParams& TP,
                                const TdmBuffers& TB, int cur, void* obs, bool obs_f64, const uint8_t* mask,
@@ -1470,6 +1471,10 @@ static int tdm_split_buffers(macm_tdm* w, size_t rows, hipStream_t s) {
     }
   }
   if (rows > w->snap_rows) {
+    // at least a whole chunk's rows at the first allocation (a warm-up rollout shorter than a chunk
+    // would otherwise leave the next rollout a synchronising reallocation)
+    const size_t chunk = (size_t)kTdmSplitChunk * w->P.n_envs;
+    if (rows < chunk) rows = chunk;
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipStreamSynchronize(w->obs_stream));
     if (w->snap) HIP_TRY(hipFree(w->snap));
@@ -1530,15 +1535,48 @@ static int tdm_tail_workers(macm_tdm* w) {
 // 13.3 -> 7.35 us, window 17.9 -> 15.3 us; 1536 envs window -3.4%), 2048 envs +4% and 4096 +24% in
 // the window (the chip is full of physics waves, so the observation waits for the tail)
 static constexpr int kTdmTailMaxEnvs = 2048;
+static constexpr int kTdmSnapMinSteps = 32;  // the tail observation's first snapshot allocation, in steps
 static bool tdm_tail_obs(macm_tdm* w) {
   const char* v = getenv("MACM_TDM_TAIL_OBS");
   if (v ? atoi(v) == 0 : w->P.n_envs >= kTdmTailMaxEnvs) return false;
   return tdm_tail_workers(w) >= 0;
 }
 
+// The steps observed in the tail: all below kTdmTailMaxEnvs; from there only the last
+// MACM_TDM_TAIL_STEPS (the earlier steps observe in the step, the fused form), so that the observation
+// of the last steps runs in the launch's tail while the heaviest envs finish
+static int tdm_tail_k0(const macm_tdm* w, int n_steps) {
+  int steps = w->P.n_envs >= kTdmTailMaxEnvs ? n_steps / 4 : n_steps;
+  if (const char* v = getenv("MACM_TDM_TAIL_STEPS")) steps = atoi(v);
+  if (steps < 1) steps = 1;
+  if (steps > n_steps) steps = n_steps;
+  return n_steps - steps;
+}
+
+// the tail observation's snapshot rows, grown rarely: a first allocation covers rollouts of up to
+// kTdmSnapMinSteps steps, so that a short warm-up rollout does not leave the next, longer one a
+// synchronising reallocation (macm_tdm_reserve sizes it ahead for longer ones)
+static int tdm_tail_snapshots(macm_tdm* w, size_t rows, hipStream_t s) {
+  if (rows <= w->tail_rows) return MACM_OK;
+  const size_t E = w->P.n_envs, N = w->P.n_agents;
+  const size_t want = rows > (size_t)kTdmSnapMinSteps * E ? rows : (size_t)kTdmSnapMinSteps * E;
+  HIP_TRY(hipStreamSynchronize(s));
+  if (w->tail_snap) HIP_TRY(hipFree(w->tail_snap));
+  w->tail_snap = nullptr;
+  w->tail_rows = 0;
+  if (hipMalloc(&w->tail_snap, want * N * sizeof(float4)) != hipSuccess) {
+    (void)hipGetLastError();
+    w->tail_snap = nullptr;
+    return fail(MACM_E_OOM, "hipMalloc (tail observation snapshots)");
+  }
+  w->tail_rows = want;
+  return MACM_OK;
+}
+
 static int tdm_rollout_tail(macm_tdm* w, const TdmBuffers& TB, const void* actions, int n_steps,
                             const macm_tdm_outputs* out, hipStream_t s, unsigned long long astride) {
-  const size_t E = w->P.n_envs, N = w->P.n_agents, rows = (size_t)n_steps * E;
+  const int k0 = tdm_tail_k0(w, n_steps);
+  const size_t E = w->P.n_envs, rows = (size_t)(n_steps - k0) * E;
   if (!w->tail_ctl) {
     if (hipMalloc(&w->tail_ctl, tail_ctl_words((int)E) * sizeof(unsigned long long)) != hipSuccess) {
       (void)hipGetLastError();
@@ -1548,23 +1586,12 @@ static int tdm_rollout_tail(macm_tdm* w, const TdmBuffers& TB, const void* actio
     HIP_TRY(hipMemsetAsync(w->tail_ctl, 0, tail_ctl_words((int)E) * sizeof(unsigned long long), s));
     w->tail_tag = 0;
   }
-  if (rows > w->tail_rows) {
-    HIP_TRY(hipStreamSynchronize(s));
-    if (w->tail_snap) HIP_TRY(hipFree(w->tail_snap));
-    w->tail_snap = nullptr;
-    w->tail_rows = 0;
-    if (hipMalloc(&w->tail_snap, rows * N * sizeof(float4)) != hipSuccess) {
-      (void)hipGetLastError();
-      w->tail_snap = nullptr;
-      return fail(MACM_E_OOM, "hipMalloc (tail observation snapshots)");
-    }
-    w->tail_rows = rows;
-  }
+  if (const int rc = tdm_tail_snapshots(w, rows, s)) return rc;
   if (++w->tail_tag == 0) w->tail_tag = 1;  // tags are > 0: a ready word of 0 never matches
   TdmBuffers TBt = TB;
   TBt.snap_out = w->tail_snap;
   HIP_TRY(launch_tdm_rollout_w64(w->P, w->B, w->TP, TBt, w->cur, actions, out->obs, w->cfg.obs_f64 != 0, out->done, s,
-                                 n_steps, astride, 1, w->tail_ctl, w->tail_tag, tdm_tail_workers(w)));
+                                 n_steps, astride, 1, w->tail_ctl, w->tail_tag, tdm_tail_workers(w), k0));
   if (n_steps & 1) w->cur ^= 1;
   return MACM_OK;
 }
@@ -1812,6 +1839,14 @@ int macm_tdm_launch_flags(const macm_tdm* w) {
   if (!w) return fail(MACM_E_INVALID, "tdm is NULL");
   return (tdm_split_obs(w) ? MACM_LAUNCH_SPLIT_OBS : 0) |
          (tdm_tail_obs(const_cast<macm_tdm*>(w)) ? MACM_LAUNCH_TAIL_OBS : 0);
+}
+
+int macm_tdm_reserve(macm_tdm* w, int32_t n_steps, void* stream) {
+  if (!w || n_steps < 0) return fail(MACM_E_INVALID, "tdm is NULL or n_steps < 0");
+  DeviceGuard g(w->device);
+  if (!tdm_tail_obs(w) || n_steps == 0) return MACM_OK;
+  const int k0 = tdm_tail_k0(w, n_steps);
+  return tdm_tail_snapshots(w, (size_t)(n_steps - k0) * w->P.n_envs, (hipStream_t)stream);
 }
 
 int macm_tdm_spilled(macm_tdm* w, int64_t* env_steps, void* stream) {

@@ -231,6 +231,7 @@ SIGNATURES = {
     "macm_tdm_counters": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_tdm_spilled": (c_int, [c_void_p, POINTER(c_int64), c_void_p]),
     "macm_tdm_launch_flags": (c_int, [c_void_p]),
+    "macm_tdm_reserve": (c_int, [c_void_p, c_int32, c_void_p]),
     "macm_tdm_set_debug": (c_int, [c_void_p, c_int32]),
     "macm_bots_flock": (c_int, [c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
     "macm_bots_combat": (c_int, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_void_p, c_void_p]),

@@ -321,6 +321,11 @@ class TdmWorld:
         _abi.check(min(f, 0), "macm_tdm_launch_flags")
         return int(f)
 
+    def reserve(self, n_steps: int) -> None:
+        """Allocate ahead what trajectory rollouts of up to n_steps steps need (macm_tdm_reserve: the tail
+        observation's snapshots), so that the rollout itself does not reallocate."""
+        _abi.check(self.L.macm_tdm_reserve(self.h, int(n_steps), self._stream()), "macm_tdm_reserve")
+
     def set_debug(self, flags: int) -> None:
         """Test hooks (macm_tdm_set_debug): _abi.DEBUG_FORCE_SPILL sends every env through the spill
         step; DEBUG_SPILL_POOL | slots << 8 shares that many working-set slots; DEBUG_SPILL_FAIL makes

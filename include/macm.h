@@ -521,6 +521,11 @@ int macm_tdm_spilled(macm_tdm* w, int64_t* env_steps, void* stream);
 /* MACM_LAUNCH_* of the next macm_tdm_step / rollout (not the closed loop) (ABI 9). */
 int macm_tdm_launch_flags(const macm_tdm* w);
 
+/* Allocates ahead what trajectory rollouts of up to n_steps steps need (the tail observation's pose
+ * snapshots, MACM_LAUNCH_TAIL_OBS), so that the rollout itself does not reallocate (a reallocation
+ * synchronises its stream); optional (a rollout grows what it needs). Synchronises `stream`. */
+int macm_tdm_reserve(macm_tdm* w, int32_t n_steps, void* stream);
+
 /* Test hooks: MACM_DEBUG_FORCE_SPILL, MACM_DEBUG_SPILL_POOL (ABI 6). */
 int macm_tdm_set_debug(macm_tdm* w, int32_t flags);
 

@@ -121,6 +121,8 @@ FUSED = {"MACM_TDM_SPLIT_OBS": "0", "MACM_TDM_TAIL_OBS": "0"}
 
 
 @pytest.mark.parametrize("E,teams,kw,debug,K,workers", [
+    (4096, [16, 16], {}, 0, 20, "steps=5"),                  # full chip: the last 5 steps in the tail
+    (64, [16, 16], {}, 0, 33, "steps=3"),                    # the last 3 of 33 steps (balanced order)
     (512, [16, 16], {}, 0, 20, None),                        # C4's shard, observe-only blocks
     (512, [16, 16], {}, 0, 20, "0"),                         # the physics waves alone observe
     (4096, [16, 16], {}, 0, 20, None),                       # C4 on one GPU: every slot an env
@@ -139,7 +141,9 @@ def test_tail_equals_fused(monkeypatch, E, teams, kw, debug, K, workers):
     a, b = pair(monkeypatch, E, teams, 500 + E + N, debug, **kw)
     acts = actions(2 * K, E, N, 3 * E + N)
     env = {"MACM_TDM_SPLIT_OBS": "0", "MACM_TDM_TAIL_OBS": "1"}
-    if workers is not None:
+    if workers is not None and workers.startswith("steps="):
+        env["MACM_TDM_TAIL_STEPS"] = workers[6:]
+    elif workers is not None:
         env["MACM_TDM_TAIL_WORKERS"] = workers
     for r in range(2):
         ta = call_env(monkeypatch, FUSED, a.rollout_traj, acts[r * K:(r + 1) * K])
@@ -150,3 +154,19 @@ def test_tail_equals_fused(monkeypatch, E, teams, kw, debug, K, workers):
     assert a.status() == 0 and b.status() == 0
     if debug:
         assert b.spilled() > 0
+
+
+def test_reserve_then_rollouts(monkeypatch):
+    """macm_tdm_reserve sizes the tail observation's snapshots ahead; rollouts shorter and longer than
+    the reservation (the latter grows it) still equal the fused form."""
+    E, teams = 64, [16, 16]
+    a, b = pair(monkeypatch, E, teams, 31)
+    b.reserve(40)
+    acts = actions(70, E, 32, 8)
+    for lo, hi in ((0, 5), (5, 45), (45, 70)):
+        ta = call_env(monkeypatch, FUSED, a.rollout_traj, acts[lo:hi])
+        tb = b.rollout_traj(acts[lo:hi])
+        for key in ta:
+            assert torch.equal(ta[key], tb[key]), f"steps {lo}..{hi}: {key}"
+    same_state(a, b, "after the rollouts")
+    assert b.launch_flags() & _abi.LAUNCH_TAIL_OBS
