@@ -866,7 +866,7 @@ __device__ __forceinline__ void tdm_tail_row(const StepParams& P, const WorldBuf
   OT* const obs_r = obs ? obs + slots * 4 : nullptr;
   uint8_t* const mask_r = TB.mask_out ? TB.mask_out + slots : nullptr;
   if constexpr (sizeof(OT) == 4) {
-    if (staged) tdm_obs_rowblocks<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang, stage);
+    if (staged) tdm_obs_rowblocks<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang, stage, true);
     else tdm_obs_pairs<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang);
   } else {
     tdm_obs_pairs<OT>(obs_r, mask_r, N, lane, livem, TP, s_c, s_ang);

@@ -181,10 +181,17 @@ __host__ __device__ constexpr int tdm_obs_rb_stage_bytes(int N) { return 512 * (
 template <typename OT>
 __device__ __forceinline__ void tdm_obs_rowblocks(OT* __restrict__ obs, uint8_t* __restrict__ mask, int N, int lane,
                                                   unsigned long long livem, const TdmParams& TP, const float2* sc,
-                                                  const float* sa, float4* stage) {
+                                                  const float* sa, float4* stage, bool mask_pieces = false) {
   static_assert(sizeof(OT) == 4, "the stage keeps the finished float32 slots");
   const int S = N - 1, nb = (N + 7) >> 3;
   const int a = lane >> 3, b = lane & 7;
+  // mask_pieces: the mask in 16-B pieces after the slots (each byte alive(i) & alive(j), from livem
+  // alone) when the env's [N, N-1] mask block is a whole number of aligned pieces (N = 32: 62 lanes, one
+  // store each) instead of a byte store per slot beside each slot's store (the byte stores are 3% of
+  // C4's step). Measured (profiles/r06/abtests/mask_pieces/): the 512-env shard -2.1%, 4096 envs
+  // +0.5 / +1.3% (window / steady), so the tail observation's rows take it and the fused step does not.
+  const bool mfast = mask_pieces && mask && ((N * S) & 15) == 0 && (reinterpret_cast<uintptr_t>(mask) & 15) == 0;
+  uint8_t* const mk = mfast ? nullptr : mask;
   int dr = 0, rem = lane & 31;  // diagonal pair `lane & 31` (< 28) of a block: row-major over dr < dc
   while (dr < 7 && rem >= 7 - dr) {
     rem -= 7 - dr;
@@ -214,7 +221,7 @@ __device__ __forceinline__ void tdm_obs_rowblocks(OT* __restrict__ obs, uint8_t*
         }
         const size_t s1 = (size_t)i * S + (j - 1);
         if (obs) store4<OT>(obs + s1 * 4, r, t1, p1, ty);
-        if (mask) mask[s1] = m ? 1 : 0;
+        if (mk) mk[s1] = m ? 1 : 0;
         // row j = 8J + b, slot i, as store4 would write it (p2 = -p1 exactly); lanes contiguous
         stage[soff(J) + 8 * i + b] = make_float4((float)r, (float)t2, (float)(-p1), (float)ty);
       }
@@ -223,7 +230,7 @@ __device__ __forceinline__ void tdm_obs_rowblocks(OT* __restrict__ obs, uint8_t*
     // tiles do): block R + 1's own pairs are written one block early
     if ((R & 1) == 0) {
       const int D = R + (lane >> 5), k = lane & 31;
-      if (k < 28 && D < nb && 8 * D + dc < N) tdm_obs_pair<OT>(obs, mask, S, 8 * D + dr, 8 * D + dc, livem, TP, sc, sa);
+      if (k < 28 && D < nb && 8 * D + dc < N) tdm_obs_pair<OT>(obs, mk, S, 8 * D + dr, 8 * D + dc, livem, TP, sc, sa);
     }
     if (R > 0) {
       wave_lds_sync();  // the stage entries of block R (other lanes, earlier blocks)
@@ -235,9 +242,25 @@ __device__ __forceinline__ void tdm_obs_rowblocks(OT* __restrict__ obs, uint8_t*
         if (j < N) {
           const size_t s2 = (size_t)j * S + o;
           if (obs) *reinterpret_cast<float4*>(obs + s2 * 4) = stage[soff(R) + e];
-          if (mask) mask[s2] = ((livem >> o) & (livem >> j) & 1ull) ? 1 : 0;
+          if (mk) mk[s2] = ((livem >> o) & (livem >> j) & 1ull) ? 1 : 0;
         }
       }
+    }
+  }
+  if (mfast) {
+    for (int q = 16 * lane; q < N * S; q += 16 * 64) {
+      int i = q / S, k = q - i * S;  // byte q: row i, slot k (the other agent k < i ? k : k + 1)
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int j = k < i ? k : k + 1;
+        w[t >> 2] |= (uint32_t)((livem >> i) & (livem >> j) & 1ull) << (8 * (t & 3));
+        if (++k == S) {
+          k = 0;
+          ++i;
+        }
+      }
+      *reinterpret_cast<uint4*>(mask + q) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
 }
